@@ -1,0 +1,182 @@
+/*
+ * owrx_amd.h -- C ABI of libowrx_amd.so, the MI355X-native IQ backend for OpenWebRX.
+ *
+ * Drop-in boundary.  In the reference the hot path ends at the pycsdr extension
+ * (pycsdr.modules / pycsdr.types, C++ csdr underneath, not in /root/reference); its Python
+ * callers are csdr/chain/{fft,selector,analog,clientaudio}.py, owrx/fft.py and owrx/dsp.py.
+ * This library is what a pycsdr-compatible binding calls instead (the in-tree binding is the
+ * ctypes package `pycsdr/` + `openwebrx_amd/`; INTEGRATION.md shows the stubs).  Plain
+ * pointers and sizes only.
+ *
+ * Return codes: >= 0 ok (or a count), negative errno-style values below; the binding maps
+ * OWRX_EINVAL to ValueError (the reference's format/parameter error convention,
+ * csdr/chain/__init__.py:60-84) and the rest to OSError.  owrx_last_error() returns the
+ * thread's last message.
+ *
+ * Threading: one engine per GPU; every call on an engine is serialised internally, setters may
+ * be called from any thread and take effect at the next processed block (owrx/dsp.py:538-562
+ * wires property callbacks from arbitrary threads).
+ */
+#ifndef OWRX_AMD_H
+#define OWRX_AMD_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OWRX_OK 0
+#define OWRX_EIO (-5)       /* HIP runtime failure (engine marked failed) */
+#define OWRX_EAGAIN (-11)   /* nothing to read yet */
+#define OWRX_ENOMEM (-12)
+#define OWRX_EINVAL (-22)
+#define OWRX_ENOSPC (-28)   /* output ring overrun (oldest data dropped) */
+#define OWRX_ENODEV (-19)   /* no gfx950 device */
+
+#define OWRX_DEMOD_NFM 0
+#define OWRX_DEMOD_AM 1
+#define OWRX_DEMOD_SSB 2    /* RealPart: usb / lsb / cw (owrx/dsp.py:617-619) */
+
+#define OWRX_OUT_S16 0      /* Convert(FLOAT, SHORT) */
+#define OWRX_OUT_ADPCM 1    /* Convert + AdpcmEncoder(sync=True) */
+#define OWRX_OUT_F32 2      /* raw float audio (no Convert) */
+
+#define OWRX_AGC_FAST 0
+#define OWRX_AGC_SLOW 1
+#define OWRX_AGC_MID 2
+#define OWRX_AGC_LAGGY 3
+
+typedef struct owrx_engine owrx_engine;
+
+const char* owrx_version(void);               /* "0.18.x-amd" (owrx/feature.py:213-221 gate) */
+const char* owrx_last_error(void);
+int owrx_device_count(void);                   /* visible HIP devices, or OWRX_ENODEV */
+
+/* ---- engine: one wideband IQ stream on one GPU ------------------------------------------
+ * Replaces the wideband pycsdr Buffer(COMPLEX_FLOAT) fed by TcpSource
+ * (owrx/source/__init__.py:307-330) and the per-module native threads. */
+int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_engine** out);
+int owrx_engine_destroy(owrx_engine* e);
+/* samples that must precede a block handed to owrx_process_device (filter/FFT history) */
+int64_t owrx_engine_history(owrx_engine* e);
+int64_t owrx_engine_max_block(owrx_engine* e);
+
+/* Host cf32 (interleaved little-endian float I,Q) -> device; processes whole blocks.
+ * Equivalent of Writer.write() on the wideband Buffer. */
+int owrx_push_iq(owrx_engine* e, const float* iq_cf32, int64_t nsamples);
+/* Device-resident cf32 block; iq_dev[-history, 0) must hold the previous samples of the stream
+ * (e.g. a contiguous HBM recording, or an RCCL-broadcast window).  Zero-copy. */
+int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t nsamples);
+/* Device window slot for the next block (write there, e.g. with ncclBroadcast), then commit. */
+int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity);
+int owrx_commit(owrx_engine* e, int64_t nsamples);
+/* Waits for all enqueued device work and drains outputs into the host rings. */
+int owrx_sync(owrx_engine* e);
+
+/* ---- waterfall: FftChain (csdr/chain/fft.py:25-96) --------------------------------------
+ * Fft(size=fft_size, every_n_samples) -> LogAveragePower(add_db, fft_size, avg_number) or
+ * LogPower(add_db) when avg_number == 0 (fft.py:18-22) -> FftSwap -> FftAdpcm if compression.
+ * fft_size: power of two, 256..16384 (owrx/controllers/settings/general.py:181). */
+int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int avg_number,
+                          float add_db, int adpcm, int* handle);
+/* FftChain._setBlockSize / setFftAverages / setCompression (fft.py:51-55, 11-16, 87-96) */
+int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_number,
+                       int adpcm);
+int owrx_waterfall_destroy(owrx_engine* e, int handle);
+/* bytes of one output row: (fft_size+10)/2 with ADPCM, 4*fft_size without */
+int64_t owrx_waterfall_row_bytes(owrx_engine* e, int handle);
+/* copies whole rows (<= max_bytes) from the row ring; 0 when none; Reader.read() of the
+ * spectrum buffer (owrx/fft.py:70-73) */
+int64_t owrx_waterfall_read(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes);
+
+/* ---- client demod chain: ClientDemodulatorChain (owrx/dsp.py:39-72) ----------------------
+ * [Selector(Shift, FirDecimate, [FractionalDecimator], [Bandpass], Squelch),
+ *  NFm | Am | Ssb, ClientAudioChain(Convert, [AdpcmEncoder(sync=True)])]. */
+typedef struct {
+    float   shift_rate;      /* Shift.setRate(-offset/inRate)      selector.py:132-140 */
+    int32_t decimation;      /* FirDecimate(decimation, transition, cutoff)  selector.py:29 */
+    float   transition;
+    float   cutoff;
+    double  frac_rate;       /* FractionalDecimator rate; 1.0 => absent   selector.py:32-33 */
+    int32_t bandpass;        /* 1 => Bandpass inserted (both cuts set)    selector.py:159-166 */
+    float   bp_low;          /* normalised to the output rate */
+    float   bp_high;
+    float   bp_transition;   /* 320/outputRate                            selector.py:115-117 */
+    int32_t sq_length;       /* Squelch(...)                              selector.py:119-130 */
+    int32_t sq_decimation;
+    int32_t sq_hang;
+    int32_t sq_flush;
+    int32_t sq_report;
+    float   sq_level;        /* linear power, setSquelchLevel(10^(dB/10)) */
+    int32_t demod;           /* OWRX_DEMOD_* */
+    int32_t agc_profile;     /* OWRX_AGC_* */
+    float   agc_initial_gain;/* < 0 => profile default; Am: 200 (analog.py:15) */
+    float   agc_max_gain;    /* < 0 => profile default; NFm: 3 (analog.py:40) */
+    int32_t audio_rate;      /* NfmDeemphasis(sampleRate) (analog.py:45) */
+    int32_t output;          /* OWRX_OUT_* */
+} owrx_chain_params;
+
+int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle);
+int owrx_chain_destroy(owrx_engine* e, int handle);
+int owrx_chain_set_shift_rate(owrx_engine* e, int handle, float rate);
+int owrx_chain_set_bandpass(owrx_engine* e, int handle, int enabled, float low, float high);
+int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level);
+/* audio bytes (s16 LE / ADPCM stream / f32) produced so far; Reader.read() of the audio
+ * buffer (owrx/dsp.py:846-863) */
+int64_t owrx_chain_read_audio(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes);
+/* Squelch power writer values (owrx/connection.py:483-489) */
+int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t max_values);
+/* absolute stream sample index of the chain's sample 0 (aligned to the decimation grid) */
+int64_t owrx_chain_origin(owrx_engine* e, int handle);
+
+/* ---- parity taps (tests): per-chain stage outputs captured while debug is enabled --------
+ * stage 0: Selector DDC output (cf32), 1: after FractionalDecimator (cf32),
+ * 2: after Bandpass (cf32), 3: after Squelch (cf32), 4: demod output before AGC (f32),
+ * 5: AGC output (f32). */
+int owrx_set_debug(owrx_engine* e, int enable);
+int64_t owrx_chain_read_debug(owrx_engine* e, int handle, int stage, void* dst,
+                              int64_t max_bytes);
+
+typedef struct {
+    int64_t samples_in;        /* IQ samples processed */
+    int64_t blocks;            /* process calls */
+    int64_t ddc_outputs;       /* sum over chains */
+    int64_t waterfall_rows;
+    int64_t audio_bytes;
+    int64_t overruns;          /* host output ring drops */
+    double  gpu_ms_ddc;        /* HIP-event time of the DDC kernels (when timing enabled) */
+    double  gpu_ms_waterfall;
+    double  gpu_ms_post;
+    int64_t ddc_launches;
+    int64_t waterfall_launches;
+} owrx_stats;
+int owrx_get_stats(owrx_engine* e, owrx_stats* s);
+/* 1 => record HIP events around each kernel group on the engine's streams */
+int owrx_set_timing(owrx_engine* e, int enable);
+
+/* ---- single-module runners (pycsdr module granularity, stateful, host buffers) -----------
+ * Used by pycsdr.modules classes that run outside a fused chain and by the per-module parity
+ * tests.  type: OWRX_MOD_*; params as documented per type; returns outputs produced. */
+#define OWRX_MOD_FMDEMOD 1
+#define OWRX_MOD_AMDEMOD 2
+#define OWRX_MOD_REALPART 3
+#define OWRX_MOD_LIMIT 4          /* p0 = max amplitude */
+#define OWRX_MOD_DCBLOCK 5
+#define OWRX_MOD_DEEMPH 6         /* p0 = alpha */
+#define OWRX_MOD_AGC 7            /* p0 profile, p1 initial gain (<0 default), p2 max gain */
+#define OWRX_MOD_CONVERT_F_S16 8
+#define OWRX_MOD_ADPCM 9          /* p0 = sync (0/1); input s16 */
+#define OWRX_MOD_FFTSWAP 10       /* p0 = fft size; input f32 rows */
+#define OWRX_MOD_FFTADPCM 11      /* p0 = fft size; input f32 rows (already swapped) */
+typedef struct owrx_module owrx_module;
+int owrx_module_create(int device, int type, double p0, double p1, double p2,
+                       owrx_module** out);
+int owrx_module_destroy(owrx_module* m);
+/* in: n input items (cf32 for demods, f32, s16 for ADPCM); out: capacity in bytes */
+int64_t owrx_module_process(owrx_module* m, const void* in, int64_t n, void* out,
+                            int64_t out_cap_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

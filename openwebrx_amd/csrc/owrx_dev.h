@@ -1,0 +1,184 @@
+// owrx_dev.h -- device-side types and per-sample DSP steps shared by the fused kernels
+// (kernels_*.hip) and the single-module runners (modules.hip).
+//
+// Semantics follow the csdr modules named in each comment (call sites in the reference's
+// csdr/chain/*.py); the fp32 operation order of every serial step is identical to
+// oracle/csdr_oracle.c, with FP contraction disabled, so identical inputs give identical bits.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define OWRX_DEV __device__ __forceinline__
+
+namespace owrx {
+
+constexpr int kWave = 64;
+constexpr int kFdPoints = 12;     // FractionalDecimator Lagrange points
+constexpr int kFdHist = 16;       // DDC outputs kept for the interpolator window
+constexpr int kBpHist = 256;      // Bandpass history (taps - 1 <= 255)
+constexpr int kAdpcmSyncPeriod = 1001;  // data bytes per "SYNC" frame (AudioEngine.js:449-491)
+constexpr float kFmK = 0.340447f; // fmdemod_quadri_K
+
+struct AgcParams {
+    float reference, attack, decay, max_gain, initial_gain;
+    int hang_time;
+};
+struct AgcState {
+    float gain;
+    int hang;
+};
+struct AdpcmState {
+    int index;
+    int pred;
+};
+
+OWRX_DEV float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// ---- serial / per-sample steps (bit-exact with the oracle) --------------------------------
+
+// FmDemod (csdr/chain/analog.py:43), quadri-correlator.
+OWRX_DEV float fm_step(float2 x, float2 last) {
+#pragma clang fp contract(off)
+    float dq = x.y - last.y;
+    float di = x.x - last.x;
+    float a = x.x * dq;
+    float b = x.y * di;
+    float num = a - b;
+    float ii = x.x * x.x;
+    float qq = x.y * x.y;
+    float den = ii + qq;
+    float kn = kFmK * num;
+    return (den != 0.0f) ? kn / den : 0.0f;
+}
+
+// AmDemod (analog.py:16)
+OWRX_DEV float am_step(float2 x) {
+#pragma clang fp contract(off)
+    float ii = x.x * x.x;
+    float qq = x.y * x.y;
+    return __fsqrt_rn(ii + qq);
+}
+
+// Limit (analog.py:44)
+OWRX_DEV float limit_step(float v, float m) {
+    if (v > m) v = m;
+    if (v < -m) v = -m;
+    return v;
+}
+
+// NfmDeemphasis (analog.py:45): y = alpha*x + (1-alpha)*y_prev
+OWRX_DEV float deemph_step(float x, float alpha, float beta, float& yp) {
+#pragma clang fp contract(off)
+    float a = alpha * x;
+    float b = beta * yp;
+    float y = a + b;
+    yp = y;
+    return y;
+}
+
+// DcBlock (analog.py:17): y = x - x_prev + 0.999*y_prev
+OWRX_DEV float dcblock_step(float x, float& xp, float& yp) {
+#pragma clang fp contract(off)
+    const float a = 0.999f;
+    float d = x - xp;
+    float f = a * yp;
+    float y = d + f;
+    xp = x;
+    yp = y;
+    return y;
+}
+
+// Agc(FLOAT) (analog.py:13-15, 38-40, 121-122)
+OWRX_DEV float agc_step(float x, const AgcParams& p, AgcState& s) {
+#pragma clang fp contract(off)
+    float a = fabsf(x);
+    if (a > 0.0f) {
+        float target = p.reference / a;
+        float err = target - s.gain;
+        float dg;
+        if (err < 0.0f) {
+            dg = err * p.attack;
+            s.hang = p.hang_time;
+        } else if (s.hang > 0) {
+            s.hang--;
+            dg = 0.0f;
+        } else {
+            dg = err * p.decay;
+        }
+        float g = s.gain + dg;
+        if (g < 0.0f) g = 0.0f;
+        if (g > p.max_gain) g = p.max_gain;
+        s.gain = g;
+    }
+    return s.gain * x;
+}
+
+OWRX_DEV int16_t f_to_s16(float v) {
+    if (v != v) return 0;
+    if (v > 32767.0f) v = 32767.0f;
+    if (v < -32768.0f) v = -32768.0f;
+    return (int16_t)v;
+}
+
+// Convert(FLOAT, SHORT) (clientaudio.py:18)
+OWRX_DEV int16_t convert_s16(float x) {
+#pragma clang fp contract(off)
+    float v = x * 32767.0f;
+    return f_to_s16(v);
+}
+
+// FftAdpcm quantiser: (short)(dB*100) (csdr/chain/fft.py:43-45, htdocs/openwebrx.js:1118-1126)
+OWRX_DEV int16_t db_to_s16(float db) {
+#pragma clang fp contract(off)
+    float t = db * 100.0f;
+    return f_to_s16(t);
+}
+
+__constant__ static const int8_t kAdpcmIndex[16] = {-1, -1, -1, -1, 2, 4, 6, 8,
+                                                     -1, -1, -1, -1, 2, 4, 6, 8};
+__constant__ static const int16_t kAdpcmStep[89] = {
+    7,     8,     9,     10,    11,    12,    13,    14,    16,    17,    19,    21,    23,
+    25,    28,    31,    34,    37,    41,    45,    50,    55,    60,    66,    73,    80,
+    88,    97,    107,   118,   130,   143,   157,   173,   190,   209,   230,   253,   279,
+    307,   337,   371,   408,   449,   494,   544,   598,   658,   724,   796,   876,   963,
+    1060,  1166,  1282,  1411,  1552,  1707,  1878,  2066,  2272,  2499,  2749,  3024,  3327,
+    3660,  4026,  4428,  4871,  5358,  5894,  6484,  7132,  7845,  8630,  9493,  10442, 11487,
+    12635, 13899, 15289, 16818, 18500, 20350, 22385, 24623, 27086, 29794, 32767};
+
+// IMA ADPCM encode of one sample (AdpcmEncoder / FftAdpcm); decoder in
+// htdocs/lib/AudioEngine.js:493-509.
+OWRX_DEV int adpcm_encode(AdpcmState& s, int sample) {
+    int step = kAdpcmStep[s.index];
+    int diff = sample - s.pred;
+    int code = 0;
+    if (diff < 0) {
+        code = 8;
+        diff = -diff;
+    }
+    int ts = step;
+    if (diff >= ts) {
+        code |= 4;
+        diff -= ts;
+    }
+    ts >>= 1;
+    if (diff >= ts) {
+        code |= 2;
+        diff -= ts;
+    }
+    ts >>= 1;
+    if (diff >= ts) code |= 1;
+    int dq = step >> 3;
+    if (code & 4) dq += step;
+    if (code & 2) dq += step >> 1;
+    if (code & 1) dq += step >> 2;
+    int p = s.pred + ((code & 8) ? -dq : dq);
+    p = p > 32767 ? 32767 : (p < -32768 ? -32768 : p);
+    s.pred = p;
+    int idx = s.index + kAdpcmIndex[code];
+    s.index = idx < 0 ? 0 : (idx > 88 ? 88 : idx);
+    return code;
+}
+
+}  // namespace owrx

@@ -1,0 +1,104 @@
+// owrx_types.h -- descriptors exchanged between the host engine (engine.hip) and the
+// kernels.  Plain structs, identical layout on host and device.
+#pragma once
+#include <stdint.h>
+#include "owrx_dev.h"
+
+namespace owrx {
+
+// ---- waterfall ---------------------------------------------------------------------------
+// One workgroup computes sum_f |FFT(w * x_f)|^2 over `nframes` consecutive frames of one row.
+struct WfGroup {
+    int64_t start;    // absolute stream index of the first frame
+    int32_t nframes;
+    int32_t hop;
+};
+// One row touched by a finalize launch: sums its groups (in order) onto the carry.
+struct WfRow {
+    int32_t first_group;
+    int32_t ngroups;
+    int32_t use_carry;   // add the carried accumulator first
+    int32_t complete;    // emit the row (else store the sum into the carry)
+    int32_t out_index;   // row slot in the output staging buffer
+    int32_t pad;
+};
+
+// ---- DDC (Shift + FirDecimate, fused, all chains of one (D, taps) group) ----------------
+struct DdcChain {
+    uint64_t rate_fx;    // shift rate in 2^-64 turns per sample
+    float2 wD;           // exp(j 2 pi D rate): rotator step between consecutive outputs
+    int64_t n0;          // phase(n) = P0 + (n - n0 + 1) * rate_fx   (absolute n)
+    uint64_t P0;
+};
+
+// ---- post-decimation chain state (device, persistent) -----------------------------------
+struct ChainState {
+    int64_t ddc_count;     // DDC outputs consumed so far (chain-local)
+    int64_t fd_next;       // next FractionalDecimator output index
+    int64_t fd_count;      // samples emitted by FractionalDecimator (or passthrough) so far
+    int32_t sq_pending;    // samples waiting for a full squelch block
+    int32_t hang_ctr;
+    int32_t flush_ctr;
+    int32_t has_left;      // ADPCM: one s16 sample waiting for its pair
+    int64_t sq_blocks;
+    int64_t adpcm_bytes;   // data bytes emitted (sync period bookkeeping)
+    float2 fm_last;
+    float deemph_y;
+    float dc_xp, dc_yp;
+    AgcState agc;
+    AdpcmState adpcm;
+    int32_t left_sample;
+    int32_t pad;
+};
+
+// Static + per-step description of one chain for the post kernel.
+struct ChainPost {
+    // configuration
+    int32_t demod;         // OWRX_DEMOD_*
+    int32_t output;        // OWRX_OUT_*
+    int32_t frac_enabled;
+    int32_t bp_ntaps;      // 0 => no bandpass
+    double frac_rate;
+    const float2* bp_taps;
+    int32_t sq_len, sq_dec, sq_hang, sq_flush, sq_report;
+    float sq_level;
+    float deemph_alpha, deemph_beta;
+    AgcParams agc;
+    // buffers
+    ChainState* state;
+    float2* ddc_buf;       // [kFdHist + cap]
+    float2* fd_buf;        // [kBpHist + cap]
+    float2* sq_buf;        // [sq_len + cap]
+    float* dem_buf;        // [cap + sq_len]
+    // this step
+    const float2* partial; // group partial sums [nseg][group_chains][nk]
+    int32_t nseg;
+    int32_t group_chains;
+    int32_t chain_in_group;
+    int32_t nk;            // group outputs this step
+    int64_t k_begin;       // absolute output index of partial column 0
+    int64_t k_first;       // absolute output index of this chain's output 0
+    // outputs
+    uint8_t* out;          // staging slot
+    int64_t out_cap;
+    float* smeter;         // staging slot
+    int32_t smeter_cap;
+    int32_t debug;         // capture stage outputs
+    float2* dbg_ddc;       // staging slots (only when debug)
+    float2* dbg_fd;
+    float2* dbg_bp;
+    float2* dbg_sq;
+    float* dbg_dem;
+    float* dbg_agc;
+    int64_t dbg_cap;
+};
+
+// Per-chain counters written by the post kernel for the host.
+struct ChainCounts {
+    int64_t out_bytes;
+    int32_t smeter;
+    int32_t pad;
+    int64_t n_ddc, n_fd, n_bp, n_sq;  // debug stage counts
+};
+
+}  // namespace owrx

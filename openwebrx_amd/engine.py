@@ -1,0 +1,208 @@
+"""Python handles over the C ABI: one Engine per GPU / wideband stream, Waterfall
+(FftChain) and Chain (ClientDemodulatorChain) objects attached to it.  Thin: every call goes
+straight to libowrx_amd.so."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+STAGE_DDC, STAGE_FRAC, STAGE_BANDPASS, STAGE_SQUELCH, STAGE_DEMOD, STAGE_AGC = range(6)
+_STAGE_DTYPE = {0: np.complex64, 1: np.complex64, 2: np.complex64, 3: np.complex64,
+                4: np.float32, 5: np.float32}
+
+
+def device_count():
+    n = lib.owrx_device_count()
+    return n if n > 0 else 0
+
+
+class Engine:
+    def __init__(self, samp_rate, max_block=1 << 20, device=0):
+        h = ctypes.c_void_p()
+        check(lib.owrx_engine_create(device, float(samp_rate), int(max_block), ctypes.byref(h)),
+              "owrx_engine_create")
+        self._h = h
+        self.samp_rate = samp_rate
+        self.device = device
+        self.max_block = int(max_block)
+        self.history = lib.owrx_engine_history(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib.owrx_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, iq):
+        """Host cf32 samples (complex64 array or interleaved float32)."""
+        a = np.ascontiguousarray(iq)
+        if a.dtype == np.complex64:
+            n = a.size
+        elif a.dtype == np.float32:
+            n = a.size // 2
+        else:
+            raise ValueError("IQ must be complex64 / interleaved float32")
+        check(lib.owrx_push_iq(self._h, a.ctypes.data, n), "owrx_push_iq")
+
+    def process_device(self, ptr, n):
+        check(lib.owrx_process_device(self._h, ctypes.c_void_p(ptr), int(n)), "owrx_process_device")
+
+    def ingest_buffer(self):
+        p = ctypes.c_void_p()
+        cap = ctypes.c_int64()
+        check(lib.owrx_ingest_buffer(self._h, ctypes.byref(p), ctypes.byref(cap)), "ingest_buffer")
+        return p.value, cap.value
+
+    def commit(self, n):
+        check(lib.owrx_commit(self._h, int(n)), "owrx_commit")
+
+    def sync(self):
+        check(lib.owrx_sync(self._h), "owrx_sync")
+
+    def set_debug(self, on=True):
+        check(lib.owrx_set_debug(self._h, 1 if on else 0), "owrx_set_debug")
+
+    def set_timing(self, on=True):
+        check(lib.owrx_set_timing(self._h, 1 if on else 0), "owrx_set_timing")
+
+    def stats(self):
+        s = _lib.Stats()
+        check(lib.owrx_get_stats(self._h, ctypes.byref(s)), "owrx_get_stats")
+        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
+
+    def waterfall(self, fft_size, every_n_samples, avg_number, add_db=-70.0, adpcm=True):
+        return Waterfall(self, fft_size, every_n_samples, avg_number, add_db, adpcm)
+
+    def chain(self, params):
+        return Chain(self, params)
+
+
+class Waterfall:
+    def __init__(self, engine, fft_size, every_n_samples, avg_number, add_db, adpcm):
+        self.engine = engine
+        h = ctypes.c_int()
+        check(lib.owrx_waterfall_create(engine.handle, int(fft_size), int(every_n_samples),
+                                        int(avg_number), float(add_db), 1 if adpcm else 0,
+                                        ctypes.byref(h)), "owrx_waterfall_create")
+        self.id = h.value
+        self.fft_size = fft_size
+        self.adpcm = adpcm
+
+    def set(self, every_n_samples, avg_number, adpcm):
+        check(lib.owrx_waterfall_set(self.engine.handle, self.id, int(every_n_samples),
+                                     int(avg_number), 1 if adpcm else 0), "owrx_waterfall_set")
+        self.adpcm = adpcm
+
+    def row_bytes(self):
+        return check(lib.owrx_waterfall_row_bytes(self.engine.handle, self.id), "row_bytes")
+
+    def read(self, max_bytes=1 << 26):
+        buf = np.empty(max_bytes, dtype=np.uint8)
+        n = check(lib.owrx_waterfall_read(self.engine.handle, self.id, buf.ctypes.data, max_bytes),
+                  "owrx_waterfall_read")
+        return buf[:n].tobytes()
+
+    def read_rows(self):
+        rb = self.row_bytes()
+        data = self.read()
+        if self.adpcm:
+            return np.frombuffer(data, dtype=np.uint8).reshape(-1, rb)
+        return np.frombuffer(data, dtype=np.float32).reshape(-1, self.fft_size)
+
+    def close(self):
+        if self.id:
+            lib.owrx_waterfall_destroy(self.engine.handle, self.id)
+            self.id = 0
+
+
+class Chain:
+    def __init__(self, engine, params):
+        self.engine = engine
+        self.params = params
+        h = ctypes.c_int()
+        check(lib.owrx_chain_create(engine.handle, ctypes.byref(params), ctypes.byref(h)),
+              "owrx_chain_create")
+        self.id = h.value
+
+    @property
+    def origin(self):
+        return check(lib.owrx_chain_origin(self.engine.handle, self.id), "origin")
+
+    def set_shift_rate(self, rate):
+        check(lib.owrx_chain_set_shift_rate(self.engine.handle, self.id, float(rate)), "shift")
+
+    def set_bandpass(self, low, high):
+        en = low is not None and high is not None
+        check(lib.owrx_chain_set_bandpass(self.engine.handle, self.id, 1 if en else 0,
+                                          float(low or 0), float(high or 0)), "bandpass")
+
+    def set_squelch_level(self, level):
+        check(lib.owrx_chain_set_squelch_level(self.engine.handle, self.id, float(level)),
+              "squelch")
+
+    def read_audio(self, max_bytes=1 << 24):
+        buf = np.empty(max_bytes, dtype=np.uint8)
+        n = check(lib.owrx_chain_read_audio(self.engine.handle, self.id, buf.ctypes.data,
+                                            max_bytes), "read_audio")
+        return buf[:n].tobytes()
+
+    def read_smeter(self, max_values=1 << 16):
+        buf = np.empty(max_values, dtype=np.float32)
+        n = check(lib.owrx_chain_read_smeter(self.engine.handle, self.id, buf.ctypes.data,
+                                             max_values), "read_smeter")
+        return buf[:n].copy()
+
+    def read_debug(self, stage, max_bytes=1 << 26):
+        buf = np.empty(max_bytes, dtype=np.uint8)
+        n = check(lib.owrx_chain_read_debug(self.engine.handle, self.id, stage, buf.ctypes.data,
+                                            max_bytes), "read_debug")
+        return np.frombuffer(buf[:n].tobytes(), dtype=_STAGE_DTYPE[stage])
+
+    def close(self):
+        if self.id:
+            lib.owrx_chain_destroy(self.engine.handle, self.id)
+            self.id = 0
+
+
+class Module:
+    """One csdr module on the GPU outside a fused chain (owrx_module_*)."""
+
+    def __init__(self, mtype, p0=0.0, p1=-1.0, p2=-1.0, device=0):
+        h = ctypes.c_void_p()
+        check(lib.owrx_module_create(device, mtype, float(p0), float(p1), float(p2),
+                                     ctypes.byref(h)), "owrx_module_create")
+        self._h = h
+        self.mtype = mtype
+
+    def process(self, data, out_bytes):
+        a = np.ascontiguousarray(data)
+        if a.dtype == np.complex64:
+            n = a.size
+        else:
+            n = a.size
+        out = np.empty(max(int(out_bytes), 1), dtype=np.uint8)
+        r = check(lib.owrx_module_process(self._h, a.ctypes.data, n, out.ctypes.data, out.size),
+                  "owrx_module_process")
+        return out[:r].tobytes()
+
+    def close(self):
+        if self._h:
+            lib.owrx_module_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

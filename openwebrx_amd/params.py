@@ -1,0 +1,104 @@
+"""Chain parameter math, restated from the reference's chain code so the engine receives the
+exact module arguments the reference would construct (pinned by tests/golden/chain_params.json):
+
+* FftChain._updateParameters / _setBlockSize -- csdr/chain/fft.py:51-55, 75-85
+* Decimator._getDecimation, transition, cutoff -- csdr/chain/selector.py:11-51
+* Selector._buildBandpass / setBandpass / _buildSquelch / _updateShift / _convertToLinear
+  -- csdr/chain/selector.py:115-147, 159-166
+* NFm / Am / Ssb / ClientAudioChain module choices -- csdr/chain/analog.py, clientaudio.py
+* mode bandpass table -- owrx/modes.py:124-129
+"""
+import math
+
+import numpy as np
+
+from . import _lib
+
+MODE_BANDPASS = {  # owrx/modes.py:124-129
+    "nfm": (-5999, 5999),
+    "am": (-4700, 4700),
+    "lsb": (-3000, -150),
+    "usb": (150, 3000),
+    "cw": (700, 900),
+}
+MODE_DEMOD = {"nfm": _lib.DEMOD_NFM, "am": _lib.DEMOD_AM, "usb": _lib.DEMOD_SSB,
+              "lsb": _lib.DEMOD_SSB, "cw": _lib.DEMOD_SSB}
+
+
+def f32(x):
+    """pycsdr receives float arguments as C float."""
+    return float(np.float32(x))
+
+
+def fft_parameters(samp_rate, fft_size, fps, voverlap):
+    """(avg_number, every_n_samples) exactly as FftChain._updateParameters computes them."""
+    avg = 0
+    if voverlap > 0:
+        avg = int(round(1.0 * samp_rate / fft_size / fps / (1.0 - voverlap)))
+    if avg == 0:
+        block = samp_rate / fps
+    else:
+        block = samp_rate / fps / avg
+    return avg, int(block)
+
+
+def decimation(input_rate, output_rate):
+    """Decimator._getDecimation + transition/cutoff (selector.py:22-27, 40-51)."""
+    if output_rate > input_rate:
+        output_rate = input_rate
+    d = input_rate / output_rate
+    d_int = int(d)
+    frac = float(input_rate / d_int) / output_rate
+    transition = 0.15 * (output_rate / float(input_rate))
+    cutoff = 0.5 * d_int / (input_rate / output_rate)
+    return d_int, frac, transition, cutoff
+
+
+def shift_rate(offset, input_rate):
+    return -offset / input_rate  # Selector._updateShift
+
+
+def squelch_parameters(output_rate, measurements_per_sec=16, readings_per_sec=4):
+    block = int(output_rate / measurements_per_sec)  # Selector._buildSquelch
+    return dict(length=block, decimation=5, hangLength=2 * block, flushLength=5 * block,
+                reportInterval=int(measurements_per_sec / readings_per_sec))
+
+
+def squelch_level(db):
+    return float(math.pow(10, db / 10))  # Selector._convertToLinear
+
+
+def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=None,
+                 squelch_db=-150, output=_lib.OUT_ADPCM, agc_profile=None):
+    """owrx_chain_params for ClientDemodulatorChain([Selector, demod, ClientAudioChain])."""
+    d, frac, tbw, cutoff = decimation(input_rate, output_rate)
+    if bandpass is None:
+        bandpass = MODE_BANDPASS.get(mode)
+    sq = squelch_parameters(output_rate)
+    p = _lib.ChainParams()
+    p.shift_rate = f32(shift_rate(offset, input_rate))
+    p.decimation = d
+    p.transition = f32(tbw)
+    p.cutoff = f32(cutoff)
+    p.frac_rate = frac  # FractionalDecimator(rate) only when frac != 1.0 (selector.py:32)
+    if bandpass is not None:
+        p.bandpass = 1
+        p.bp_low = f32(bandpass[0] / output_rate)
+        p.bp_high = f32(bandpass[1] / output_rate)
+    p.bp_transition = f32(320.0 / output_rate)
+    p.sq_length = sq["length"]
+    p.sq_decimation = sq["decimation"]
+    p.sq_hang = sq["hangLength"]
+    p.sq_flush = sq["flushLength"]
+    p.sq_report = sq["reportInterval"]
+    p.sq_level = f32(squelch_level(squelch_db))
+    demod = MODE_DEMOD[mode]
+    p.demod = demod
+    if agc_profile is None:  # NFm/Am: SLOW (analog.py:35,12); Ssb: ssb_agc_profile "Fast"
+        agc_profile = _lib.AGC_FAST if demod == _lib.DEMOD_SSB else _lib.AGC_SLOW
+    p.agc_profile = agc_profile
+    p.agc_initial_gain = 200.0 if demod == _lib.DEMOD_AM else -1.0   # Am: setInitialGain(200)
+    p.agc_max_gain = 3.0 if demod == _lib.DEMOD_NFM else -1.0        # NFm: setMaxGain(3)
+    p.audio_rate = output_rate
+    p.output = output
+    return p
