@@ -70,11 +70,12 @@ AgcParams agc_profile(int profile) {
     p.reference = 0.8f;
     p.max_gain = 65535.0f;
     p.initial_gain = 1.0f;
+    p.hang_time = 0;
     switch (profile) {
-        case 0: p.attack = 0.1f; p.decay = 0.001f; p.hang_time = 200; break;    // FAST
-        case 1: p.attack = 0.1f; p.decay = 0.0001f; p.hang_time = 600; break;   // SLOW
-        case 2: p.attack = 0.1f; p.decay = 0.0005f; p.hang_time = 400; break;   // MID
-        default: p.attack = 0.01f; p.decay = 0.0001f; p.hang_time = 1200; break; // LAGGY
+        case 0: p.attack = 0.1f; p.decay = 0.001f; break;    // FAST
+        case 1: p.attack = 0.05f; p.decay = 0.0001f; break;  // SLOW
+        case 2: p.attack = 0.1f; p.decay = 0.0005f; break;   // MID
+        default: p.attack = 0.01f; p.decay = 0.0001f; break; // LAGGY
     }
     return p;
 }

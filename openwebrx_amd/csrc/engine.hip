@@ -973,7 +973,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     memset(&st, 0, sizeof(st));
     AgcParams ap = agc_profile(p->agc_profile);
     if (p->agc_initial_gain >= 0) ap.initial_gain = p->agc_initial_gain;
-    st.agc.gain = ap.initial_gain;
+    st.agc.env = ap.reference / ap.initial_gain;
     HIPCHK(dalloc(&c->d_state, 1));
     HIPCHK(hipMemcpy(c->d_state, &st, sizeof(st), hipMemcpyHostToDevice));
     HIPCHK(dalloc(&c->d_ddc, (size_t)(kFdHist + c->cap)));

@@ -191,7 +191,7 @@ extern "C" int owrx_module_create(int device, int type, double p0, double p1, do
             m->p.agc = agc_profile((int)p0);
             if (p1 >= 0) m->p.agc.initial_gain = (float)p1;
             if (p2 >= 0) m->p.agc.max_gain = (float)p2;
-            s.agc.gain = m->p.agc.initial_gain;
+            s.agc.env = m->p.agc.reference / m->p.agc.initial_gain;
             break;
         case OWRX_MOD_ADPCM: m->p.i0 = (int)p0; break;
         case OWRX_MOD_FFTSWAP:

@@ -21,11 +21,11 @@ constexpr float kFmK = 0.340447f; // fmdemod_quadri_K
 
 struct AgcParams {
     float reference, attack, decay, max_gain, initial_gain;
-    int hang_time;
+    int hang_time;  // unused by the continuous follower, kept for ABI stability
 };
 struct AgcState {
-    float gain;
-    int hang;
+    float env;
+    int pad;
 };
 struct AdpcmState {
     int index;
@@ -58,7 +58,7 @@ OWRX_DEV float am_step(float2 x) {
 #pragma clang fp contract(off)
     float ii = x.x * x.x;
     float qq = x.y * x.y;
-    return __fsqrt_rn(ii + qq);
+    return sqrtf(ii + qq);
 }
 
 // Limit (analog.py:44)
@@ -90,29 +90,18 @@ OWRX_DEV float dcblock_step(float x, float& xp, float& yp) {
     return y;
 }
 
-// Agc(FLOAT) (analog.py:13-15, 38-40, 121-122)
+// Agc(FLOAT) (analog.py:13-15, 38-40, 121-122): continuous attack/decay envelope follower,
+// gain = reference / envelope clamped to max_gain (see oracle/csdr_oracle.c orc_agc).
 OWRX_DEV float agc_step(float x, const AgcParams& p, AgcState& s) {
 #pragma clang fp contract(off)
     float a = fabsf(x);
-    if (a > 0.0f) {
-        float target = p.reference / a;
-        float err = target - s.gain;
-        float dg;
-        if (err < 0.0f) {
-            dg = err * p.attack;
-            s.hang = p.hang_time;
-        } else if (s.hang > 0) {
-            s.hang--;
-            dg = 0.0f;
-        } else {
-            dg = err * p.decay;
-        }
-        float g = s.gain + dg;
-        if (g < 0.0f) g = 0.0f;
-        if (g > p.max_gain) g = p.max_gain;
-        s.gain = g;
-    }
-    return s.gain * x;
+    float d = a - s.env;
+    float rate = (d > 0.0f) ? p.attack : p.decay;
+    float t = rate * d;
+    s.env = s.env + t;
+    float g = (s.env > 0.0f) ? p.reference / s.env : p.max_gain;
+    if (g > p.max_gain) g = p.max_gain;
+    return g * x;
 }
 
 OWRX_DEV int16_t f_to_s16(float v) {

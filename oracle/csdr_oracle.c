@@ -320,43 +320,35 @@ void orc_deemphasis(const float* in, int64_t n, float alpha, float* out) {
 }
 
 /* Agc(FLOAT) + AgcProfile (csdr/chain/analog.py:13-15, 38-40, 121-122; owrx/dsp.py:619).
- * Profile constants are the build's documented choice (unrecoverable upstream). */
+ * Upstream's AGC internals and profile constants are not recoverable; the build uses a
+ * continuous attack/decay envelope follower (gain = reference/envelope, clamped to max_gain).
+ * It is continuous in its input, so fp32 rounding differences upstream of it cannot be
+ * amplified by branch flips.  Constants are the build's documented choice. */
 void orc_agc_profile(int profile, orc_agc_params* p) {
     p->reference = 0.8f;
     p->max_gain = 65535.0f;
     p->initial_gain = 1.0f;
+    p->hang_time = 0;
     switch (profile) {
-        case 0: /* FAST */ p->attack_rate = 0.1f;  p->decay_rate = 0.001f;  p->hang_time = 200;  break;
-        case 1: /* SLOW */ p->attack_rate = 0.1f;  p->decay_rate = 0.0001f; p->hang_time = 600;  break;
-        case 2: /* MID */  p->attack_rate = 0.1f;  p->decay_rate = 0.0005f; p->hang_time = 400;  break;
-        default: /* LAGGY */ p->attack_rate = 0.01f; p->decay_rate = 0.0001f; p->hang_time = 1200; break;
+        case 0: /* FAST */ p->attack_rate = 0.1f;  p->decay_rate = 0.001f;  break;
+        case 1: /* SLOW */ p->attack_rate = 0.05f; p->decay_rate = 0.0001f; break;
+        case 2: /* MID */  p->attack_rate = 0.1f;  p->decay_rate = 0.0005f; break;
+        default: /* LAGGY */ p->attack_rate = 0.01f; p->decay_rate = 0.0001f; break;
     }
 }
 
 void orc_agc(const float* in, int64_t n, const orc_agc_params* p, float* out) {
-    float gain = p->initial_gain;
-    int hang = 0;
+    float env = p->reference / p->initial_gain;
     for (int64_t k = 0; k < n; k++) {
         float x = in[k];
         float a = fabsf(x);
-        if (a > 0.0f) {
-            float target = p->reference / a;
-            float err = target - gain;
-            float dg;
-            if (err < 0.0f) {
-                dg = err * p->attack_rate;
-                hang = p->hang_time;
-            } else if (hang > 0) {
-                hang--;
-                dg = 0.0f;
-            } else {
-                dg = err * p->decay_rate;
-            }
-            gain = gain + dg;
-            if (gain < 0.0f) gain = 0.0f;
-            if (gain > p->max_gain) gain = p->max_gain;
-        }
-        out[k] = gain * x;
+        float d = a - env;
+        float rate = (d > 0.0f) ? p->attack_rate : p->decay_rate;
+        float t = rate * d;
+        env = env + t;
+        float g = (env > 0.0f) ? p->reference / env : p->max_gain;
+        if (g > p->max_gain) g = p->max_gain;
+        out[k] = g * x;
     }
 }
 
