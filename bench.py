@@ -162,6 +162,7 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    eng.sync()
     eng.set_timing(True)
     s0 = eng.stats()
     if dist:
@@ -171,6 +172,7 @@ def main():
     out_bytes = 0
     for i in range(args.warmup, nsteps):
         out_bytes += step(i)
+    eng.sync()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()

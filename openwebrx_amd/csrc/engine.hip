@@ -2,11 +2,14 @@
 //
 // Replaces the reference's per-module native threads + ring buffers (pycsdr Buffer/Reader,
 // csdr modules; callers owrx/fft.py:36-73 and owrx/dsp.py:39-72, 835-863) with a block
-// scheduler: each processed block runs
-//   waterfall:  wf_fft_power -> wf_finalize -> wf_adpcm_rows      (per FftChain)
-//   chains:     ddc_polyphase per (D, taps) group -> post_chains   (all client chains)
-// on one HIP stream, then copies the finished waterfall rows, audio bytes and s-meter values
-// to host rings that the pycsdr binding drains.
+// scheduler over three HIP streams:
+//   A (main):   wf_fft_power + wf_finalize per FftChain; ddc_polyphase per (D, taps) group;
+//               post_parallel for all client chains
+//   B (serial): post_serial (deemphasis / DC block, AGC, Convert, ADPCM), then D2H of audio,
+//               s-meter and debug taps
+//   C (rows):   wf_adpcm_rows, then D2H of waterfall rows
+// Block k's B and C work runs concurrently with block k+1's A work; staging buffers are
+// double-buffered by block parity and drained into host rings that the pycsdr binding reads.
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -43,18 +46,21 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st);
 hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, int row_bytes,
-                           hipStream_t st);
+                           uint8_t* codes, uint32_t* traj, hipStream_t st);
 hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_end,
                       const float* taps_poly, const DdcChain* chains, int nchains, int D,
                       int64_t k_begin, int nk, int nseg, float2* partial, hipStream_t st);
 int ddc_padded_p(int p);
 int ddc_segments(int D, int nseg);
-hipError_t launch_post(const ChainPost* posts, int nchains, ChainCounts* counts,
-                       hipStream_t st);
+hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
+                                hipStream_t st);
+hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
+                              int nsel, int output, int debug, hipStream_t st);
 
 constexpr int kWfFramesPerGroup = 4;
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
+constexpr int kRowSlots = 2;  // waterfall row-encoding blocks in flight (streams R0, R1)
 
 #define HIPCHK(expr)                                                                    \
     do {                                                                                \
@@ -64,6 +70,12 @@ constexpr int kDebugStages = 6;
                            __FILE__, __LINE__);                                         \
             return OWRX_EIO;                                                            \
         }                                                                               \
+    } while (0)
+
+#define RCCHK(expr)               \
+    do {                          \
+        int _rc = (expr);         \
+        if (_rc) return _rc;      \
     } while (0)
 
 template <typename T>
@@ -77,6 +89,17 @@ static hipError_t dalloc(T** p, size_t count) {
 template <typename T>
 static void dfree(T*& p) {
     if (p) hipFree((void*)p);
+    p = nullptr;
+}
+template <typename T>
+static hipError_t halloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    return hipHostMalloc((void**)p, sizeof(T) * count, 0);
+}
+template <typename T>
+static void hfree(T*& p) {
+    if (p) hipHostFree((void*)p);
     p = nullptr;
 }
 
@@ -123,15 +146,21 @@ struct Waterfall {
     float* d_carry[2] = {nullptr, nullptr};
     WfGroup* d_groups = nullptr;
     WfRow* d_rows = nullptr;
-    int16_t* d_s16 = nullptr;
-    float* d_f32 = nullptr;
-    uint8_t* d_bytes = nullptr;
-    uint8_t* h_bytes = nullptr;  // pinned
     int rows_cap = 0;
+    // one set per row slot (kRowSlots blocks of rows in flight)
+    int16_t* d_s16[kRowSlots] = {};
+    float* d_f32[kRowSlots] = {};
+    uint8_t* d_bytes[kRowSlots] = {};
+    uint8_t* d_codes[kRowSlots] = {};   // row-parallel ADPCM scratch
+    uint32_t* d_traj[kRowSlots] = {};
+    uint8_t* h_bytes[kRowSlots] = {};
+    int pend_rows[kRowSlots] = {};
+    int pend_adpcm[kRowSlots] = {};
     ByteRing ring;
     std::vector<WfGroup> groups;
     std::vector<WfRow> rowdesc;
-    int64_t row_bytes() const { return adpcm ? (N + 10) / 2 : 4 * (int64_t)N; }
+    int64_t row_bytes_for(int adp) const { return adp ? (N + 10) / 2 : 4 * (int64_t)N; }
+    int64_t row_bytes() const { return row_bytes_for(adpcm); }
 };
 
 struct ChainGroup {
@@ -145,6 +174,8 @@ struct ChainGroup {
     float2* d_partial = nullptr;
     size_t partial_elems = 0;
     int nseg = 1;
+    DdcChain* h_chains = nullptr;  // pinned copy source
+    int h_cap = 0;
 };
 
 struct Chain {
@@ -160,11 +191,12 @@ struct Chain {
     bool rate_pending = false;
     float new_rate = 0.0f;
     // device
-    ChainState* d_state = nullptr;
+    ChainStateP* d_pstate = nullptr;
+    ChainStateS* d_sstate = nullptr;
     float2* d_ddc = nullptr;
     float2* d_fd = nullptr;
     float2* d_sq = nullptr;
-    float* d_dem = nullptr;
+    float* d_dem[2] = {nullptr, nullptr};
     float2* d_bp_taps = nullptr;
     int bp_ntaps = 0;
     int64_t cap = 0;      // per-step sample capacity of stage buffers
@@ -175,17 +207,50 @@ struct Chain {
     ByteRing dbg[kDebugStages];
 };
 
+struct Slot {  // one block's outputs in flight on streams B / C
+    bool chains_pending = false;
+    std::vector<int> post_ids;
+    bool debug = false;
+    ChainPost* d_posts = nullptr;
+    ChainPost* h_posts = nullptr;
+    int* d_sel = nullptr;   // post indices grouped by output mode
+    int* h_sel = nullptr;
+    ChainCounts* d_counts = nullptr;
+    ChainCounts* h_counts = nullptr;
+    uint8_t* d_out = nullptr;
+    uint8_t* h_out = nullptr;
+    float* d_sm = nullptr;
+    float* h_sm = nullptr;
+    uint8_t* d_dbg = nullptr;
+    uint8_t* h_dbg = nullptr;
+    hipEvent_t evA = nullptr;   // stream A finished this block's post_parallel
+    hipEvent_t evB = nullptr;   // stream B finished (audio copied to host)
+    // timing brackets: A: [a0 wf a1 ddc a2 post_parallel a3]; B: [b0 post_serial b1]
+    hipEvent_t a0 = nullptr, a1 = nullptr, a2 = nullptr, a3 = nullptr;
+    hipEvent_t b0 = nullptr, b1 = nullptr;
+    bool timed = false;
+    bool timed_wf = false;
+};
+
+struct RowSlot {  // one block's waterfall rows being encoded / copied on its own stream
+    hipStream_t stream = nullptr;
+    hipEvent_t evWf = nullptr;  // stream A finished the block's finalize
+    hipEvent_t evC = nullptr;   // rows copied to host
+    bool pending = false;
+};
+
 }  // namespace owrx
 
 using namespace owrx;
 
 struct owrx_engine {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t sA = nullptr, sB = nullptr;
     double samp_rate = 0;
     int64_t max_block = 0;
     int64_t history = kDefaultHistory;
     int64_t pos = 0;  // absolute samples processed
+    int64_t block_index = 0;
     bool failed = false;
     bool debug = false;
     bool timing = false;
@@ -198,23 +263,15 @@ struct owrx_engine {
     std::map<int, std::unique_ptr<Chain>> chains;
     std::vector<std::unique_ptr<ChainGroup>> groups;
     int next_handle = 1;
-    // post staging (all chains)
+    // post staging (all chains), per block parity
     int post_cap = 0;
-    ChainPost* d_posts = nullptr;
-    ChainCounts* d_counts = nullptr;
-    ChainCounts* h_counts = nullptr;
-    uint8_t* d_out = nullptr;
-    uint8_t* h_out = nullptr;
-    float* d_sm = nullptr;
-    float* h_sm = nullptr;
-    int64_t out_stride = 0, sm_stride = 0;
-    uint8_t* d_dbg = nullptr;
-    uint8_t* h_dbg = nullptr;
-    int64_t dbg_stride = 0;  // bytes per chain per stage
+    int64_t out_stride = 0, sm_stride = 0, dbg_stride = 0;
+    Slot slots[2];
+    RowSlot rslots[kRowSlots];
+    int64_t row_head = 0;  // next row slot to fill
+    int64_t row_tail = 0;  // oldest row slot not yet drained
     std::vector<ChainPost> posts;
-    std::vector<int> post_ids;
     owrx_stats stats;
-    hipEvent_t ev[6];
 };
 
 // ------------------------------------------------------------------------------------------
@@ -228,11 +285,13 @@ static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
 }
 
 static void free_chain(Chain* c) {
-    dfree(c->d_state);
+    dfree(c->d_pstate);
+    dfree(c->d_sstate);
     dfree(c->d_ddc);
     dfree(c->d_fd);
     dfree(c->d_sq);
-    dfree(c->d_dem);
+    dfree(c->d_dem[0]);
+    dfree(c->d_dem[1]);
     dfree(c->d_bp_taps);
 }
 
@@ -244,18 +303,127 @@ static void free_wf(Waterfall* w) {
     dfree(w->d_carry[1]);
     dfree(w->d_groups);
     dfree(w->d_rows);
-    dfree(w->d_s16);
-    dfree(w->d_f32);
-    dfree(w->d_bytes);
-    if (w->h_bytes) hipHostFree(w->h_bytes);
-    w->h_bytes = nullptr;
+    for (int s = 0; s < kRowSlots; ++s) {
+        dfree(w->d_s16[s]);
+        dfree(w->d_f32[s]);
+        dfree(w->d_bytes[s]);
+        dfree(w->d_codes[s]);
+        dfree(w->d_traj[s]);
+        hfree(w->h_bytes[s]);
+    }
+}
+
+static void free_slot_staging(Slot& s) {
+    dfree(s.d_posts);
+    dfree(s.d_sel);
+    hfree(s.h_sel);
+    dfree(s.d_counts);
+    dfree(s.d_out);
+    dfree(s.d_sm);
+    dfree(s.d_dbg);
+    hfree(s.h_posts);
+    hfree(s.h_counts);
+    hfree(s.h_out);
+    hfree(s.h_sm);
+    hfree(s.h_dbg);
+}
+
+// Drain one block's outputs (streams B / C) into the host rings.
+static int drain_slot(owrx_engine* e, int si) {
+    Slot& s = e->slots[si];
+    if (s.chains_pending) {
+        HIPCHK(hipEventSynchronize(s.evB));
+        s.chains_pending = false;
+        if (s.timed) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, s.a1, s.a2) == hipSuccess) e->stats.gpu_ms_ddc += ms;
+            if (hipEventElapsedTime(&ms, s.b0, s.b1) == hipSuccess) e->stats.gpu_ms_post += ms;
+            if (hipEventElapsedTime(&ms, s.a2, s.a3) == hipSuccess) e->stats.gpu_ms_post += ms;
+            s.timed = false;
+        }
+        for (size_t k = 0; k < s.post_ids.size(); ++k) {
+            auto it = e->chains.find(s.post_ids[k]);
+            if (it == e->chains.end()) continue;
+            Chain* c = it->second.get();
+            const ChainCounts& cc = s.h_counts[k];
+            const int64_t nb = std::min<int64_t>(cc.out_bytes, e->out_stride);
+            if (cc.out_bytes > e->out_stride) e->stats.overruns++;
+            c->audio.push(s.h_out + (int64_t)k * e->out_stride, (size_t)nb);
+            e->stats.audio_bytes += nb;
+            e->stats.ddc_outputs += cc.n_ddc;
+            c->smeter.push((const uint8_t*)(s.h_sm + (int64_t)k * e->sm_stride),
+                           sizeof(float) * (size_t)std::min<int64_t>(cc.smeter, e->sm_stride));
+            if (s.debug && s.h_dbg) {
+                const uint8_t* base = s.h_dbg + (int64_t)k * kDebugStages * e->dbg_stride;
+                const int64_t cnt[kDebugStages] = {cc.n_ddc, cc.n_fd, cc.n_bp,
+                                                   cc.n_sq,  cc.n_sq, cc.n_sq};
+                const int64_t isz[kDebugStages] = {8, 8, 8, 8, 4, 4};
+                for (int st = 0; st < kDebugStages; ++st) {
+                    const int64_t bytes = std::min(cnt[st] * isz[st], e->dbg_stride);
+                    c->dbg[st].push(base + st * e->dbg_stride, (size_t)bytes);
+                }
+            }
+        }
+    } else if (s.timed) {
+        float ms = 0;
+        HIPCHK(hipEventSynchronize(s.a3));
+        if (hipEventElapsedTime(&ms, s.a1, s.a2) == hipSuccess) e->stats.gpu_ms_ddc += ms;
+        s.timed = false;
+    }
+    if (s.timed_wf) {
+        float ms = 0;
+        HIPCHK(hipEventSynchronize(s.a1));
+        if (hipEventElapsedTime(&ms, s.a0, s.a1) == hipSuccess) e->stats.gpu_ms_waterfall += ms;
+        s.timed_wf = false;
+    }
+    return OWRX_OK;
+}
+
+// Drain finished row slots in order; with `block` wait until `upto` slots remain in flight.
+static int drain_rows(owrx_engine* e, bool block, int keep) {
+    while (e->row_tail < e->row_head) {
+        const int ri = (int)(e->row_tail % kRowSlots);
+        RowSlot& r = e->rslots[ri];
+        const bool must = block && (e->row_head - e->row_tail) > keep;
+        if (!must) {
+            hipError_t q = hipEventQuery(r.evC);
+            if (q == hipErrorNotReady) break;
+            HIPCHK(q);
+        } else {
+            HIPCHK(hipEventSynchronize(r.evC));
+        }
+        for (auto& kv : e->wfs) {
+            Waterfall* w = kv.second.get();
+            const int nr = w->pend_rows[ri];
+            if (nr <= 0) continue;
+            const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
+            w->ring.push(w->h_bytes[ri], (size_t)(rb * nr));
+            w->rows += nr;
+            e->stats.waterfall_rows += nr;
+            w->pend_rows[ri] = 0;
+        }
+        r.pending = false;
+        e->row_tail++;
+    }
+    return OWRX_OK;
+}
+
+static int drain_all(owrx_engine* e) {
+    HIPCHK(hipStreamSynchronize(e->sA));
+    RCCHK(drain_rows(e, true, 0));
+    for (int i = 0; i < 2; ++i) {
+        const int si = (int)((e->block_index + i) & 1);  // oldest first
+        RCCHK(drain_slot(e, si));
+    }
+    return OWRX_OK;
 }
 
 static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
     // capacities derived from the current hop/avg; re-run when they change
     const int64_t frames = e->max_block / std::max(1, w->hop) + 2 * kWfFramesPerGroup + 2;
-    const int groups = (int)(frames / 1 + 2);  // a group may hold a single frame at row ends
+    const int groups = (int)(frames + 2);  // a group may hold a single frame at row ends
     const int rows = (int)(frames / std::max(1, w->avg) + 3);
+    if (groups > w->partial_groups || rows > w->rows_cap) RCCHK(drain_all(e));
     if (groups > w->partial_groups) {
         dfree(w->d_partial);
         dfree(w->d_groups);
@@ -265,16 +433,21 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
     }
     if (rows > w->rows_cap) {
         dfree(w->d_rows);
-        dfree(w->d_s16);
-        dfree(w->d_f32);
-        dfree(w->d_bytes);
-        if (w->h_bytes) hipHostFree(w->h_bytes);
-        w->h_bytes = nullptr;
         HIPCHK(dalloc(&w->d_rows, (size_t)rows + 1));
-        HIPCHK(dalloc(&w->d_s16, (size_t)rows * w->N));
-        HIPCHK(dalloc(&w->d_f32, (size_t)rows * w->N));
-        HIPCHK(dalloc(&w->d_bytes, (size_t)rows * 4 * w->N));
-        HIPCHK(hipHostMalloc((void**)&w->h_bytes, (size_t)rows * 4 * w->N, 0));
+        for (int s = 0; s < kRowSlots; ++s) {
+            dfree(w->d_s16[s]);
+            dfree(w->d_f32[s]);
+            dfree(w->d_bytes[s]);
+            dfree(w->d_codes[s]);
+            dfree(w->d_traj[s]);
+            hfree(w->h_bytes[s]);
+            HIPCHK(dalloc(&w->d_codes[s], (size_t)rows * (w->N + 10)));
+            HIPCHK(dalloc(&w->d_traj[s], (size_t)rows * (w->N + 10)));
+            HIPCHK(dalloc(&w->d_s16[s], (size_t)rows * w->N));
+            HIPCHK(dalloc(&w->d_f32[s], (size_t)rows * w->N));
+            HIPCHK(dalloc(&w->d_bytes[s], (size_t)rows * 4 * w->N));
+            HIPCHK(halloc(&w->h_bytes[s], (size_t)rows * 4 * w->N));
+        }
         w->rows_cap = rows;
     }
     return OWRX_OK;
@@ -291,35 +464,28 @@ static int ensure_post_capacity(owrx_engine* e) {
     if (n <= e->post_cap && need_out <= e->out_stride && need_sm <= e->sm_stride &&
         (!e->debug || need_dbg <= e->dbg_stride))
         return OWRX_OK;
+    RCCHK(drain_all(e));
     const int cap = std::max(n, e->post_cap ? e->post_cap * 2 : 16);
-    dfree(e->d_posts);
-    dfree(e->d_counts);
-    dfree(e->d_out);
-    dfree(e->d_sm);
-    dfree(e->d_dbg);
-    if (e->h_counts) hipHostFree(e->h_counts);
-    if (e->h_out) hipHostFree(e->h_out);
-    if (e->h_sm) hipHostFree(e->h_sm);
-    if (e->h_dbg) hipHostFree(e->h_dbg);
-    e->h_counts = nullptr;
-    e->h_out = nullptr;
-    e->h_sm = nullptr;
-    e->h_dbg = nullptr;
     e->out_stride = (need_out + 255) & ~(int64_t)255;
     e->sm_stride = need_sm;
-    HIPCHK(dalloc(&e->d_posts, cap));
-    HIPCHK(dalloc(&e->d_counts, cap));
-    HIPCHK(dalloc(&e->d_out, (size_t)cap * e->out_stride));
-    HIPCHK(dalloc(&e->d_sm, (size_t)cap * e->sm_stride));
-    HIPCHK(hipHostMalloc((void**)&e->h_counts, sizeof(ChainCounts) * cap, 0));
-    HIPCHK(hipHostMalloc((void**)&e->h_out, (size_t)cap * e->out_stride, 0));
-    HIPCHK(hipHostMalloc((void**)&e->h_sm, sizeof(float) * cap * e->sm_stride, 0));
-    if (e->debug) {
-        e->dbg_stride = (need_dbg + 255) & ~(int64_t)255;
-        HIPCHK(dalloc(&e->d_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
-        HIPCHK(hipHostMalloc((void**)&e->h_dbg, (size_t)cap * kDebugStages * e->dbg_stride, 0));
-    } else {
-        e->dbg_stride = 0;
+    e->dbg_stride = e->debug ? (need_dbg + 255) & ~(int64_t)255 : 0;
+    for (int si = 0; si < 2; ++si) {
+        Slot& s = e->slots[si];
+        free_slot_staging(s);
+        HIPCHK(dalloc(&s.d_posts, cap));
+        HIPCHK(halloc(&s.h_posts, cap));
+        HIPCHK(dalloc(&s.d_sel, cap));
+        HIPCHK(halloc(&s.h_sel, cap));
+        HIPCHK(dalloc(&s.d_counts, cap));
+        HIPCHK(dalloc(&s.d_out, (size_t)cap * e->out_stride));
+        HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
+        HIPCHK(halloc(&s.h_counts, (size_t)cap));
+        HIPCHK(halloc(&s.h_out, (size_t)cap * e->out_stride));
+        HIPCHK(halloc(&s.h_sm, (size_t)cap * e->sm_stride));
+        if (e->debug) {
+            HIPCHK(dalloc(&s.d_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
+            HIPCHK(halloc(&s.h_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
+        }
     }
     e->post_cap = cap;
     return OWRX_OK;
@@ -329,9 +495,12 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     // per-chain DDC descriptors + partial buffer sized for the current membership
     const int n = (int)g->members.size();
     if (n > g->chains_cap) {
+        RCCHK(drain_all(e));
         dfree(g->d_chains);
+        hfree(g->h_chains);
         g->chains_cap = std::max(n, 2 * g->chains_cap);
         HIPCHK(dalloc(&g->d_chains, (size_t)g->chains_cap));
+        HIPCHK(halloc(&g->h_chains, (size_t)g->chains_cap));
     }
     const int64_t nk_max = e->max_block / g->D + 4;
     // segments: enough waves to fill 256 CUs x 4 SIMDs x ~4 waves
@@ -347,6 +516,7 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     nseg = ddc_segments(g->D, nseg);
     const size_t need = (size_t)nseg * std::max(1, n) * nk_max;
     if (need > g->partial_elems) {
+        RCCHK(drain_all(e));
         dfree(g->d_partial);
         HIPCHK(dalloc(&g->d_partial, need));
         g->partial_elems = need;
@@ -359,13 +529,17 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
 // block processing
 // ------------------------------------------------------------------------------------------
 
+// Schedules and launches one FftChain's work for the block on stream A; completed rows are
+// staged in slot `si` (their ADPCM / copy is enqueued by the caller on stream C).
 static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, int64_t blk_start,
-                             int64_t blk_end) {
+                             int64_t blk_end, int ri, int* completed) {
+    *completed = 0;
     w->groups.clear();
     w->rowdesc.clear();
-    // schedule whole groups whose frames are inside the block (plus history)
     int cur_row_first_group = 0;
     bool row_open = false;
+    const int adpcm_now = w->adpcm;
+    const int avg_now = w->avg;
     while (true) {
         const int gf = std::min(kWfFramesPerGroup, w->avg - w->row_frame);
         const int64_t last = w->next_start + (int64_t)(gf - 1) * w->hop;
@@ -390,18 +564,17 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
             w->row_frame = 0;
             w->carry_valid = false;
             row_open = false;
-            if (w->pending) {  // parameter changes apply at row boundaries
+            if (w->pending) {  // parameter changes apply at row boundaries (next block)
                 w->hop = w->new_hop;
                 w->avg = w->new_avg;
                 w->adpcm = w->new_adpcm;
                 w->pending = false;
-                int rc = wf_alloc_buffers(e, w);
-                if (rc) return rc;
+                break;
             }
             if ((int)w->rowdesc.size() + 1 >= w->rows_cap) break;
         }
     }
-    int ncomplete = (int)w->rowdesc.size();
+    const int ncomplete = (int)w->rowdesc.size();
     if (row_open) {  // partially accumulated row: sum into the carry
         WfRow r;
         r.first_group = cur_row_first_group;
@@ -414,59 +587,80 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     }
     if (w->groups.empty()) return OWRX_OK;
     HIPCHK(hipMemcpyAsync(w->d_groups, w->groups.data(), sizeof(WfGroup) * w->groups.size(),
-                          hipMemcpyHostToDevice, e->stream));
+                          hipMemcpyHostToDevice, e->sA));
     HIPCHK(hipMemcpyAsync(w->d_rows, w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size(),
-                          hipMemcpyHostToDevice, e->stream));
-    if (e->timing) hipEventRecord(e->ev[2], e->stream);
+                          hipMemcpyHostToDevice, e->sA));
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(),
-                         w->d_window, w->d_tw, w->d_partial, e->stream));
-    if (e->timing) hipEventRecord(e->ev[3], e->stream);
-    const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, w->avg)));
+                         w->d_window, w->d_tw, w->d_partial, e->sA));
+    const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
     const int cin = w->carry_idx, cout = 1 - w->carry_idx;
     HIPCHK(launch_wf_finalize(w->d_partial, w->d_rows, (int)w->rowdesc.size(), w->d_carry[cin],
-                              w->d_carry[cout], w->N, corr, w->adpcm, w->d_s16, w->d_f32,
-                              e->stream));
+                              w->d_carry[cout], w->N, corr, adpcm_now, w->d_s16[ri],
+                              w->d_f32[ri], e->sA));
     if (row_open) {
         w->carry_idx = cout;
         w->carry_valid = true;
     }
     e->stats.waterfall_launches++;
-    if (ncomplete > 0) {
-        const int64_t rb = w->row_bytes();
-        if (w->adpcm) {
-            HIPCHK(launch_wf_adpcm(w->d_s16, w->N, ncomplete, w->d_bytes, (int)rb, e->stream));
-            HIPCHK(hipMemcpyAsync(w->h_bytes, w->d_bytes, rb * ncomplete, hipMemcpyDeviceToHost,
-                                  e->stream));
-        } else {
-            HIPCHK(hipMemcpyAsync(w->h_bytes, w->d_f32, rb * ncomplete, hipMemcpyDeviceToHost,
-                                  e->stream));
-        }
-    }
+    w->pend_rows[ri] = ncomplete;
+    w->pend_adpcm[ri] = adpcm_now;
+    *completed = ncomplete;
     return OWRX_OK;
 }
 
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const int64_t blk_start = e->pos;
     const int64_t blk_end = e->pos + n;
-    if (e->timing) hipEventRecord(e->ev[0], e->stream);
+    const int si = (int)(e->block_index & 1);
+    Slot& S = e->slots[si];
+    // the slot's previous block (k-2) must be drained before its buffers are reused
+    RCCHK(drain_slot(e, si));
+    const bool timed = e->timing;
+    if (timed) HIPCHK(hipEventRecord(S.a0, e->sA));
 
-    // ---- waterfalls
-    std::vector<std::pair<Waterfall*, int>> wf_done;
-    for (auto& kv : e->wfs) {
-        Waterfall* w = kv.second.get();
-        const size_t before = w->rowdesc.size();
-        (void)before;
-        int rc = process_waterfall(e, w, blk, blk_start, blk_end);
-        if (rc) return rc;
-        int complete = 0;
-        for (auto& r : w->rowdesc) complete += r.complete;
-        if (!w->groups.empty() && complete) wf_done.push_back({w, complete});
+    // ---- waterfalls (stream A); row encoding + copy on the row slot's own stream
+    bool any_rows = false;
+    if (!e->wfs.empty()) {
+        RCCHK(drain_rows(e, true, kRowSlots - 1));  // frees the slot about to be reused
+        const int ri = (int)(e->row_head % kRowSlots);
+        RowSlot& R = e->rslots[ri];
+        for (auto& kv : e->wfs) {
+            Waterfall* w = kv.second.get();
+            int done = 0;
+            RCCHK(process_waterfall(e, w, blk, blk_start, blk_end, ri, &done));
+            any_rows |= done > 0;
+        }
+        if (any_rows) {
+            HIPCHK(hipEventRecord(R.evWf, e->sA));
+            HIPCHK(hipStreamWaitEvent(R.stream, R.evWf, 0));
+            for (auto& kv : e->wfs) {
+                Waterfall* w = kv.second.get();
+                const int nr = w->pend_rows[ri];
+                if (nr <= 0) continue;
+                const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
+                if (w->pend_adpcm[ri]) {
+                    HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
+                                           w->d_codes[ri], w->d_traj[ri], R.stream));
+                    HIPCHK(hipMemcpyAsync(w->h_bytes[ri], w->d_bytes[ri], rb * nr,
+                                          hipMemcpyDeviceToHost, R.stream));
+                } else {
+                    HIPCHK(hipMemcpyAsync(w->h_bytes[ri], w->d_f32[ri], rb * nr,
+                                          hipMemcpyDeviceToHost, R.stream));
+                }
+            }
+            HIPCHK(hipEventRecord(R.evC, R.stream));
+            R.pending = true;
+            e->row_head++;
+        }
+    }
+    if (timed) {
+        HIPCHK(hipEventRecord(S.a1, e->sA));
+        S.timed_wf = !e->wfs.empty();
     }
 
-    // ---- chains: apply pending setters, DDC per group, then one post launch
+    // ---- chains: DDC per group (A), post_parallel (A), post_serial + copies (B)
     e->posts.clear();
-    e->post_ids.clear();
-    if (e->timing) hipEventRecord(e->ev[4], e->stream);
+    S.post_ids.clear();
     for (auto& gp : e->groups) {
         ChainGroup* g = gp.get();
         if (g->members.empty()) continue;
@@ -475,28 +669,27 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         const int64_t nk64 = k_end - g->k_next;
         if (nk64 <= 0) continue;
         const int nk = (int)nk64;
-        std::vector<DdcChain> dc(g->members.size());
         for (size_t i = 0; i < g->members.size(); ++i) {
             Chain* c = e->chains[g->members[i]].get();
             if (c->rate_pending) {  // retune at output boundary k_next (phase continuous)
                 const int64_t nb = std::max(g->k_next, c->k_first) * g->D;
-                const uint64_t ph_last = c->P0 + (uint64_t)(nb - c->n0) * c->rate_fx;
-                c->P0 = ph_last;
+                c->P0 = c->P0 + (uint64_t)(nb - c->n0) * c->rate_fx;
                 c->n0 = nb;
                 c->rate = c->new_rate;
                 c->rate_fx = rate_to_fx(c->rate);
                 c->rate_pending = false;
             }
-            dc[i].rate_fx = c->rate_fx;
-            dc[i].wD = rate_rotator(c->rate, g->D);
-            dc[i].n0 = c->n0;
-            dc[i].P0 = c->P0;
+            DdcChain& d = g->h_chains[i];
+            d.rate_fx = c->rate_fx;
+            d.wD = rate_rotator(c->rate, g->D);
+            d.n0 = c->n0;
+            d.P0 = c->P0;
         }
-        HIPCHK(hipMemcpyAsync(g->d_chains, dc.data(), sizeof(DdcChain) * dc.size(),
-                              hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemcpyAsync(g->d_chains, g->h_chains, sizeof(DdcChain) * g->members.size(),
+                              hipMemcpyHostToDevice, e->sA));
         HIPCHK(launch_ddc(g->P, blk, blk_start, blk_end, g->d_taps, g->d_chains,
                           (int)g->members.size(), g->D, g->k_next, nk, g->nseg, g->d_partial,
-                          e->stream));
+                          e->sA));
         e->stats.ddc_launches++;
         for (size_t i = 0; i < g->members.size(); ++i) {
             Chain* c = e->chains[g->members[i]].get();
@@ -520,26 +713,27 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.agc = agc_profile(q.agc_profile);
             if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
             if (q.agc_max_gain >= 0) p.agc.max_gain = q.agc_max_gain;
-            p.state = c->d_state;
+            p.pstate = c->d_pstate;
+            p.sstate = c->d_sstate;
             p.ddc_buf = c->d_ddc;
             p.fd_buf = c->d_fd;
             p.sq_buf = c->d_sq;
-            p.dem_buf = c->d_dem;
+            p.dem = c->d_dem[si];
             p.partial = g->d_partial;
-            p.nseg = ddc_segments(g->D, g->nseg);
+            p.nseg = g->nseg;
             p.group_chains = (int)g->members.size();
             p.chain_in_group = (int)i;
             p.nk = nk;
             p.k_begin = g->k_next;
             p.k_first = c->k_first;
             const int slot = (int)e->posts.size();
-            p.out = e->d_out + (int64_t)slot * e->out_stride;
+            p.out = S.d_out + (int64_t)slot * e->out_stride;
             p.out_cap = e->out_stride;
-            p.smeter = e->d_sm + (int64_t)slot * e->sm_stride;
+            p.smeter = S.d_sm + (int64_t)slot * e->sm_stride;
             p.smeter_cap = (int)e->sm_stride;
-            p.debug = e->debug ? 1 : 0;
-            if (e->debug) {
-                uint8_t* base = e->d_dbg + (int64_t)slot * kDebugStages * e->dbg_stride;
+            p.debug = (e->debug && S.d_dbg) ? 1 : 0;
+            if (p.debug) {
+                uint8_t* base = S.d_dbg + (int64_t)slot * kDebugStages * e->dbg_stride;
                 p.dbg_ddc = (float2*)(base + 0 * e->dbg_stride);
                 p.dbg_fd = (float2*)(base + 1 * e->dbg_stride);
                 p.dbg_bp = (float2*)(base + 2 * e->dbg_stride);
@@ -549,69 +743,58 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 p.dbg_cap = e->dbg_stride / 8;
             }
             e->posts.push_back(p);
-            e->post_ids.push_back(g->members[i]);
+            S.post_ids.push_back(g->members[i]);
         }
         g->k_next = k_end;
     }
-    if (e->timing) hipEventRecord(e->ev[5], e->stream);
     const int np = (int)e->posts.size();
+    if (timed) HIPCHK(hipEventRecord(S.a2, e->sA));
     if (np > 0) {
-        HIPCHK(hipMemcpyAsync(e->d_posts, e->posts.data(), sizeof(ChainPost) * np,
-                              hipMemcpyHostToDevice, e->stream));
-        HIPCHK(launch_post(e->d_posts, np, e->d_counts, e->stream));
-        HIPCHK(hipMemcpyAsync(e->h_counts, e->d_counts, sizeof(ChainCounts) * np,
-                              hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipMemcpyAsync(e->h_out, e->d_out, (size_t)np * e->out_stride,
-                              hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipMemcpyAsync(e->h_sm, e->d_sm, sizeof(float) * np * e->sm_stride,
-                              hipMemcpyDeviceToHost, e->stream));
-        if (e->debug)
-            HIPCHK(hipMemcpyAsync(e->h_dbg, e->d_dbg, (size_t)np * kDebugStages * e->dbg_stride,
-                                  hipMemcpyDeviceToHost, e->stream));
+        memcpy(S.h_posts, e->posts.data(), sizeof(ChainPost) * np);
+        HIPCHK(hipMemcpyAsync(S.d_posts, S.h_posts, sizeof(ChainPost) * np,
+                              hipMemcpyHostToDevice, e->sA));
+        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
+        HIPCHK(hipEventRecord(S.evA, e->sA));
+        HIPCHK(hipStreamWaitEvent(e->sB, S.evA, 0));
+        // one post_serial instantiation per output format present (S16 / ADPCM / F32)
+        int nsel[3] = {0, 0, 0};
+        for (int i = 0; i < np; ++i) nsel[e->posts[i].output]++;
+        int off[3] = {0, nsel[0], nsel[0] + nsel[1]};
+        int fill[3] = {off[0], off[1], off[2]};
+        for (int i = 0; i < np; ++i) S.h_sel[fill[e->posts[i].output]++] = i;
+        HIPCHK(hipMemcpyAsync(S.d_sel, S.h_sel, sizeof(int) * np, hipMemcpyHostToDevice, e->sB));
+        if (timed) HIPCHK(hipEventRecord(S.b0, e->sB));
+        const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
+        for (int o = 0; o < 3; ++o)
+            HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o], nsel[o], o, dbg,
+                                      e->sB));
+        if (timed) HIPCHK(hipEventRecord(S.b1, e->sB));
+        HIPCHK(hipMemcpyAsync(S.h_counts, S.d_counts, sizeof(ChainCounts) * np,
+                              hipMemcpyDeviceToHost, e->sB));
+        HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, (size_t)np * e->out_stride,
+                              hipMemcpyDeviceToHost, e->sB));
+        HIPCHK(hipMemcpyAsync(S.h_sm, S.d_sm, sizeof(float) * np * e->sm_stride,
+                              hipMemcpyDeviceToHost, e->sB));
+        S.debug = e->debug && S.d_dbg;
+        if (S.debug)
+            HIPCHK(hipMemcpyAsync(S.h_dbg, S.d_dbg, (size_t)np * kDebugStages * e->dbg_stride,
+                                  hipMemcpyDeviceToHost, e->sB));
+        HIPCHK(hipEventRecord(S.evB, e->sB));
+        S.chains_pending = true;
     }
-    if (e->timing) hipEventRecord(e->ev[1], e->stream);
-    HIPCHK(hipStreamSynchronize(e->stream));
-
-    // ---- drain into host rings
-    for (auto& wd : wf_done) {
-        Waterfall* w = wd.first;
-        const int64_t rb = w->row_bytes();
-        w->ring.push(w->h_bytes, (size_t)(rb * wd.second));
-        w->rows += wd.second;
-        e->stats.waterfall_rows += wd.second;
+    if (timed) {
+        HIPCHK(hipEventRecord(S.a3, e->sA));
+        S.timed = true;
     }
-    for (int s = 0; s < np; ++s) {
-        Chain* c = e->chains[e->post_ids[s]].get();
-        const ChainCounts& cc = e->h_counts[s];
-        const int64_t nb = std::min<int64_t>(cc.out_bytes, e->out_stride);
-        if (cc.out_bytes > e->out_stride) e->stats.overruns++;
-        c->audio.push(e->h_out + (int64_t)s * e->out_stride, (size_t)nb);
-        e->stats.audio_bytes += nb;
-        e->stats.ddc_outputs += cc.n_ddc;
-        c->smeter.push((const uint8_t*)(e->h_sm + (int64_t)s * e->sm_stride),
-                       sizeof(float) * (size_t)cc.smeter);
-        if (e->debug) {
-            const uint8_t* base = e->h_dbg + (int64_t)s * kDebugStages * e->dbg_stride;
-            const int64_t cnt[kDebugStages] = {cc.n_ddc, cc.n_fd, cc.n_bp, cc.n_sq, cc.n_sq,
-                                               cc.n_sq};
-            const int64_t isz[kDebugStages] = {8, 8, 8, 8, 4, 4};
-            for (int st = 0; st < kDebugStages; ++st) {
-                const int64_t bytes = std::min(cnt[st] * isz[st], e->dbg_stride);
-                c->dbg[st].push(base + st * e->dbg_stride, (size_t)bytes);
-            }
-        }
-    }
-    if (e->timing) {
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, e->ev[4], e->ev[5]) == hipSuccess) e->stats.gpu_ms_ddc += ms;
-        if (!e->wfs.empty() && hipEventElapsedTime(&ms, e->ev[0], e->ev[4]) == hipSuccess)
-            e->stats.gpu_ms_waterfall += ms;
-        if (hipEventElapsedTime(&ms, e->ev[5], e->ev[1]) == hipSuccess) e->stats.gpu_ms_post += ms;
-    }
+    // the input block and the host-side descriptors are free once stream A is done
+    HIPCHK(hipStreamSynchronize(e->sA));
     e->pos = blk_end;
     e->stats.samples_in += n;
     e->stats.blocks++;
-    return OWRX_OK;
+    e->block_index++;
+    // drain the previous block (its B work overlapped this block's A work) and any rows done
+    RCCHK(drain_slot(e, (int)(e->block_index & 1)));
+    return drain_rows(e, false, 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -630,13 +813,13 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     }                                                                \
     hipSetDevice((e)->device);
 
-#define RC_FAIL(e, expr)          \
-    do {                          \
-        int _rc = (expr);         \
-        if (_rc < 0) {            \
+#define RC_FAIL(e, expr)                             \
+    do {                                             \
+        int _rc = (expr);                            \
+        if (_rc < 0) {                               \
             if (_rc == OWRX_EIO) (e)->failed = true; \
-            return _rc;           \
-        }                         \
+            return _rc;                              \
+        }                                            \
     } while (0)
 
 extern "C" {
@@ -669,22 +852,34 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
     e->samp_rate = samp_rate;
     e->max_block = max_block;
     memset(&e->stats, 0, sizeof(e->stats));
-    int rc = OWRX_OK;
     auto fail = [&](const char* what) {
         set_last_error("owrx_engine_create: %s", what);
         owrx_engine_destroy(e);
         return OWRX_EIO;
     };
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    // A, B, R0, R1: four streams = the four hardware queues HIP gives a process
+    // (GPU_MAX_HW_QUEUES), so no two of them serialise on a shared queue
+    if (hipStreamCreateWithFlags(&e->sA, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->sB, hipStreamNonBlocking) != hipSuccess)
         return fail("stream");
-    for (int i = 0; i < 6; ++i)
-        if (hipEventCreate(&e->ev[i]) != hipSuccess) return fail("event");
+    for (auto& r : e->rslots) {
+        if (hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
+            return fail("row stream");
+    }
+    for (auto& s : e->slots) {
+        if (hipEventCreateWithFlags(&s.evA, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.evB, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreate(&s.a0) != hipSuccess || hipEventCreate(&s.a1) != hipSuccess ||
+            hipEventCreate(&s.a2) != hipSuccess || hipEventCreate(&s.a3) != hipSuccess ||
+            hipEventCreate(&s.b0) != hipSuccess || hipEventCreate(&s.b1) != hipSuccess)
+            return fail("event");
+    }
     for (int i = 0; i < 2; ++i)
         if (dalloc(&e->d_win[i], (size_t)(e->history + max_block)) != hipSuccess)
             return fail("window");
-    if (hipHostMalloc((void**)&e->h_in, sizeof(float2) * (size_t)max_block, 0) != hipSuccess)
-        return fail("pinned input");
-    (void)rc;
+    if (halloc(&e->h_in, 2 * (size_t)max_block) != hipSuccess) return fail("pinned input");
     *out = e;
     return OWRX_OK;
 }
@@ -692,29 +887,32 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
 int owrx_engine_destroy(owrx_engine* e) {
     if (!e) return OWRX_EINVAL;
     hipSetDevice(e->device);
-    if (e->stream) hipStreamSynchronize(e->stream);
+    if (e->sA) hipStreamSynchronize(e->sA);
+    if (e->sB) hipStreamSynchronize(e->sB);
     for (auto& kv : e->chains) free_chain(kv.second.get());
     for (auto& kv : e->wfs) free_wf(kv.second.get());
     for (auto& g : e->groups) {
         dfree(g->d_taps);
         dfree(g->d_chains);
         dfree(g->d_partial);
+        hfree(g->h_chains);
     }
     dfree(e->d_win[0]);
     dfree(e->d_win[1]);
-    dfree(e->d_posts);
-    dfree(e->d_counts);
-    dfree(e->d_out);
-    dfree(e->d_sm);
-    dfree(e->d_dbg);
-    if (e->h_in) hipHostFree(e->h_in);
-    if (e->h_counts) hipHostFree(e->h_counts);
-    if (e->h_out) hipHostFree(e->h_out);
-    if (e->h_sm) hipHostFree(e->h_sm);
-    if (e->h_dbg) hipHostFree(e->h_dbg);
-    for (int i = 0; i < 6; ++i)
-        if (e->ev[i]) hipEventDestroy(e->ev[i]);
-    if (e->stream) hipStreamDestroy(e->stream);
+    hfree(e->h_in);
+    for (auto& s : e->slots) {
+        free_slot_staging(s);
+        for (hipEvent_t ev : {s.evA, s.evB, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1})
+            if (ev) hipEventDestroy(ev);
+    }
+    for (auto& r : e->rslots) {
+        if (r.stream) hipStreamSynchronize(r.stream);
+        if (r.evWf) hipEventDestroy(r.evWf);
+        if (r.evC) hipEventDestroy(r.evC);
+        if (r.stream) hipStreamDestroy(r.stream);
+    }
+    if (e->sA) hipStreamDestroy(e->sA);
+    if (e->sB) hipStreamDestroy(e->sB);
     delete e;
     return OWRX_OK;
 }
@@ -750,8 +948,8 @@ int owrx_commit(owrx_engine* e, int64_t n) {
     RC_FAIL(e, process_block(e, w + e->history, n));
     // carry the last `history` samples into the other window
     float2* o = e->d_win[1 - e->win_idx];
-    if (hipMemcpyAsync(o, w + n, sizeof(float2) * e->history, hipMemcpyDeviceToDevice,
-                       e->stream) != hipSuccess) {
+    if (hipMemcpyAsync(o, w + n, sizeof(float2) * e->history, hipMemcpyDeviceToDevice, e->sA) !=
+        hipSuccess) {
         e->failed = true;
         set_last_error("window carry copy failed");
         return OWRX_EIO;
@@ -766,9 +964,11 @@ int owrx_push_iq(owrx_engine* e, const float* iq, int64_t n) {
     int64_t done = 0;
     while (done < n) {
         const int64_t m = std::min(n - done, e->max_block);
+        // stream A is idle between blocks (process_block waits for it) except for the window
+        // carry copy, which does not touch h_in
         memcpy(e->h_in, iq + 2 * done, sizeof(float2) * m);
         float2* dst = e->d_win[e->win_idx] + e->history;
-        if (hipMemcpyAsync(dst, e->h_in, sizeof(float2) * m, hipMemcpyHostToDevice, e->stream) !=
+        if (hipMemcpyAsync(dst, e->h_in, sizeof(float2) * m, hipMemcpyHostToDevice, e->sA) !=
             hipSuccess) {
             e->failed = true;
             set_last_error("H2D copy failed");
@@ -783,7 +983,7 @@ int owrx_push_iq(owrx_engine* e, const float* iq, int64_t n) {
 
 int owrx_sync(owrx_engine* e) {
     ENGINE_GUARD(e);
-    HIPCHK(hipStreamSynchronize(e->stream));
+    RC_FAIL(e, drain_all(e));
     return OWRX_OK;
 }
 
@@ -804,6 +1004,7 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
         set_last_error("owrx_waterfall_create: hop too large for engine history");
         return OWRX_EINVAL;
     }
+    RC_FAIL(e, drain_all(e));
     auto w = std::make_unique<Waterfall>();
     w->N = fft_size;
     w->logn = logn;
@@ -838,6 +1039,7 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
     if (it == e->wfs.end() || every_n_samples <= 0 || avg_number < 0) return OWRX_EINVAL;
     Waterfall* w = it->second.get();
     if ((int64_t)kWfFramesPerGroup * every_n_samples + w->N > e->history) return OWRX_EINVAL;
+    RC_FAIL(e, drain_all(e));
     w->new_hop = every_n_samples;
     w->new_avg = std::max(1, avg_number);
     w->new_adpcm = adpcm ? 1 : 0;
@@ -846,9 +1048,10 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
         w->avg = w->new_avg;
         w->adpcm = w->new_adpcm;
         w->pending = false;
-        return wf_alloc_buffers(e, w);
+    } else {
+        w->pending = true;
     }
-    w->pending = true;
+    RC_FAIL(e, wf_alloc_buffers(e, w));  // sized for the larger of old/new settings
     return OWRX_OK;
 }
 
@@ -856,6 +1059,7 @@ int owrx_waterfall_destroy(owrx_engine* e, int handle) {
     ENGINE_GUARD(e);
     auto it = e->wfs.find(handle);
     if (it == e->wfs.end()) return OWRX_EINVAL;
+    RC_FAIL(e, drain_all(e));
     free_wf(it->second.get());
     e->wfs.erase(it);
     return OWRX_OK;
@@ -898,10 +1102,9 @@ static int chain_set_bandpass_taps(owrx_engine* e, Chain* c) {
         return OWRX_EINVAL;
     }
     std::vector<float> taps = firdes_bandpass_c(T, c->prm.bp_low, c->prm.bp_high);
+    RCCHK(drain_all(e));
     if (!c->d_bp_taps) HIPCHK(dalloc(&c->d_bp_taps, (size_t)kBpHist + 1));
-    HIPCHK(hipMemcpyAsync(c->d_bp_taps, taps.data(), sizeof(float) * 2 * T,
-                          hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(c->d_bp_taps, taps.data(), sizeof(float) * 2 * T, hipMemcpyHostToDevice));
     c->bp_ntaps = T;
     return OWRX_OK;
 }
@@ -923,6 +1126,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         set_last_error("owrx_chain_create: polyphase depth %d unsupported", (T + D - 1) / D);
         return OWRX_EINVAL;
     }
+    RC_FAIL(e, drain_all(e));
     // group lookup by (D, transition, cutoff)
     uint32_t tb, cb;
     memcpy(&tb, &p->transition, 4);
@@ -969,17 +1173,22 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     const int64_t scap = c->cap + p->sq_length + 16;
     c->out_cap = 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
     c->sm_cap = (int)(scap / p->sq_length + 4);
-    ChainState st;
-    memset(&st, 0, sizeof(st));
+    ChainStateP ps;
+    memset(&ps, 0, sizeof(ps));
+    ChainStateS ss;
+    memset(&ss, 0, sizeof(ss));
     AgcParams ap = agc_profile(p->agc_profile);
     if (p->agc_initial_gain >= 0) ap.initial_gain = p->agc_initial_gain;
-    st.agc.env = ap.reference / ap.initial_gain;
-    HIPCHK(dalloc(&c->d_state, 1));
-    HIPCHK(hipMemcpy(c->d_state, &st, sizeof(st), hipMemcpyHostToDevice));
+    ss.agc.env = ap.reference / ap.initial_gain;
+    HIPCHK(dalloc(&c->d_pstate, 1));
+    HIPCHK(dalloc(&c->d_sstate, 1));
+    HIPCHK(hipMemcpy(c->d_pstate, &ps, sizeof(ps), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_sstate, &ss, sizeof(ss), hipMemcpyHostToDevice));
     HIPCHK(dalloc(&c->d_ddc, (size_t)(kFdHist + c->cap)));
     HIPCHK(dalloc(&c->d_fd, (size_t)(kBpHist + c->cap)));
     HIPCHK(dalloc(&c->d_sq, (size_t)scap));
-    HIPCHK(dalloc(&c->d_dem, (size_t)scap));
+    HIPCHK(dalloc(&c->d_dem[0], (size_t)scap + 16));
+    HIPCHK(dalloc(&c->d_dem[1], (size_t)scap + 16));
     int rc = chain_set_bandpass_taps(e, c.get());
     if (rc) {
         free_chain(c.get());
@@ -998,6 +1207,8 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     ENGINE_GUARD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
+    RC_FAIL(e, drain_all(e));
+    HIPCHK(hipStreamSynchronize(e->sB));
     ChainGroup* g = it->second->group;
     g->members.erase(std::remove(g->members.begin(), g->members.end(), handle), g->members.end());
     free_chain(it->second.get());
@@ -1022,11 +1233,12 @@ int owrx_chain_set_bandpass(owrx_engine* e, int handle, int enabled, float low, 
     if (it == e->chains.end()) return OWRX_EINVAL;
     Chain* c = it->second.get();
     if (enabled && low >= high) return OWRX_EINVAL;
+    if (enabled && c->prm.bp_transition <= 0) return OWRX_EINVAL;
     c->prm.bandpass = enabled ? 1 : 0;
     c->prm.bp_low = low;
     c->prm.bp_high = high;
-    if (enabled && c->prm.bp_transition <= 0) return OWRX_EINVAL;
-    return chain_set_bandpass_taps(e, c);
+    RC_FAIL(e, chain_set_bandpass_taps(e, c));
+    return OWRX_OK;
 }
 
 int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level) {
@@ -1061,9 +1273,11 @@ int64_t owrx_chain_origin(owrx_engine* e, int handle) {
 
 int owrx_set_debug(owrx_engine* e, int enable) {
     ENGINE_GUARD(e);
+    RC_FAIL(e, drain_all(e));
     e->debug = enable != 0;
     e->post_cap = 0;  // force reallocation with debug staging
-    return ensure_post_capacity(e);
+    RC_FAIL(e, ensure_post_capacity(e));
+    return OWRX_OK;
 }
 
 int64_t owrx_chain_read_debug(owrx_engine* e, int handle, int stage, void* dst,

@@ -170,4 +170,52 @@ OWRX_DEV int adpcm_encode(AdpcmState& s, int sample) {
     return code;
 }
 
+// Same encoder with the step-table lookup taken off the dependency chain: the five possible
+// next steps (index -1, +2, +4, +6, +8, clamped) are read from an LDS copy of the table while
+// this sample's code is being formed, then selected by the code bits.  Bit-identical to
+// adpcm_encode.
+struct AdpcmFast {
+    int index;
+    int pred;
+    int step;
+};
+
+OWRX_DEV AdpcmFast adpcm_fast_init(AdpcmState s, const int16_t* T) {
+    return AdpcmFast{s.index, s.pred, (int)T[s.index]};
+}
+
+OWRX_DEV int adpcm_encode_fast(AdpcmFast& s, int sample, const int16_t* __restrict__ T) {
+    // branch-free: every decision is a mask / select (no exec-mask regions in the hot loops)
+    const int idx = s.index;
+    const int cm1 = T[max(idx - 1, 0)];
+    const int c2 = T[min(idx + 2, 88)];
+    const int c4 = T[min(idx + 4, 88)];
+    const int c6 = T[min(idx + 6, 88)];
+    const int c8 = T[min(idx + 8, 88)];
+    const int step = s.step;
+    int diff = sample - s.pred;
+    const int sgn = diff >> 31;        // -1 if negative
+    diff = (diff ^ sgn) - sgn;         // |diff|
+    int dq = step >> 3;
+    int ts = step;
+    const int m4 = -(int)(diff >= ts);
+    diff -= ts & m4;
+    dq += ts & m4;
+    ts >>= 1;
+    const int m2 = -(int)(diff >= ts);
+    diff -= ts & m2;
+    dq += ts & m2;
+    ts >>= 1;
+    const int m1 = -(int)(diff >= ts);
+    dq += ts & m1;
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    const int mag = (m4 & 4) | (m2 & 2) | (m1 & 1);
+    const int ni = m4 ? idx + 2 * ((mag & 3) + 1) : idx - 1;
+    const int hi_step = m2 ? (m1 ? c8 : c6) : (m1 ? c4 : c2);
+    s.step = m4 ? hi_step : cm1;
+    s.index = min(max(ni, 0), 88);
+    return mag | (sgn & 8);
+}
+
 }  // namespace owrx

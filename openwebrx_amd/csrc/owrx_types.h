@@ -32,26 +32,30 @@ struct DdcChain {
 };
 
 // ---- post-decimation chain state (device, persistent) -----------------------------------
-struct ChainState {
+// Owned by post_parallel (stream A).
+struct ChainStateP {
     int64_t ddc_count;     // DDC outputs consumed so far (chain-local)
     int64_t fd_next;       // next FractionalDecimator output index
     int64_t fd_count;      // samples emitted by FractionalDecimator (or passthrough) so far
+    int64_t sq_blocks;
     int32_t sq_pending;    // samples waiting for a full squelch block
     int32_t hang_ctr;
     int32_t flush_ctr;
-    int32_t has_left;      // ADPCM: one s16 sample waiting for its pair
-    int64_t sq_blocks;
-    int64_t adpcm_bytes;   // data bytes emitted (sync period bookkeeping)
+    int32_t pad;
     float2 fm_last;
+};
+// Owned by post_serial (stream B).
+struct ChainStateS {
+    int64_t adpcm_bytes;   // data bytes emitted (sync period bookkeeping)
     float deemph_y;
     float dc_xp, dc_yp;
     AgcState agc;
     AdpcmState adpcm;
-    int32_t left_sample;
-    int32_t pad;
+    int32_t has_left;      // ADPCM: one encoded nibble waiting for its pair
+    int32_t left_code;
 };
 
-// Static + per-step description of one chain for the post kernel.
+// Static + per-step description of one chain, shared by post_parallel and post_serial.
 struct ChainPost {
     // configuration
     int32_t demod;         // OWRX_DEMOD_*
@@ -65,11 +69,12 @@ struct ChainPost {
     float deemph_alpha, deemph_beta;
     AgcParams agc;
     // buffers
-    ChainState* state;
+    ChainStateP* pstate;
+    ChainStateS* sstate;
     float2* ddc_buf;       // [kFdHist + cap]
     float2* fd_buf;        // [kBpHist + cap]
     float2* sq_buf;        // [sq_len + cap]
-    float* dem_buf;        // [cap + sq_len]
+    float* dem;            // this step's demodulator output slot [cap + sq_len + 16]
     // this step
     const float2* partial; // group partial sums [nseg][group_chains][nk]
     int32_t nseg;
@@ -93,12 +98,12 @@ struct ChainPost {
     int64_t dbg_cap;
 };
 
-// Per-chain counters written by the post kernel for the host.
+// Per-chain counters written by the post kernels for the host (and n_sq for post_serial).
 struct ChainCounts {
     int64_t out_bytes;
     int32_t smeter;
     int32_t pad;
-    int64_t n_ddc, n_fd, n_bp, n_sq;  // debug stage counts
+    int64_t n_ddc, n_fd, n_bp, n_sq;  // stage sample counts this step
 };
 
 }  // namespace owrx

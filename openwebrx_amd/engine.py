@@ -13,6 +13,17 @@ _STAGE_DTYPE = {0: np.complex64, 1: np.complex64, 2: np.complex64, 3: np.complex
                 4: np.float32, 5: np.float32}
 
 
+_SCRATCH = {}
+
+
+def _scratch(nbytes):
+    """Reusable host buffer for ring reads (avoids a fresh multi-MB allocation per call)."""
+    b = _SCRATCH.get(nbytes)
+    if b is None:
+        b = _SCRATCH[nbytes] = np.empty(nbytes, dtype=np.uint8)
+    return b
+
+
 def device_count():
     n = lib.owrx_device_count()
     return n if n > 0 else 0
@@ -107,11 +118,21 @@ class Waterfall:
     def row_bytes(self):
         return check(lib.owrx_waterfall_row_bytes(self.engine.handle, self.id), "row_bytes")
 
-    def read(self, max_bytes=1 << 26):
-        buf = np.empty(max_bytes, dtype=np.uint8)
-        n = check(lib.owrx_waterfall_read(self.engine.handle, self.id, buf.ctypes.data, max_bytes),
-                  "owrx_waterfall_read")
-        return buf[:n].tobytes()
+    def read(self, max_bytes=None):
+        """Whole rows produced so far (or at most max_bytes worth of rows)."""
+        rb = self.row_bytes()
+        out = []
+        left = max_bytes if max_bytes is not None else 1 << 62
+        buf = _scratch(max(rb * 16, 1 << 20))
+        while left >= rb:
+            m = min(left, buf.size)
+            n = check(lib.owrx_waterfall_read(self.engine.handle, self.id, buf.ctypes.data, m),
+                      "owrx_waterfall_read")
+            if n <= 0:
+                break
+            out.append(buf[:n].tobytes())
+            left -= n
+        return b"".join(out)
 
     def read_rows(self):
         rb = self.row_bytes()
@@ -151,14 +172,25 @@ class Chain:
         check(lib.owrx_chain_set_squelch_level(self.engine.handle, self.id, float(level)),
               "squelch")
 
-    def read_audio(self, max_bytes=1 << 24):
-        buf = np.empty(max_bytes, dtype=np.uint8)
-        n = check(lib.owrx_chain_read_audio(self.engine.handle, self.id, buf.ctypes.data,
-                                            max_bytes), "read_audio")
-        return buf[:n].tobytes()
+    def read_audio(self, max_bytes=None):
+        """All audio bytes produced so far (or at most max_bytes)."""
+        out = []
+        left = max_bytes if max_bytes is not None else 1 << 62
+        buf = _scratch(1 << 20)
+        while left > 0:
+            m = min(left, buf.size)
+            n = check(lib.owrx_chain_read_audio(self.engine.handle, self.id, buf.ctypes.data, m),
+                      "read_audio")
+            if n <= 0:
+                break
+            out.append(buf[:n].tobytes())
+            left -= n
+            if n < m:
+                break
+        return b"".join(out)
 
     def read_smeter(self, max_values=1 << 16):
-        buf = np.empty(max_values, dtype=np.float32)
+        buf = _scratch(4 * max_values).view(np.float32)[:max_values]
         n = check(lib.owrx_chain_read_smeter(self.engine.handle, self.id, buf.ctypes.data,
                                              max_values), "read_smeter")
         return buf[:n].copy()

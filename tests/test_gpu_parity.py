@@ -121,6 +121,7 @@ def _wf(amd, iq, fs, N, hop, avg, adpcm, block):
     wf = eng.waterfall(N, hop, avg, adpcm=adpcm)
     for i in range(0, iq.size, block):
         eng.push(iq[i:i + block])
+    eng.sync()
     rows = wf.read_rows()
     eng.close()
     return rows
@@ -174,6 +175,7 @@ def _run_chains(amd, iq, fs, plist, block, debug=True):
         eng.push(iq[i:i + s])
         i += s
         k += 1
+    eng.sync()
     return eng, chains
 
 
@@ -238,4 +240,28 @@ def test_adpcm_chain_output_decodes(amd):
     agc = ch.read_debug(5)
     ref_bytes = oracle.adpcm_encode(oracle.convert_s16(agc), 1)
     assert data == ref_bytes[:len(data)] and len(ref_bytes) - len(data) <= 9
+    eng.close()
+
+
+@pytest.mark.parametrize("N,fs", [(4096, 2400000), (16384, 10000000)])
+def test_waterfall_adpcm_rows_bit_exact(amd, N, fs):
+    """The row-parallel speculative IMA-ADPCM encoder is bit-identical to the sequential
+    FftAdpcm restatement: two FftChains on one engine (float and ADPCM output) see the same
+    dB rows, and the ADPCM bytes equal oracle.fft_adpcm_row() of the float rows."""
+    from openwebrx_amd import synth
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+    avg = min(avg, 8)
+    n = hop * avg * 5 + N
+    iq, _ = synth.make_iq(fs, n, ["nfm", "am", "usb", "cw"])
+    eng = amd.Engine(fs, max_block=1 << 18)
+    wf_f = eng.waterfall(N, hop, avg, adpcm=False)
+    wf_a = eng.waterfall(N, hop, avg, adpcm=True)
+    for i in range(0, n, 1 << 18):
+        eng.push(iq[i:i + (1 << 18)])
+    eng.sync()
+    rf = wf_f.read_rows()
+    ra = wf_a.read_rows()
+    assert rf.shape[0] == ra.shape[0] == 5
+    for r in range(rf.shape[0]):
+        assert ra[r].tobytes() == oracle.fft_adpcm_row(rf[r])
     eng.close()
