@@ -84,12 +84,14 @@ def cpu_baseline(fs, n_fft, hop, avg, plist, seconds_target=15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--block", type=int, default=1 << 22)
     ap.add_argument("--chains", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-waterfall", action="store_true")
+    ap.add_argument("--no-timing", action="store_true",
+                    help="skip the per-kernel HIP-event brackets (roofline fields become null)")
     args = ap.parse_args()
 
     import torch
@@ -130,8 +132,9 @@ def main():
         stream = gen_stream_torch(torch, dev, fs, hist + total, modes, offs)
         base = stream.data_ptr() + 8 * hist
     else:
-        window = torch.empty(hist + block, dtype=torch.complex64, device=dev)
-        window.zero_()
+        # two windows [history | block], alternated: the engine reads block k's window until
+        # the next process call returns, so block k+1 is assembled in the other one
+        windows = [torch.zeros(hist + block, dtype=torch.complex64, device=dev) for _ in range(2)]
     torch.cuda.synchronize(dev)
 
     def drain():
@@ -143,9 +146,19 @@ def main():
             nbytes += len(wf.read())
         return nbytes
 
+    host_s = {"process": 0.0, "drain": 0.0}
+
     def step(i):
+        t0 = time.perf_counter()
+        n = _step(i)
+        host_s["drain"] += time.perf_counter() - t0
+        return n
+
+    def _step(i):
         if world == 1:
+            t0 = time.perf_counter()
             eng.process_device(base + 8 * i * block, block)
+            host_s["process"] += time.perf_counter() - t0
         else:
             if rank == 0:
                 blk = stream[hist + i * block: hist + (i + 1) * block]
@@ -153,36 +166,49 @@ def main():
                 torch.cuda.synchronize(dev)
                 eng.process_device(base + 8 * i * block, block)
             else:
-                dst = window[hist:hist + block]
+                w, prev = windows[i % 2], windows[(i + 1) % 2]
+                w[:hist].copy_(prev[block:block + hist])
+                dst = w[hist:hist + block]
                 dist.broadcast(dst, src=0)
                 torch.cuda.synchronize(dev)
                 eng.process_device(dst.data_ptr(), block)
-                window[:hist].copy_(window[block:block + hist].clone())
         return drain()
 
     for i in range(args.warmup):
         step(i)
+    # the Python driver's garbage collector stalls the host for milliseconds at times; keep it
+    # out of the timed region (the engine itself allocates nothing per block)
+    import gc
+    gc.collect()
+    gc.disable()
     eng.sync()
-    eng.set_timing(True)
+    eng.set_timing(not args.no_timing)
     s0 = eng.stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     out_bytes = 0
+    marks = []
     for i in range(args.warmup, nsteps):
         out_bytes += step(i)
+        marks.append(time.perf_counter() - t0)
     eng.sync()
+    marks.append(time.perf_counter() - t0)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    gc.enable()
     s1 = eng.stats()
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
+    print("host seconds over all steps: process_device %.4f, step total %.4f, wall %.4f"
+          % (host_s["process"], host_s["drain"], dt), file=sys.stderr)
+    print("step marks (ms): " + " ".join("%.2f" % (1e3 * m) for m in marks), file=sys.stderr)
     samples = args.steps * block
     value = world * samples / dt / 1e6
     ms_step = dt * 1e3 / args.steps
@@ -195,7 +221,8 @@ def main():
     nk_total = (s1["ddc_outputs"] - s0["ddc_outputs"]) / max(1, C)
     flops = C * nk_total * (4.0 * T + 6.0 * D)
     avg_launch_s = ddc_ms / 1e3 / max(1, launches)
-    achieved_tf = flops / max(1, launches) / avg_launch_s / 1e12 if launches else 0.0
+    achieved_tf = (flops / max(1, launches) / avg_launch_s / 1e12
+                   if launches and avg_launch_s > 0 else 0.0)
     wf_ms = s1["gpu_ms_waterfall"] - s0["gpu_ms_waterfall"]
     post_ms = s1["gpu_ms_post"] - s0["gpu_ms_post"]
     wf_launches = s1["waterfall_launches"] - s0["waterfall_launches"]

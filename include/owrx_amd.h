@@ -65,7 +65,9 @@ int64_t owrx_engine_max_block(owrx_engine* e);
  * Equivalent of Writer.write() on the wideband Buffer. */
 int owrx_push_iq(owrx_engine* e, const float* iq_cf32, int64_t nsamples);
 /* Device-resident cf32 block; iq_dev[-history, 0) must hold the previous samples of the stream
- * (e.g. a contiguous HBM recording, or an RCCL-broadcast window).  Zero-copy. */
+ * (e.g. a contiguous HBM recording, or an RCCL-broadcast window).  Zero-copy and asynchronous:
+ * the block (with its history) must stay unmodified until the next owrx_process_device /
+ * owrx_commit / owrx_push_iq / owrx_sync call on this engine has returned. */
 int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t nsamples);
 /* Device window slot for the next block (write there, e.g. with ncclBroadcast), then commit. */
 int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity);

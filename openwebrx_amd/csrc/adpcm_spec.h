@@ -1,0 +1,114 @@
+// adpcm_spec.h -- speculative segment-parallel IMA-ADPCM window encoder (exact), shared by
+// the waterfall row encoder (kernels_waterfall.hip).
+#pragma once
+#include "owrx_dev.h"
+
+namespace owrx {
+
+// Speculative segment-parallel IMA-ADPCM (exact).  IMA-ADPCM is a serial recurrence, but two
+// encoders started from different states on the same input reach the same (index, predictor)
+// state after a few samples and are identical from then on.  A window of up to kSpecWin
+// samples (staged in LDS) is split into segments, one thread each:
+//   pass 1: every segment encodes from a guessed state (segment 0 from the true state),
+//           storing its codes and its state trajectory;
+//   pass 2: a segment whose start differs from its predecessor's final state re-encodes from
+//           that state until its state equals the stored trajectory (the stored codes are
+//           exact from there on) or to its end (its trajectory / final state are replaced);
+//           Jacobi rounds until no segment re-runs.
+// The fixed point is the sequential trajectory, so codes are bit-identical to the serial
+// encoder (oracle orc_adpcm_encode / orc_fft_adpcm_row).
+constexpr int kSpecThreads = 256;
+
+OWRX_DEV uint32_t pack_state(const AdpcmFast& s) {
+    return ((uint32_t)s.index << 16) | ((uint32_t)s.pred & 0xffffu);
+}
+OWRX_DEV AdpcmFast unpack_state(uint32_t v, const int16_t* T) {
+    AdpcmFast s;
+    s.index = (int)(v >> 16);
+    s.pred = (int)(int16_t)(v & 0xffffu);
+    s.step = T[s.index];
+    return s;
+}
+
+template <int WIN>
+struct SpecLds {
+    uint32_t NS[kAdpcmTabEntries];  // adpcm_encode_tab successor table (16-B aligned rows)
+    int16_t x[WIN];
+    uint8_t code[WIN];
+    uint32_t traj[WIN];
+    uint32_t seg_start[kSpecThreads], seg_final[kSpecThreads];
+    int16_t T[96];
+    int any;
+};
+
+// Encodes L.x[0, n) from `start` (block-uniform).  Returns with L.code / L.traj filled.
+// Segments start from (index = `guess_index`, predictor = previous sample), or with
+// guess_index < 0 from the step index matching the local slope.
+template <int WIN>
+OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int guess_index,
+                                int min_seg) {
+    const int tid = threadIdx.x;
+    const int seg = max(min_seg, (((n + kSpecThreads - 1) / kSpecThreads) + 1) & ~1);
+    const int nseg = (n + seg - 1) / seg;
+    const int b0 = min(tid * seg, n), b1 = min(b0 + seg, n);
+    const int16_t* T = L.T;
+    // pass 1
+    if (tid < nseg) {
+        AdpcmFast st;
+        if (tid == 0) {
+            st = unpack_state(start, T);
+        } else if (guess_index >= 0) {
+            st = AdpcmFast{guess_index, (int)L.x[b0 - 1], (int)T[guess_index]};
+        } else {
+            // predictor = previous sample, step index from the local slope
+            const int d = abs((int)L.x[b0 - 1] - (int)L.x[b0 - 2]);
+            int lo = 0, hi = 88;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (T[mid] < d) lo = mid + 1; else hi = mid;
+            }
+            st = AdpcmFast{lo, (int)L.x[b0 - 1], (int)T[lo]};
+        }
+        L.seg_start[tid] = pack_state(st);
+        for (int t = b0; t < b1; ++t) {
+            L.code[t] = (uint8_t)adpcm_encode_tab(st, L.x[t], L.NS);
+            L.traj[t] = pack_state(st);
+        }
+        L.seg_final[tid] = pack_state(st);
+    }
+    __syncthreads();
+    // pass 2
+    for (int round = 0; round < nseg; ++round) {
+        if (tid == 0) L.any = 0;
+        uint32_t want = 0, fin = 0;
+        bool rerun = false;
+        if (tid < nseg && tid > 0) {
+            want = L.seg_final[tid - 1];
+            rerun = want != L.seg_start[tid];
+            fin = L.seg_final[tid];
+        }
+        __syncthreads();  // every start was read before any final changes
+        if (rerun) {
+            AdpcmFast r = unpack_state(want, T);
+            bool merged = false;
+            for (int t = b0; t < b1; ++t) {
+                L.code[t] = (uint8_t)adpcm_encode_tab(r, L.x[t], L.NS);
+                const uint32_t ps = pack_state(r);
+                if (ps == L.traj[t]) {
+                    merged = true;
+                    break;
+                }
+                L.traj[t] = ps;
+            }
+            if (!merged) fin = pack_state(r);
+            L.seg_start[tid] = want;
+            L.seg_final[tid] = fin;
+            L.any = 1;
+        }
+        __syncthreads();
+        if (!L.any) break;
+        __syncthreads();
+    }
+}
+
+}  // namespace owrx

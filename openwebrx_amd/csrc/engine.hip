@@ -46,7 +46,7 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st);
 hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, int row_bytes,
-                           uint8_t* codes, uint32_t* traj, hipStream_t st);
+                           hipStream_t st);
 hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_end,
                       const float* taps_poly, const DdcChain* chains, int nchains, int D,
                       int64_t k_begin, int nk, int nseg, float2* partial, hipStream_t st);
@@ -56,11 +56,14 @@ hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts
                                 hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, int output, int debug, hipStream_t st);
+hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
+                              int nsel, hipStream_t st);
 
-constexpr int kWfFramesPerGroup = 4;
+constexpr int kWfFramesPerGroup = 1;
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
-constexpr int kRowSlots = 2;  // waterfall row-encoding blocks in flight (streams R0, R1)
+constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
+constexpr int kRowSlots = 2;  // waterfall row blocks in flight (encoded in order on stream R)
 
 #define HIPCHK(expr)                                                                    \
     do {                                                                                \
@@ -143,6 +146,8 @@ struct Waterfall {
     float2* d_tw = nullptr;
     float* d_partial = nullptr;
     int partial_groups = 0;
+    WfGroup* h_groups[2] = {};  // pinned copy sources, per block parity
+    WfRow* h_rows[2] = {};
     float* d_carry[2] = {nullptr, nullptr};
     WfGroup* d_groups = nullptr;
     WfRow* d_rows = nullptr;
@@ -151,8 +156,6 @@ struct Waterfall {
     int16_t* d_s16[kRowSlots] = {};
     float* d_f32[kRowSlots] = {};
     uint8_t* d_bytes[kRowSlots] = {};
-    uint8_t* d_codes[kRowSlots] = {};   // row-parallel ADPCM scratch
-    uint32_t* d_traj[kRowSlots] = {};
     uint8_t* h_bytes[kRowSlots] = {};
     int pend_rows[kRowSlots] = {};
     int pend_adpcm[kRowSlots] = {};
@@ -171,10 +174,10 @@ struct ChainGroup {
     int64_t k_next = 0;
     DdcChain* d_chains = nullptr;
     int chains_cap = 0;
-    float2* d_partial = nullptr;
+    float2* d_partial[kSlots] = {};  // DDC segment partials, per slot (A writes, B reads)
     size_t partial_elems = 0;
     int nseg = 1;
-    DdcChain* h_chains = nullptr;  // pinned copy source
+    DdcChain* h_chains[2] = {};  // pinned copy sources, per block parity
     int h_cap = 0;
 };
 
@@ -196,7 +199,8 @@ struct Chain {
     float2* d_ddc = nullptr;
     float2* d_fd = nullptr;
     float2* d_sq = nullptr;
-    float* d_dem[2] = {nullptr, nullptr};
+    float* d_dem[kSlots] = {};
+    int16_t* d_s16[kSlots] = {};  // ADPCM encoder input, per slot (B -> C)
     float2* d_bp_taps = nullptr;
     int bp_ntaps = 0;
     int64_t cap = 0;      // per-step sample capacity of stage buffers
@@ -224,16 +228,18 @@ struct Slot {  // one block's outputs in flight on streams B / C
     uint8_t* d_dbg = nullptr;
     uint8_t* h_dbg = nullptr;
     hipEvent_t evA = nullptr;   // stream A finished this block's post_parallel
-    hipEvent_t evB = nullptr;   // stream B finished (audio copied to host)
-    // timing brackets: A: [a0 wf a1 ddc a2 post_parallel a3]; B: [b0 post_serial b1]
+    hipEvent_t evF = nullptr;   // stream B finished this block's post_serial_front
+    hipEvent_t evB = nullptr;   // stream C finished (audio copied to host)
+    // timing brackets: A: [a0 waterfall + descriptors a1 DDC kernels a2 .. a3];
+    // B/C: [b0 post_parallel, post_serial_front .. chain_adpcm b1]
     hipEvent_t a0 = nullptr, a1 = nullptr, a2 = nullptr, a3 = nullptr;
     hipEvent_t b0 = nullptr, b1 = nullptr;
     bool timed = false;
     bool timed_wf = false;
 };
 
-struct RowSlot {  // one block's waterfall rows being encoded / copied on its own stream
-    hipStream_t stream = nullptr;
+struct RowSlot {  // one block's waterfall rows being encoded / copied on stream R
+    hipStream_t stream = nullptr;  // = engine sR
     hipEvent_t evWf = nullptr;  // stream A finished the block's finalize
     hipEvent_t evC = nullptr;   // rows copied to host
     bool pending = false;
@@ -245,12 +251,16 @@ using namespace owrx;
 
 struct owrx_engine {
     int device = 0;
-    hipStream_t sA = nullptr, sB = nullptr;
+    // A: waterfall FFT + DDC + post_parallel; B: post_serial_front; C: ADPCM + output copies;
+    // R: waterfall row encoding + copies.  Four streams = the four hardware queues HIP gives a
+    // process (GPU_MAX_HW_QUEUES), so no two of them serialise on a shared queue.
+    hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sR = nullptr;
     double samp_rate = 0;
     int64_t max_block = 0;
     int64_t history = kDefaultHistory;
     int64_t pos = 0;  // absolute samples processed
     int64_t block_index = 0;
+    int64_t slot_tail = 0;  // oldest block whose outputs are not yet in the host rings
     bool failed = false;
     bool debug = false;
     bool timing = false;
@@ -258,7 +268,9 @@ struct owrx_engine {
     // push-path window (ping-pong): [history | block]
     float2* d_win[2] = {nullptr, nullptr};
     int win_idx = 0;
-    float* h_in = nullptr;  // pinned staging for push_iq
+    float* h_in = nullptr;  // pinned staging for push_iq, two blocks (per block parity)
+    hipEvent_t evIn = nullptr;  // end of the last block's stream-A work (input reusable)
+    bool in_pending = false;
     std::map<int, std::unique_ptr<Waterfall>> wfs;
     std::map<int, std::unique_ptr<Chain>> chains;
     std::vector<std::unique_ptr<ChainGroup>> groups;
@@ -266,7 +278,7 @@ struct owrx_engine {
     // post staging (all chains), per block parity
     int post_cap = 0;
     int64_t out_stride = 0, sm_stride = 0, dbg_stride = 0;
-    Slot slots[2];
+    Slot slots[kSlots];
     RowSlot rslots[kRowSlots];
     int64_t row_head = 0;  // next row slot to fill
     int64_t row_tail = 0;  // oldest row slot not yet drained
@@ -290,8 +302,8 @@ static void free_chain(Chain* c) {
     dfree(c->d_ddc);
     dfree(c->d_fd);
     dfree(c->d_sq);
-    dfree(c->d_dem[0]);
-    dfree(c->d_dem[1]);
+    for (int i = 0; i < kSlots; ++i) dfree(c->d_dem[i]);
+    for (int i = 0; i < kSlots; ++i) dfree(c->d_s16[i]);
     dfree(c->d_bp_taps);
 }
 
@@ -303,12 +315,14 @@ static void free_wf(Waterfall* w) {
     dfree(w->d_carry[1]);
     dfree(w->d_groups);
     dfree(w->d_rows);
+    for (int b = 0; b < 2; ++b) {
+        hfree(w->h_groups[b]);
+        hfree(w->h_rows[b]);
+    }
     for (int s = 0; s < kRowSlots; ++s) {
         dfree(w->d_s16[s]);
         dfree(w->d_f32[s]);
         dfree(w->d_bytes[s]);
-        dfree(w->d_codes[s]);
-        dfree(w->d_traj[s]);
         hfree(w->h_bytes[s]);
     }
 }
@@ -408,14 +422,30 @@ static int drain_rows(owrx_engine* e, bool block, int keep) {
     return OWRX_OK;
 }
 
+// Drain finished chain slots in block order; with `block` wait until `keep` remain in flight.
+static int drain_slots(owrx_engine* e, bool block, int keep) {
+    while (e->slot_tail < e->block_index) {
+        const int si = (int)(e->slot_tail % kSlots);
+        Slot& s = e->slots[si];
+        const bool must = block && (e->block_index - e->slot_tail) > keep;
+        if (!must) {
+            hipEvent_t ev = s.chains_pending ? s.evB : (s.timed ? s.a3 : nullptr);
+            if (ev) {
+                hipError_t q = hipEventQuery(ev);
+                if (q == hipErrorNotReady) break;
+                HIPCHK(q);
+            }
+        }
+        RCCHK(drain_slot(e, si));
+        e->slot_tail++;
+    }
+    return OWRX_OK;
+}
+
 static int drain_all(owrx_engine* e) {
     HIPCHK(hipStreamSynchronize(e->sA));
     RCCHK(drain_rows(e, true, 0));
-    for (int i = 0; i < 2; ++i) {
-        const int si = (int)((e->block_index + i) & 1);  // oldest first
-        RCCHK(drain_slot(e, si));
-    }
-    return OWRX_OK;
+    return drain_slots(e, true, 0);
 }
 
 static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
@@ -429,20 +459,24 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
         dfree(w->d_groups);
         HIPCHK(dalloc(&w->d_partial, (size_t)groups * w->N));
         HIPCHK(dalloc(&w->d_groups, (size_t)groups));
+        for (int b = 0; b < 2; ++b) {
+            hfree(w->h_groups[b]);
+            HIPCHK(halloc(&w->h_groups[b], (size_t)groups));
+        }
         w->partial_groups = groups;
     }
     if (rows > w->rows_cap) {
         dfree(w->d_rows);
         HIPCHK(dalloc(&w->d_rows, (size_t)rows + 1));
+        for (int b = 0; b < 2; ++b) {
+            hfree(w->h_rows[b]);
+            HIPCHK(halloc(&w->h_rows[b], (size_t)rows + 1));
+        }
         for (int s = 0; s < kRowSlots; ++s) {
             dfree(w->d_s16[s]);
             dfree(w->d_f32[s]);
             dfree(w->d_bytes[s]);
-            dfree(w->d_codes[s]);
-            dfree(w->d_traj[s]);
             hfree(w->h_bytes[s]);
-            HIPCHK(dalloc(&w->d_codes[s], (size_t)rows * (w->N + 10)));
-            HIPCHK(dalloc(&w->d_traj[s], (size_t)rows * (w->N + 10)));
             HIPCHK(dalloc(&w->d_s16[s], (size_t)rows * w->N));
             HIPCHK(dalloc(&w->d_f32[s], (size_t)rows * w->N));
             HIPCHK(dalloc(&w->d_bytes[s], (size_t)rows * 4 * w->N));
@@ -469,13 +503,13 @@ static int ensure_post_capacity(owrx_engine* e) {
     e->out_stride = (need_out + 255) & ~(int64_t)255;
     e->sm_stride = need_sm;
     e->dbg_stride = e->debug ? (need_dbg + 255) & ~(int64_t)255 : 0;
-    for (int si = 0; si < 2; ++si) {
+    for (int si = 0; si < kSlots; ++si) {
         Slot& s = e->slots[si];
         free_slot_staging(s);
         HIPCHK(dalloc(&s.d_posts, cap));
         HIPCHK(halloc(&s.h_posts, cap));
-        HIPCHK(dalloc(&s.d_sel, cap));
-        HIPCHK(halloc(&s.h_sel, cap));
+        HIPCHK(dalloc(&s.d_sel, (size_t)cap + 64 * 3 * 4));  // + demodulator-run padding
+        HIPCHK(halloc(&s.h_sel, (size_t)cap + 64 * 3 * 4));
         HIPCHK(dalloc(&s.d_counts, cap));
         HIPCHK(dalloc(&s.d_out, (size_t)cap * e->out_stride));
         HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
@@ -497,10 +531,12 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     if (n > g->chains_cap) {
         RCCHK(drain_all(e));
         dfree(g->d_chains);
-        hfree(g->h_chains);
+        hfree(g->h_chains[0]);
+        hfree(g->h_chains[1]);
         g->chains_cap = std::max(n, 2 * g->chains_cap);
         HIPCHK(dalloc(&g->d_chains, (size_t)g->chains_cap));
-        HIPCHK(halloc(&g->h_chains, (size_t)g->chains_cap));
+        HIPCHK(halloc(&g->h_chains[0], (size_t)g->chains_cap));
+        HIPCHK(halloc(&g->h_chains[1], (size_t)g->chains_cap));
     }
     const int64_t nk_max = e->max_block / g->D + 4;
     // segments: enough waves to fill 256 CUs x 4 SIMDs x ~4 waves
@@ -511,14 +547,17 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     const int64_t ntg = ((nk_max + R - 1) / R + tpw - 1) / tpw;
     const int64_t ncg = (n + cpw - 1) / cpw;
     const int64_t base = std::max<int64_t>(1, ntg * ncg);
-    int nseg = (int)std::min<int64_t>(std::max<int64_t>(1, (4096 + base - 1) / base),
-                                      std::max(1, g->D / 8));
+    // each segment is one 4-wave workgroup per tile group (phases split across its waves)
+    int nseg = (int)std::min<int64_t>(std::max<int64_t>(1, (1024 + base - 1) / base),
+                                      std::max(1, g->D / 32));
     nseg = ddc_segments(g->D, nseg);
     const size_t need = (size_t)nseg * std::max(1, n) * nk_max;
     if (need > g->partial_elems) {
         RCCHK(drain_all(e));
-        dfree(g->d_partial);
-        HIPCHK(dalloc(&g->d_partial, need));
+        for (int i = 0; i < kSlots; ++i) {
+            dfree(g->d_partial[i]);
+            HIPCHK(dalloc(&g->d_partial[i], need));
+        }
         g->partial_elems = need;
     }
     g->nseg = nseg;
@@ -586,9 +625,12 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         w->rowdesc.push_back(r);
     }
     if (w->groups.empty()) return OWRX_OK;
-    HIPCHK(hipMemcpyAsync(w->d_groups, w->groups.data(), sizeof(WfGroup) * w->groups.size(),
+    const int bp = (int)(e->block_index & 1);
+    memcpy(w->h_groups[bp], w->groups.data(), sizeof(WfGroup) * w->groups.size());
+    memcpy(w->h_rows[bp], w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size());
+    HIPCHK(hipMemcpyAsync(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(),
                           hipMemcpyHostToDevice, e->sA));
-    HIPCHK(hipMemcpyAsync(w->d_rows, w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size(),
+    HIPCHK(hipMemcpyAsync(w->d_rows, w->h_rows[bp], sizeof(WfRow) * w->rowdesc.size(),
                           hipMemcpyHostToDevice, e->sA));
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(),
                          w->d_window, w->d_tw, w->d_partial, e->sA));
@@ -609,12 +651,19 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
 }
 
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
+    // the previous block's stream-A work must be done before its input / descriptors are
+    // reused; waiting here (not at the end of that block) lets the caller's host work overlap it
+    if (e->in_pending) {
+        HIPCHK(hipEventSynchronize(e->evIn));
+        e->in_pending = false;
+    }
+    const int bp = (int)(e->block_index & 1);
     const int64_t blk_start = e->pos;
     const int64_t blk_end = e->pos + n;
-    const int si = (int)(e->block_index & 1);
+    const int si = (int)(e->block_index % kSlots);
     Slot& S = e->slots[si];
-    // the slot's previous block (k-2) must be drained before its buffers are reused
-    RCCHK(drain_slot(e, si));
+    // the slot's previous block (k - kSlots) must be drained before its buffers are reused
+    RCCHK(drain_slots(e, true, kSlots - 1));
     const bool timed = e->timing;
     if (timed) HIPCHK(hipEventRecord(S.a0, e->sA));
 
@@ -640,7 +689,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
                 if (w->pend_adpcm[ri]) {
                     HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
-                                           w->d_codes[ri], w->d_traj[ri], R.stream));
+                                           R.stream));
                     HIPCHK(hipMemcpyAsync(w->h_bytes[ri], w->d_bytes[ri], rb * nr,
                                           hipMemcpyDeviceToHost, R.stream));
                 } else {
@@ -653,22 +702,22 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             e->row_head++;
         }
     }
-    if (timed) {
-        HIPCHK(hipEventRecord(S.a1, e->sA));
-        S.timed_wf = !e->wfs.empty();
-    }
-
-    // ---- chains: DDC per group (A), post_parallel (A), post_serial + copies (B)
+    // ---- chains: DDC per group (A); post_parallel + post_serial_front (B); ADPCM + copies (C)
     e->posts.clear();
     S.post_ids.clear();
-    for (auto& gp : e->groups) {
+    struct GroupWork {
+        ChainGroup* g;
+        int64_t k_end;
+        int nk;
+    };
+    std::vector<GroupWork> work;
+    for (auto& gp : e->groups) {  // descriptors first, so the DDC bracket holds only kernels
         ChainGroup* g = gp.get();
         if (g->members.empty()) continue;
         if (blk_end < g->T) continue;
         const int64_t k_end = (blk_end - g->T) / g->D + 1;
         const int64_t nk64 = k_end - g->k_next;
         if (nk64 <= 0) continue;
-        const int nk = (int)nk64;
         for (size_t i = 0; i < g->members.size(); ++i) {
             Chain* c = e->chains[g->members[i]].get();
             if (c->rate_pending) {  // retune at output boundary k_next (phase continuous)
@@ -679,16 +728,26 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 c->rate_fx = rate_to_fx(c->rate);
                 c->rate_pending = false;
             }
-            DdcChain& d = g->h_chains[i];
+            DdcChain& d = g->h_chains[bp][i];
             d.rate_fx = c->rate_fx;
             d.wD = rate_rotator(c->rate, g->D);
             d.n0 = c->n0;
             d.P0 = c->P0;
         }
-        HIPCHK(hipMemcpyAsync(g->d_chains, g->h_chains, sizeof(DdcChain) * g->members.size(),
+        HIPCHK(hipMemcpyAsync(g->d_chains, g->h_chains[bp], sizeof(DdcChain) * g->members.size(),
                               hipMemcpyHostToDevice, e->sA));
+        work.push_back(GroupWork{g, k_end, (int)nk64});
+    }
+    if (timed) {
+        HIPCHK(hipEventRecord(S.a1, e->sA));
+        S.timed_wf = !e->wfs.empty();
+    }
+    for (const GroupWork& gw : work) {
+        ChainGroup* g = gw.g;
+        const int64_t k_end = gw.k_end;
+        const int nk = gw.nk;
         HIPCHK(launch_ddc(g->P, blk, blk_start, blk_end, g->d_taps, g->d_chains,
-                          (int)g->members.size(), g->D, g->k_next, nk, g->nseg, g->d_partial,
+                          (int)g->members.size(), g->D, g->k_next, nk, g->nseg, g->d_partial[si],
                           e->sA));
         e->stats.ddc_launches++;
         for (size_t i = 0; i < g->members.size(); ++i) {
@@ -719,7 +778,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.fd_buf = c->d_fd;
             p.sq_buf = c->d_sq;
             p.dem = c->d_dem[si];
-            p.partial = g->d_partial;
+            p.s16 = c->d_s16[si];
+            p.partial = g->d_partial[si];
             p.nseg = g->nseg;
             p.group_chains = (int)g->members.size();
             p.chain_in_group = (int)i;
@@ -750,50 +810,71 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const int np = (int)e->posts.size();
     if (timed) HIPCHK(hipEventRecord(S.a2, e->sA));
     if (np > 0) {
-        memcpy(S.h_posts, e->posts.data(), sizeof(ChainPost) * np);
-        HIPCHK(hipMemcpyAsync(S.d_posts, S.h_posts, sizeof(ChainPost) * np,
-                              hipMemcpyHostToDevice, e->sA));
-        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
+        // stream B: post_parallel + post_serial_front, behind this block's DDC
         HIPCHK(hipEventRecord(S.evA, e->sA));
         HIPCHK(hipStreamWaitEvent(e->sB, S.evA, 0));
-        // one post_serial instantiation per output format present (S16 / ADPCM / F32)
-        int nsel[3] = {0, 0, 0};
-        for (int i = 0; i < np; ++i) nsel[e->posts[i].output]++;
-        int off[3] = {0, nsel[0], nsel[0] + nsel[1]};
-        int fill[3] = {off[0], off[1], off[2]};
-        for (int i = 0; i < np; ++i) S.h_sel[fill[e->posts[i].output]++] = i;
-        HIPCHK(hipMemcpyAsync(S.d_sel, S.h_sel, sizeof(int) * np, hipMemcpyHostToDevice, e->sB));
+        memcpy(S.h_posts, e->posts.data(), sizeof(ChainPost) * np);
+        HIPCHK(hipMemcpyAsync(S.d_posts, S.h_posts, sizeof(ChainPost) * np,
+                              hipMemcpyHostToDevice, e->sB));
         if (timed) HIPCHK(hipEventRecord(S.b0, e->sB));
+        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sB));
+        // one post_serial_front launch per output format present (S16 / ADPCM / F32); within
+        // a format the chains are ordered by demodulator and every demodulator's run is padded
+        // to whole 64-lane workgroups (-1 = idle lane), so each wave has a uniform demodulator
+        int nsel[3] = {0, 0, 0}, off[3] = {0, 0, 0};
+        int nfill = 0;
+        for (int o = 0; o < 3; ++o) {
+            off[o] = nfill;
+            for (int dm = 0; dm < 4; ++dm) {
+                int run = 0;
+                for (int i = 0; i < np; ++i)
+                    if (e->posts[i].output == o && e->posts[i].demod == dm) {
+                        S.h_sel[nfill++] = i;
+                        run++;
+                    }
+                while (run % 64) {
+                    S.h_sel[nfill++] = -1;
+                    run++;
+                }
+            }
+            nsel[o] = nfill - off[o];
+        }
+        HIPCHK(hipMemcpyAsync(S.d_sel, S.h_sel, sizeof(int) * nfill, hipMemcpyHostToDevice,
+                              e->sB));
         const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
         for (int o = 0; o < 3; ++o)
             HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o], nsel[o], o, dbg,
                                       e->sB));
-        if (timed) HIPCHK(hipEventRecord(S.b1, e->sB));
+        HIPCHK(hipEventRecord(S.evF, e->sB));
+        // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host
+        HIPCHK(hipStreamWaitEvent(e->sC, S.evF, 0));
+        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + off[1], nsel[1], e->sC));
+        if (timed) HIPCHK(hipEventRecord(S.b1, e->sC));
         HIPCHK(hipMemcpyAsync(S.h_counts, S.d_counts, sizeof(ChainCounts) * np,
-                              hipMemcpyDeviceToHost, e->sB));
+                              hipMemcpyDeviceToHost, e->sC));
         HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, (size_t)np * e->out_stride,
-                              hipMemcpyDeviceToHost, e->sB));
+                              hipMemcpyDeviceToHost, e->sC));
         HIPCHK(hipMemcpyAsync(S.h_sm, S.d_sm, sizeof(float) * np * e->sm_stride,
-                              hipMemcpyDeviceToHost, e->sB));
+                              hipMemcpyDeviceToHost, e->sC));
         S.debug = e->debug && S.d_dbg;
         if (S.debug)
             HIPCHK(hipMemcpyAsync(S.h_dbg, S.d_dbg, (size_t)np * kDebugStages * e->dbg_stride,
-                                  hipMemcpyDeviceToHost, e->sB));
-        HIPCHK(hipEventRecord(S.evB, e->sB));
+                                  hipMemcpyDeviceToHost, e->sC));
+        HIPCHK(hipEventRecord(S.evB, e->sC));
         S.chains_pending = true;
     }
     if (timed) {
         HIPCHK(hipEventRecord(S.a3, e->sA));
         S.timed = true;
     }
-    // the input block and the host-side descriptors are free once stream A is done
-    HIPCHK(hipStreamSynchronize(e->sA));
+    HIPCHK(hipEventRecord(e->evIn, e->sA));
+    e->in_pending = true;
     e->pos = blk_end;
     e->stats.samples_in += n;
     e->stats.blocks++;
     e->block_index++;
-    // drain the previous block (its B work overlapped this block's A work) and any rows done
-    RCCHK(drain_slot(e, (int)(e->block_index & 1)));
+    // collect whatever earlier blocks have finished (B / C / R work overlaps later blocks)
+    RCCHK(drain_slots(e, false, 0));
     return drain_rows(e, false, 0);
 }
 
@@ -857,19 +938,20 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
         owrx_engine_destroy(e);
         return OWRX_EIO;
     };
-    // A, B, R0, R1: four streams = the four hardware queues HIP gives a process
-    // (GPU_MAX_HW_QUEUES), so no two of them serialise on a shared queue
     if (hipStreamCreateWithFlags(&e->sA, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->sB, hipStreamNonBlocking) != hipSuccess)
+        hipStreamCreateWithFlags(&e->sB, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->sC, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->sR, hipStreamNonBlocking) != hipSuccess)
         return fail("stream");
     for (auto& r : e->rslots) {
-        if (hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
+        r.stream = e->sR;
+        if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
             return fail("row stream");
     }
     for (auto& s : e->slots) {
         if (hipEventCreateWithFlags(&s.evA, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.evF, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.evB, hipEventDisableTiming) != hipSuccess ||
             hipEventCreate(&s.a0) != hipSuccess || hipEventCreate(&s.a1) != hipSuccess ||
             hipEventCreate(&s.a2) != hipSuccess || hipEventCreate(&s.a3) != hipSuccess ||
@@ -879,7 +961,9 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
     for (int i = 0; i < 2; ++i)
         if (dalloc(&e->d_win[i], (size_t)(e->history + max_block)) != hipSuccess)
             return fail("window");
-    if (halloc(&e->h_in, 2 * (size_t)max_block) != hipSuccess) return fail("pinned input");
+    if (halloc(&e->h_in, 4 * (size_t)max_block) != hipSuccess) return fail("pinned input");
+    if (hipEventCreateWithFlags(&e->evIn, hipEventDisableTiming) != hipSuccess)
+        return fail("event");
     *out = e;
     return OWRX_OK;
 }
@@ -887,32 +971,32 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
 int owrx_engine_destroy(owrx_engine* e) {
     if (!e) return OWRX_EINVAL;
     hipSetDevice(e->device);
-    if (e->sA) hipStreamSynchronize(e->sA);
-    if (e->sB) hipStreamSynchronize(e->sB);
+    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR})
+        if (st) hipStreamSynchronize(st);
     for (auto& kv : e->chains) free_chain(kv.second.get());
     for (auto& kv : e->wfs) free_wf(kv.second.get());
     for (auto& g : e->groups) {
         dfree(g->d_taps);
         dfree(g->d_chains);
-        dfree(g->d_partial);
-        hfree(g->h_chains);
+        for (int i = 0; i < kSlots; ++i) dfree(g->d_partial[i]);
+        hfree(g->h_chains[0]);
+        hfree(g->h_chains[1]);
     }
     dfree(e->d_win[0]);
     dfree(e->d_win[1]);
     hfree(e->h_in);
+    if (e->evIn) hipEventDestroy(e->evIn);
     for (auto& s : e->slots) {
         free_slot_staging(s);
-        for (hipEvent_t ev : {s.evA, s.evB, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1})
+        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1})
             if (ev) hipEventDestroy(ev);
     }
     for (auto& r : e->rslots) {
-        if (r.stream) hipStreamSynchronize(r.stream);
         if (r.evWf) hipEventDestroy(r.evWf);
         if (r.evC) hipEventDestroy(r.evC);
-        if (r.stream) hipStreamDestroy(r.stream);
     }
-    if (e->sA) hipStreamDestroy(e->sA);
-    if (e->sB) hipStreamDestroy(e->sB);
+    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR})
+        if (st) hipStreamDestroy(st);
     delete e;
     return OWRX_OK;
 }
@@ -964,11 +1048,12 @@ int owrx_push_iq(owrx_engine* e, const float* iq, int64_t n) {
     int64_t done = 0;
     while (done < n) {
         const int64_t m = std::min(n - done, e->max_block);
-        // stream A is idle between blocks (process_block waits for it) except for the window
-        // carry copy, which does not touch h_in
-        memcpy(e->h_in, iq + 2 * done, sizeof(float2) * m);
+        // staging half (block parity) last used two blocks ago: its copy finished before that
+        // block's stream-A work, which process_block waited for at the start of the last block
+        float* hb = e->h_in + 2 * (e->block_index & 1) * e->max_block;
+        memcpy(hb, iq + 2 * done, sizeof(float2) * m);
         float2* dst = e->d_win[e->win_idx] + e->history;
-        if (hipMemcpyAsync(dst, e->h_in, sizeof(float2) * m, hipMemcpyHostToDevice, e->sA) !=
+        if (hipMemcpyAsync(dst, hb, sizeof(float2) * m, hipMemcpyHostToDevice, e->sA) !=
             hipSuccess) {
             e->failed = true;
             set_last_error("H2D copy failed");
@@ -1187,8 +1272,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     HIPCHK(dalloc(&c->d_ddc, (size_t)(kFdHist + c->cap)));
     HIPCHK(dalloc(&c->d_fd, (size_t)(kBpHist + c->cap)));
     HIPCHK(dalloc(&c->d_sq, (size_t)scap));
-    HIPCHK(dalloc(&c->d_dem[0], (size_t)scap + 16));
-    HIPCHK(dalloc(&c->d_dem[1], (size_t)scap + 16));
+    // slack: the serial kernels read whole 64-sample chunks / 8-sample prefetches unguarded
+    for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_dem[i], (size_t)scap + 160));
+    for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_s16[i], (size_t)scap + 160));
     int rc = chain_set_bandpass_taps(e, c.get());
     if (rc) {
         free_chain(c.get());
@@ -1209,6 +1295,7 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     if (it == e->chains.end()) return OWRX_EINVAL;
     RC_FAIL(e, drain_all(e));
     HIPCHK(hipStreamSynchronize(e->sB));
+    HIPCHK(hipStreamSynchronize(e->sC));
     ChainGroup* g = it->second->group;
     g->members.erase(std::remove(g->members.begin(), g->members.end(), handle), g->members.end());
     free_chain(it->second.get());

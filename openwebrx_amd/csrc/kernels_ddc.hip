@@ -13,13 +13,16 @@
 // a per-lane rotator, seeded exactly from 64-bit fixed-point phase once per phase and advanced
 // by exp(j 2 pi D rate) per sample) and then feeds up to P accumulators: ~27 complex x real
 // MACs (54 FMAs) per load, so the kernel is FP32-VALU bound, not HBM bound.
-// Phases are split into `nseg` segments across workgroups to fill the chip; the post kernel
-// adds the segment partials in a fixed order (deterministic).
+// Phases are split into `nseg` segments across workgroups to fill the chip, each segment four
+// ways across the waves of its workgroup (reduced through LDS); the post kernel adds the
+// segment partials in a fixed order (deterministic).
 #include <type_traits>
 
 #include "owrx_types.h"
 
 namespace owrx {
+
+typedef float f2v __attribute__((ext_vector_type(2)));  // packed FP32 (v_pk_fma_f32) pair
 
 template <int I, int N, typename F>
 OWRX_DEV void static_for(F&& f) {
@@ -40,16 +43,24 @@ OWRX_DEV float2 seed_rotator(const DdcChain& ch, int64_t n) {
     return make_float2(c, s);
 }
 
-template <int P, int R>
-__global__ void __launch_bounds__(256)
+constexpr int kDdcWaves = 4;  // phase sub-segments per workgroup, reduced through LDS
+
+// Tuning knobs (defaults = the production configuration, launch_ddc_p):
+//   R    outputs per lane (register tile)          WPE  waves-per-SIMD target (VGPR budget)
+//   SB   scheduling barrier every SB samples (bounds load hoisting), 0 = none
+// Measured on MI355X (tools/micro/ddc_bench.cpp, D = 833, 27 phases x 32 outputs): R = 32,
+// WPE = 2, SB = 16 -> 58 TFLOP/s at 32 chains, 65 TFLOP/s at 256 (buffer-load addressing was
+// 2x slower than the flat loads; WPE >= 3 spills).
+template <int P, int R, int WPE, int SB>
+__global__ void __launch_bounds__(64 * kDdcWaves) __attribute__((amdgpu_waves_per_eu(WPE)))
 ddc_polyphase(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end,
               const float* __restrict__ taps_poly,  // [D][P]: taps_poly[r*P + p] = h[pD + r]
               const DdcChain* __restrict__ chains, int nchains, int D, int64_t k_begin,
-              int nk, int cpw, int tpw, int ntg, int pps, float2* __restrict__ partial) {
+              int nk, int cpw, int tpw, int pps, float2* __restrict__ partial) {
+    // the workgroup's waves share one tile group and split its phase segment four ways
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int tg = blockIdx.x * 4 + wave;  // tile group handled by this wave
-    if (tg >= ntg) return;                 // wave-uniform
+    const int tg = blockIdx.x;
     const int seg = blockIdx.y;
     const int ci = lane % cpw;
     const int ti = lane / cpw;
@@ -61,69 +72,120 @@ ddc_polyphase(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end
     const DdcChain ch = chains[chain];
     const int64_t k0 = k_begin + (int64_t)tile_c * R;
 
-    const int r_begin = seg * pps;
+    const int sub = seg * kDdcWaves + wave;
+    const int r_begin = min(D, sub * pps);
     const int r_end = min(D, r_begin + pps);
 
-    float2 acc[R];
+    // (re, im) accumulator pairs: one v_pk_fma_f32 per tap and output (2 FMAs per instruction,
+    // the form the FP32 vector peak assumes)
+    f2v acc[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) acc[i] = make_float2(0.0f, 0.0f);
+    for (int i = 0; i < R; ++i) acc[i] = f2v{0.0f, 0.0f};
+
+    // lane offset (in samples) from the wave's first tile: the per-q sample address is then a
+    // wave-uniform base (SGPR arithmetic) plus this fixed per-lane offset
+    const int ti_c = tile_c - tg * tpw;
+    const int lane_off = ti_c * R * D;
+    const int64_t k0_wave = k_begin + (int64_t)tg * tpw * R;
+    const f2v wv = f2v{ch.wD.x, ch.wD.y};
+    const f2v wp = f2v{-ch.wD.y, ch.wD.x};  // j * wD
 
     for (int r = r_begin; r < r_end; ++r) {
         float h[P];
 #pragma unroll
         for (int p = 0; p < P; ++p) h[p] = taps_poly[r * P + p];
         const int64_t n0 = k0 * D + r;  // absolute index of q = 0
-        float2 rot = seed_rotator(ch, n0);
-        const float2 wD = ch.wD;
-        // last q whose sample is inside the block (samples past it only feed discarded outputs)
-        const int64_t qmax = (blk_end - 1 - n0) / D;
-        const float2* xp = blk + (n0 - blk_start);
-        const int qmax32 = (int)(qmax < (int64_t)(R + P) ? qmax : (int64_t)(R + P));
-        // fully unrolled at compile time: every acc index is a constant (registers, no scratch)
-        static_for<0, R + P - 1>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            const int qq = q < qmax32 ? q : qmax32;
-            const float2 x = xp[qq * D];
-            const float2 s = cmul(x, rot);
-            rot = cmul(rot, wD);
-            constexpr int plo = q - R + 1 > 0 ? q - R + 1 : 0;
-            constexpr int phi = q < P - 1 ? q : P - 1;
-            static_for<plo, phi + 1>([&](auto pc) {
-                constexpr int p = decltype(pc)::value;
-                acc[q - p].x = fmaf(h[p], s.x, acc[q - p].x);
-                acc[q - p].y = fmaf(h[p], s.y, acc[q - p].y);
+        const float2 rot0 = seed_rotator(ch, n0);
+        f2v rv = f2v{rot0.x, rot0.y};
+        const float2* wbase = blk + (k0_wave * D + r - blk_start);  // wave-uniform
+        // fast path: every lane's window [n0, n0 + (R+P-2) D] lies inside the block
+        const bool inside = n0 + (int64_t)(R + P - 2) * D < blk_end;
+        auto body = [&](auto clamp) {
+            constexpr bool CLAMP = decltype(clamp)::value;
+            int qmax32 = R + P;
+            if (CLAMP) {  // last q whose sample is inside the block (later ones feed discarded outputs)
+                const int64_t qmax = (blk_end - 1 - n0) / D;
+                qmax32 = (int)(qmax < (int64_t)(R + P) ? qmax : (int64_t)(R + P));
+            }
+            // fully unrolled at compile time: every acc index is a constant (registers, no scratch)
+            static_for<0, R + P - 1>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                float2 x;
+                if (CLAMP) {
+                    const int qq = q < qmax32 ? q : qmax32;
+                    x = wbase[qq * D + lane_off];
+                } else {
+                    const float2* wq = wbase + q * D;  // uniform
+                    x = wq[lane_off];
+                }
+                // s = x * rot, rot *= wD, as packed pairs: x.re * rot + x.im * (j rot)
+                const f2v rp = f2v{-rv.y, rv.x};
+                const f2v sv = __builtin_elementwise_fma(f2v{x.y, x.y}, rp, f2v{x.x, x.x} * rv);
+                rv = __builtin_elementwise_fma(f2v{rv.y, rv.y}, wp, f2v{rv.x, rv.x} * wv);
+                constexpr int plo = q - R + 1 > 0 ? q - R + 1 : 0;
+                constexpr int phi = q < P - 1 ? q : P - 1;
+                static_for<plo, phi + 1>([&](auto pc) {
+                    constexpr int p = decltype(pc)::value;
+                    acc[q - p] = __builtin_elementwise_fma(f2v{h[p], h[p]}, sv, acc[q - p]);
+                });
+                // bound the scheduler's load hoisting (keeps ~8 samples in flight per wave
+                // instead of the whole window, which would cost occupancy)
+                if constexpr (SB > 0 && (q % SB) == SB - 1) __builtin_amdgcn_sched_barrier(0);
             });
-            // bound the scheduler's load hoisting (keeps ~8 samples in flight per wave instead of
-            // the whole window, which would cost 1 wave/SIMD of occupancy)
-            if constexpr ((q % 8) == 7) __builtin_amdgcn_sched_barrier(0);
-        });
+        };
+        if (__all(inside)) body(std::false_type{});
+        else body(std::true_type{});
     }
-    if (!active) return;
+    // fixed-order tree over the four waves: ((w0 + w2) + (w1 + w3))
+    __shared__ float2 red[2][R][64];
+    if (wave >= 2) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) red[wave - 2][i][lane] = make_float2(acc[i].x, acc[i].y);
+    }
+    __syncthreads();
+    if (wave < 2) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const float2 v = red[wave][i][lane];
+            acc[i] += f2v{v.x, v.y};
+        }
+    }
+    __syncthreads();
+    if (wave == 1) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) red[0][i][lane] = make_float2(acc[i].x, acc[i].y);
+    }
+    __syncthreads();
+    if (wave != 0 || !active) return;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const float2 v = red[0][i][lane];
+        acc[i] += f2v{v.x, v.y};
+    }
     float2* out = partial + ((int64_t)seg * nchains + chain) * nk;
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         const int kk = tile * R + i;
-        if (kk < nk) out[kk] = acc[i];
+        if (kk < nk) out[kk] = make_float2(acc[i].x, acc[i].y);
     }
 }
 
-template <int P>
+template <int P, int R = 32, int WPE = 2, int SB = 16>
 static hipError_t launch_ddc_p(const float2* blk, int64_t blk_start, int64_t blk_end,
                                const float* taps_poly, const DdcChain* chains, int nchains,
                                int D, int64_t k_begin, int nk, int nseg, float2* partial,
                                hipStream_t st) {
-    constexpr int R = 32;
     int cpw = 1;
     while (cpw < nchains && cpw < 64) cpw <<= 1;
     const int tpw = 64 / cpw;
     const int ntiles = (nk + R - 1) / R;
     const int ntg = (ntiles + tpw - 1) / tpw;
     const int ncg = (nchains + cpw - 1) / cpw;
-    const int pps = (D + nseg - 1) / nseg;
-    const int segs = (D + pps - 1) / pps;
-    dim3 grid((ntg + 3) / 4, segs, ncg);
-    hipLaunchKernelGGL((ddc_polyphase<P, R>), grid, dim3(256), 0, st, blk, blk_start, blk_end,
-                       taps_poly, chains, nchains, D, k_begin, nk, cpw, tpw, ntg, pps, partial);
+    const int pps = (D + kDdcWaves * nseg - 1) / (kDdcWaves * nseg);
+    dim3 grid(ntg, nseg, ncg);  // nseg comes from ddc_segments (no empty segment)
+    hipLaunchKernelGGL((ddc_polyphase<P, R, WPE, SB>), grid, dim3(64 * kDdcWaves), 0, st, blk, blk_start,
+                       blk_end, taps_poly, chains, nchains, D, k_begin, nk, cpw, tpw, pps,
+                       partial);
     return hipGetLastError();
 }
 
@@ -135,10 +197,12 @@ int ddc_padded_p(int p) {
     return -1;
 }
 
-// Number of phase segments actually launched for a requested split.
+// Number of phase segments (= partial sums written per output) actually launched for a
+// requested split; each segment is kDdcWaves sub-segments of pps phases, one per wave.
 int ddc_segments(int D, int nseg) {
-    const int pps = (D + nseg - 1) / nseg;
-    return (D + pps - 1) / pps;
+    const int pps = (D + kDdcWaves * nseg - 1) / (kDdcWaves * nseg);
+    const int subs = (D + pps - 1) / pps;
+    return (subs + kDdcWaves - 1) / kDdcWaves;
 }
 
 hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_end,

@@ -8,12 +8,12 @@
 //      is the same linear operator; selector.py:115-117, 159-166)
 //   -> Squelch (block power, gate, s-meter writer; selector.py:119-130)
 //   -> demodulator front: FmDemod + Limit | AmDemod | RealPart (csdr/chain/analog.py)
-// post_serial (stream B, one LANE per chain, 64 chains per wave): the recurrences
-//   NfmDeemphasis | DcBlock -> Agc -> Convert(FLOAT, SHORT) -> AdpcmEncoder(sync=True)
-//   (analog.py, clientaudio.py).  All lanes walk their streams in lockstep, so 32-256 chains
-//   cost about one chain; inputs are prefetched 16 samples ahead, the ADPCM step table lives in
-//   LDS and its lookup is off the dependency chain (adpcm_encode_fast).  Runs concurrently
-//   with the next block's stream-A work.
+// post_serial_front (stream B, one LANE per chain, 64 chains per workgroup): the recurrences
+//   NfmDeemphasis | DcBlock -> Agc -> Convert(FLOAT, SHORT)  (analog.py, clientaudio.py),
+//   pipelined over three waves; all lanes walk their streams in lockstep, so 32-256 chains
+//   cost about one chain.
+// chain_adpcm (stream C, one LANE per chain): AdpcmEncoder(sync=True).  Streams B and C run
+//   concurrently with the next blocks' stream-A work.
 #include <type_traits>
 
 #include "owrx_types.h"
@@ -46,6 +46,13 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     __shared__ float sh_power[kMaxSqBlocks];
     __shared__ uint8_t sh_pass[kMaxSqBlocks];
 
+    const auto partial = gp(P.partial);
+    const auto ddc_buf = gp(P.ddc_buf);
+    const auto fd_buf = gp(P.fd_buf);
+    const auto sq_buf = gp(P.sq_buf);
+    const auto dem = gp(P.dem);
+    const auto bp_taps = gp(P.bp_taps);
+    const auto smeter = gp(P.smeter);
     if (tid == 0) S = *P.pstate;
     __syncthreads();
 
@@ -54,16 +61,31 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     const int64_t nn = P.k_begin + P.nk - kb;
     const int n_new = nn > 0 ? (int)nn : 0;
     const int col0 = (int)(kb - P.k_begin);
-    for (int i = tid; i < n_new; i += NT) {
-        float2 y = make_float2(0.0f, 0.0f);
-        for (int s = 0; s < P.nseg; ++s) {
-            const float2 v =
-                P.partial[((int64_t)s * P.group_chains + P.chain_in_group) * P.nk + col0 + i];
-            y.x += v.x;
-            y.y += v.y;
+    {   // segment partials: 8 independent loads in flight per thread, summed in segment order
+        const int64_t sstride = (int64_t)P.group_chains * P.nk;
+        const int nseg = P.nseg;
+        for (int i = tid; i < n_new; i += NT) {
+            const auto src = partial + (int64_t)P.chain_in_group * P.nk + col0 + i;
+            float2 y = make_float2(0.0f, 0.0f);
+            int s = 0;
+            for (; s + 8 <= nseg; s += 8) {
+                float2 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = src[(s + u) * sstride];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    y.x += v[u].x;
+                    y.y += v[u].y;
+                }
+            }
+            for (; s < nseg; ++s) {
+                const float2 v = src[s * sstride];
+                y.x += v.x;
+                y.y += v.y;
+            }
+            ddc_buf[kFdHist + i] = y;
+            if (P.debug && i < P.dbg_cap) P.dbg_ddc[i] = y;
         }
-        P.ddc_buf[kFdHist + i] = y;
-        if (P.debug && i < P.dbg_cap) P.dbg_ddc[i] = y;
     }
     __syncthreads();
     const int64_t ddc_base = S.ddc_count - kFdHist;  // local index of ddc_buf[0]
@@ -101,27 +123,28 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
             suf[kFdPoints - 1] = 1.0f;
 #pragma unroll
             for (int i = kFdPoints - 2; i >= 0; --i) suf[i] = suf[i + 1] * d[i + 1];
-            const float2* x = P.ddc_buf + (lo - ddc_base);
+            const auto x = ddc_buf + (lo - ddc_base);
             float2 acc = make_float2(0.0f, 0.0f);
 #pragma unroll
             for (int i = 0; i < kFdPoints; ++i) {
                 const float L = pre[i] * suf[i] * lagrange_den(i);
-                acc.x = fmaf(L, x[i].x, acc.x);
-                acc.y = fmaf(L, x[i].y, acc.y);
+                const float2 xi = x[i];
+                acc.x = fmaf(L, xi.x, acc.x);
+                acc.y = fmaf(L, xi.y, acc.y);
             }
-            P.fd_buf[kBpHist + j] = acc;
+            fd_buf[kBpHist + j] = acc;
         }
     } else {
         if (tid == 0) sh_n_fd = n_new;
-        for (int j = tid; j < n_new; j += NT) P.fd_buf[kBpHist + j] = P.ddc_buf[kFdHist + j];
+        for (int j = tid; j < n_new; j += NT) fd_buf[kBpHist + j] = ddc_buf[kFdHist + j];
     }
     __syncthreads();
     const int n_fd = sh_n_fd;
     {   // keep the last kFdHist DDC outputs as interpolator history
         float2 t = make_float2(0.0f, 0.0f);
-        if (tid < kFdHist) t = P.ddc_buf[n_new + tid];
+        if (tid < kFdHist) t = ddc_buf[n_new + tid];
         __syncthreads();
-        if (tid < kFdHist) P.ddc_buf[tid] = t;
+        if (tid < kFdHist) ddc_buf[tid] = t;
     }
 
     // ---- 2. Bandpass (inputs + taps staged in LDS when they fit) ------------------------
@@ -129,12 +152,12 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     const int nbt = P.bp_ntaps;
     const bool lds_bp = nbt > 0 && (kBpHist + n_fd) <= kBpLds;
     if (lds_bp) {
-        for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[j] = P.fd_buf[j];
-        for (int t = tid; t < nbt; t += NT) sh_taps[t] = P.bp_taps[t];
+        for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[j] = fd_buf[j];
+        for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
         __syncthreads();
     }
     for (int j = tid; j < n_fd; j += NT) {
-        const float2* x = P.fd_buf + kBpHist + j;
+        const auto x = fd_buf + kBpHist + j;
         float2 y;
         if (lds_bp) {
             const float2* xs = sh_x + kBpHist + j;
@@ -165,7 +188,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         } else if (nbt > 0) {
             float ar = 0.0f, ai = 0.0f;
             for (int t = 0; t < nbt; ++t) {
-                const float2 g = P.bp_taps[t];
+                const float2 g = bp_taps[t];
                 const float2 v = x[-t];
                 ar = fmaf(g.x, v.x, ar);
                 ar = fmaf(-g.y, v.y, ar);
@@ -176,7 +199,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         } else {
             y = x[0];
         }
-        P.sq_buf[pend + j] = y;
+        sq_buf[pend + j] = y;
         if (P.debug && j < P.dbg_cap) {
             P.dbg_fd[j] = x[0];
             P.dbg_bp[j] = y;
@@ -184,9 +207,9 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     }
     __syncthreads();
     {   // keep the last kBpHist bandpass inputs
-        const float2 t = P.fd_buf[n_fd + tid];  // kBpHist == NT
+        const float2 t = fd_buf[n_fd + tid];  // kBpHist == NT
         __syncthreads();
-        P.fd_buf[tid] = t;
+        fd_buf[tid] = t;
     }
 
     // ---- 3. Squelch: block powers, gate, s-meter ---------------------------------------
@@ -199,7 +222,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         for (int b = wave; b < nb; b += NT / 64) {
             float p = 0.0f;
             for (int m = lane; m < nper; m += 64) {
-                const float2 v = P.sq_buf[b * L + m * P.sq_dec];
+                const float2 v = sq_buf[b * L + m * P.sq_dec];
                 p = fmaf(v.x, v.x, p);
                 p = fmaf(v.y, v.y, p);
             }
@@ -214,7 +237,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
             const float power = sh_power[b];
             const int64_t bi = S.sq_blocks + b;
             if (P.sq_report > 0 && ((bi + 1) % P.sq_report) == 0) {
-                if (ns < P.smeter_cap) P.smeter[ns] = power;
+                if (ns < P.smeter_cap) smeter[ns] = power;
                 ns++;
             }
             int pass;
@@ -239,36 +262,36 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     const int nsq = nb * L;
     const float2 fm_prev0 = S.fm_last;
     for (int i = tid; i < nsq; i += NT) {
-        const float2 x = sh_pass[i / L] ? P.sq_buf[i] : make_float2(0.0f, 0.0f);
+        const float2 x = sh_pass[i / L] ? sq_buf[i] : make_float2(0.0f, 0.0f);
         if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
         float v;
         if (P.demod == 0) {
             float2 prev = fm_prev0;
-            if (i > 0) prev = sh_pass[(i - 1) / L] ? P.sq_buf[i - 1] : make_float2(0.0f, 0.0f);
+            if (i > 0) prev = sh_pass[(i - 1) / L] ? sq_buf[i - 1] : make_float2(0.0f, 0.0f);
             v = limit_step(fm_step(x, prev), 1.0f);
         } else if (P.demod == 1) {
             v = am_step(x);
         } else {
             v = x.x;
         }
-        P.dem[i] = v;
+        dem[i] = v;
     }
     __syncthreads();
     {   // move the incomplete squelch block to the front
         const int rem = total - nsq;
         float2 last = S.fm_last;
-        if (nsq > 0) last = sh_pass[nb - 1] ? P.sq_buf[nsq - 1] : make_float2(0.0f, 0.0f);
+        if (nsq > 0) last = sh_pass[nb - 1] ? sq_buf[nsq - 1] : make_float2(0.0f, 0.0f);
         float2 t[kMaxSqLen / NT];
 #pragma unroll
         for (int m = 0; m < kMaxSqLen / NT; ++m) {
             const int i = tid + m * NT;
-            if (i < rem) t[m] = P.sq_buf[nsq + i];
+            if (i < rem) t[m] = sq_buf[nsq + i];
         }
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < kMaxSqLen / NT; ++m) {
             const int i = tid + m * NT;
-            if (i < rem) P.sq_buf[i] = t[m];
+            if (i < rem) sq_buf[i] = t[m];
         }
         if (tid == 0) {
             S.fm_last = last;
@@ -288,337 +311,263 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
 }
 
 // ---------------------------------------------------------------------------------------------
-// post_serial: one lane per chain.  Branch-free hot loop (mode selects instead of exec-mask
-// regions), 8 samples per iteration loaded one block ahead, lanes that run out of samples keep
-// computing on padding but their state updates / stores are masked by selects.
-struct SerState {
-    float deemph_y, dc_xp, dc_yp;
-    AgcState agc;
-    AdpcmFast ad;
-};
+// post_serial_front: the per-chain recurrences after the demodulator, one LANE per chain
+// (64 chains per workgroup), three waves pipelined by chunks of kSerChunk samples through LDS:
+//   wave 0   NfmDeemphasis | DcBlock and the AGC envelope (chunk c) -> (u, env) in LDS
+//   wave 1,2 gain = reference / env (clamped), a = u * gain, Convert (chunk c-1; even / odd
+//            samples): int16 to the output slot (S16), float (F32), or the chain's int16
+//            scratch for the ADPCM encoder (chain_adpcm below)
+// The arithmetic is exactly deemph_step / dcblock_step / agc_step / convert_s16 split at the
+// AGC gain, so the result is bit-identical to the sequential order (oracle orc_agc etc.).
+constexpr int kSerChunk = 64;
+constexpr int kFrontThreads = 192;
 
-OWRX_DEV float serial_front(float v, int demod, float alpha, float beta, const AgcParams& agcp,
-                            SerState& s, float* dem_out) {
-    // NfmDeemphasis and DcBlock both advance (only the chain's own one is ever output)
-    const float vd = deemph_step(v, alpha, beta, s.deemph_y);
-    const float vc = dcblock_step(v, s.dc_xp, s.dc_yp);
-    const float u = demod == 0 ? vd : (demod == 1 ? vc : v);
-    *dem_out = u;
-    return agc_step(u, agcp, s.agc);
+// Lane -> chain for the serial kernels.  The host orders `sel` by demodulator and pads every
+// demodulator's run to whole workgroups with -1 (inactive lanes), so the demodulator is
+// uniform per workgroup; sel[first lane of the workgroup] is always a real chain.
+struct SerLane {
+    int c;        // chain (a real one even for inactive lanes)
+    bool active;
+};
+OWRX_DEV SerLane ser_lane(const int* __restrict__ sel, int nsel) {
+    const int k = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int c0 = sel[blockIdx.x * 64];
+    const int cs = k < nsel ? sel[k] : -1;
+    return SerLane{cs >= 0 ? cs : c0, cs >= 0};
 }
 
 template <int OUT, bool DEBUG>
-__global__ void __launch_bounds__(64)
-post_serial(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
-            const int* __restrict__ sel, int nsel) {
-    __shared__ int16_t T[96];
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 89; i += 64) T[i] = kAdpcmStep[i];
-    __syncthreads();
-    const int k = blockIdx.x * 64 + lane;
-    const bool active = k < nsel;
-    const int c = sel[active ? k : nsel - 1];
+__global__ void __launch_bounds__(kFrontThreads)
+post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
+                  const int* __restrict__ sel, int nsel) {
+    __shared__ float2 ue[2][kSerChunk][64];  // wave 0 -> waves 1, 2: (u, envelope)
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const SerLane sl = ser_lane(sel, nsel);
+    const int c = sl.c;
     const ChainPost* Pp = posts + c;
-    const int n = active ? (int)counts[c].n_sq : 0;
-    const int demod = Pp->demod;
+    const int n = sl.active ? (int)counts[c].n_sq : 0;
+    int nmax = n, nmin = n;
+    for (int o = 32; o > 0; o >>= 1) {
+        nmax = max(nmax, __shfl_xor(nmax, o));
+        nmin = min(nmin, __shfl_xor(nmin, o));
+    }
+    const int nchunks = (nmax + kSerChunk - 1) / kSerChunk;
+    const int nfull = nmin / kSerChunk;  // chunks in which every lane has kSerChunk samples
     const AgcParams agcp = Pp->agc;
-    const float alpha = Pp->deemph_alpha, beta = Pp->deemph_beta;
-    uint8_t* __restrict__ out = Pp->out;
-    const int64_t cap = Pp->out_cap;
-    float* __restrict__ dbg_dem = Pp->dbg_dem;
-    float* __restrict__ dbg_agc = Pp->dbg_agc;
-    const int64_t dcap = Pp->dbg_cap;
-    const float* __restrict__ dem = Pp->dem;
+    ChainStateS* sp = Pp->sstate;
+    const int demod = __builtin_amdgcn_readfirstlane(Pp->demod);  // uniform (see ser_lane)
+
+    if (wave == 0) {
+        // ---- recurrences: NfmDeemphasis | DcBlock, AGC envelope -> (u, env)
+        float deemph_y = sp->deemph_y, dc_xp = sp->dc_xp, dc_yp = sp->dc_yp;
+        AgcState agc = sp->agc;
+        const float alpha = Pp->deemph_alpha, beta = Pp->deemph_beta;
+        const auto dem = gp(Pp->dem);
+        auto run = [&](auto dm, auto fl, int ch) {
+            constexpr int DM = decltype(dm)::value;
+            constexpr bool FULL = decltype(fl)::value;
+            const int base = ch * kSerChunk;
+            float2(*dst)[64] = ue[ch & 1];
+            float cur[8], nxt[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cur[j] = dem[base + j];  // slack: never out of bounds
+            for (int i = 0; i < kSerChunk; i += 8) {
+                if (i + 8 < kSerChunk) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) nxt[j] = dem[base + i + 8 + j];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float v = cur[j];
+                    const float ky = deemph_y, kx = dc_xp, kyy = dc_yp, ke = agc.env;
+                    float u;
+                    if (DM == 0) u = deemph_step(v, alpha, beta, deemph_y);
+                    else if (DM == 1) u = dcblock_step(v, dc_xp, dc_yp);
+                    else u = v;
+                    {
+#pragma clang fp contract(off)
+                        const float a = fabsf(u);
+                        const float d = a - agc.env;
+                        const float rate = (d > 0.0f) ? agcp.attack : agcp.decay;
+                        const float t = rate * d;
+                        agc.env = agc.env + t;
+                    }
+                    dst[i + j][lane] = make_float2(u, agc.env);
+                    if (!FULL && base + i + j >= n) {  // past this lane's end: keep state
+                        deemph_y = ky;
+                        dc_xp = kx;
+                        dc_yp = kyy;
+                        agc.env = ke;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+            }
+        };
+        auto run_dm = [&](auto dm, int ch) {
+            if (ch < nfull) run(dm, std::true_type{}, ch);
+            else run(dm, std::false_type{}, ch);
+        };
+        for (int it = 0; it < nchunks + 1; ++it) {
+            if (it < nchunks) {
+                if (demod == 0) run_dm(std::integral_constant<int, 0>{}, it);
+                else if (demod == 1) run_dm(std::integral_constant<int, 1>{}, it);
+                else run_dm(std::integral_constant<int, 2>{}, it);
+            }
+            __syncthreads();
+        }
+        if (sl.active) {
+            sp->deemph_y = deemph_y;
+            sp->dc_xp = dc_xp;
+            sp->dc_yp = dc_yp;
+            sp->agc = agc;
+            if (OUT == 2) counts[c].out_bytes = 4 * (int64_t)n;
+            if (OUT == 0) counts[c].out_bytes = 2 * (int64_t)n;
+        }
+    } else {
+        // ---- gain + Convert (wave 1: even samples, wave 2: odd), one chunk behind
+        for (int it = 0; it < nchunks + 1; ++it) {
+            const int ch = it - 1;
+            if (ch >= 0) {
+                const int base = ch * kSerChunk;
+                const float2(*srcu)[64] = ue[ch & 1];
+                const bool full = ch < nfull;
+#pragma unroll 8
+                for (int j = wave - 1; j < kSerChunk; j += 2) {
+                    const float2 q = srcu[j][lane];
+                    float a;
+                    {
+#pragma clang fp contract(off)
+                        float g = (q.y > 0.0f) ? agcp.reference / q.y : agcp.max_gain;
+                        if (g > agcp.max_gain) g = agcp.max_gain;
+                        a = g * q.x;
+                    }
+                    const int64_t qi = base + j;
+                    const bool valid = full || qi < n;
+                    if (OUT == 2) {
+                        if (valid && 4 * qi + 4 <= Pp->out_cap) gp(reinterpret_cast<float*>(Pp->out))[qi] = a;
+                    } else if (OUT == 0) {
+                        if (valid && 2 * qi + 2 <= Pp->out_cap)
+                            gp(reinterpret_cast<int16_t*>(Pp->out))[qi] = convert_s16(a);
+                    } else if (sl.active) {
+                        gp(Pp->s16)[qi] = convert_s16(a);  // slack covers the ragged chunk
+                    }
+                    if (DEBUG && valid && qi < Pp->dbg_cap) {
+                        gp(Pp->dbg_dem)[qi] = q.x;
+                        gp(Pp->dbg_agc)[qi] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// AdpcmEncoder(sync=True), one LANE per chain (64 chains per wave).  IMA-ADPCM's predictor
+// carries offsets indefinitely (two encoders started apart on the same audio do not re-merge),
+// so unlike the waterfall rows the chain audio cannot be encoded speculatively in segments;
+// this kernel is the serial recurrence with the per-sample work cut to the state update:
+// samples prefetched 8 ahead from the int16 scratch, successor index / step from the LDS
+// table (adpcm_encode_tab), one byte per sample pair (low nibble first) and a "SYNC" +
+// (index, predictor) frame before the byte whose data count is a multiple of 1001
+// (AudioEngine.js:449-491).  It runs on its own stream behind post_serial_front, so block k's
+// encoding overlaps block k+1's front and block k+2's DDC.
+__global__ void __launch_bounds__(64)
+chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
+            const int* __restrict__ sel, int nsel) {
+    __shared__ __align__(16) uint32_t NS[kAdpcmTabEntries];
+    const int lane = threadIdx.x;
+    adpcm_tab_fill(NS, lane, 64);
+    __syncthreads();
+    const SerLane sl = ser_lane(sel, nsel);
+    const int c = sl.c;
+    const ChainPost* Pp = posts + c;
+    const int n = sl.active ? (int)counts[c].n_sq : 0;
     ChainStateS* sp = Pp->sstate;
     const ChainStateS st0 = *sp;
-
-    SerState S;
-    S.deemph_y = st0.deemph_y;
-    S.dc_xp = st0.dc_xp;
-    S.dc_yp = st0.dc_yp;
-    S.agc = st0.agc;
-    S.ad = adpcm_fast_init(st0.adpcm, T);
+    const auto src = gp(Pp->s16);
+    const auto out = gp(Pp->out);
+    const int64_t cap = Pp->out_cap;
+    AdpcmFast ad{st0.adpcm.index, st0.adpcm.pred, (int)kAdpcmStep[st0.adpcm.index]};
     int has_left = st0.has_left;
-    int left_code = st0.left_code;
+    int left = st0.left_code;
     int64_t bytes = st0.adpcm_bytes;
+    int until_sync = 0;  // data bytes before the next "SYNC" frame (set below)
     int64_t ob = 0;
-
-    // ADPCM: a pending nibble first pairs with sample 0 (per-lane, once)
-    int i0 = 0;
-    if (OUT == 1 && has_left && n > 0) {
-        float dv;
-        const float a = serial_front(dem[0], demod, alpha, beta, agcp, S, &dv);
-        if (DEBUG && dcap > 0) {
-            dbg_dem[0] = dv;
-            dbg_agc[0] = a;
+    auto frame = [&]() {
+        if (ob + 8 <= cap) {
+            out[ob] = (uint8_t)'S';
+            out[ob + 1] = (uint8_t)'Y';
+            out[ob + 2] = (uint8_t)'N';
+            out[ob + 3] = (uint8_t)'C';
+            const uint32_t w1 = (uint32_t)(uint16_t)ad.index | ((uint32_t)(uint16_t)ad.pred << 16);
+            for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
         }
-        const int code = adpcm_encode_fast(S.ad, convert_s16(a), T);
-        if (ob < cap) out[ob] = (uint8_t)(left_code | (code << 4));
+        ob += 8;
+        until_sync = kAdpcmSyncPeriod;
+    };
+    // a pending nibble pairs with sample 0
+    int i0 = 0;
+    if (has_left && n > 0) {
+        const int code = adpcm_encode_tab(ad, src[0], NS);
+        if (ob < cap) out[ob] = (uint8_t)(left | (code << 4));
         ob++;
-        bytes++;
+        bytes++;  // this byte's frame (if due) went out with its first nibble, last block
         has_left = 0;
         i0 = 1;
     }
-    const int nrem = n - i0;  // samples in the main loop
-    int nmax = nrem;
-    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
-    const float* __restrict__ src = dem + i0;
-    // countdown to the next "SYNC" header (before data byte bytes % 1001 == 0)
-    int until_sync = (int)((kAdpcmSyncPeriod - (bytes % kAdpcmSyncPeriod)) % kAdpcmSyncPeriod);
-
-    float cur[8], nxt[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cur[j] = j < nrem ? src[j] : 0.0f;
-    int nmin = nrem;
-    for (int o = 32; o > 0; o >>= 1) nmin = min(nmin, __shfl_xor(nmin, o));
-    auto block8 = [&](int i, auto guard) {
-        constexpr bool G = decltype(guard)::value;
-            if (OUT == 1) {
-    #pragma unroll
-                for (int j = 0; j < 8; j += 2) {
-                    const bool valid = !G || (i + j + 1 < nrem);  // whole pair present
-                    const SerState keep = S;
-                    float d0, d1;
-                    const float a0 = serial_front(cur[j], demod, alpha, beta, agcp, S, &d0);
-                    const float a1 = serial_front(cur[j + 1], demod, alpha, beta, agcp, S, &d1);
-                    if (valid && until_sync == 0) {  // rare: header carries the state before the pair
-                        if (ob + 8 <= cap) {
-                            const uint32_t w0 = 0x434e5953u;  // "SYNC"
-                            const uint32_t w1 = (uint32_t)(uint16_t)S.ad.index |
-                                                ((uint32_t)(uint16_t)S.ad.pred << 16);
-                            for (int b = 0; b < 4; ++b) out[ob + b] = (uint8_t)(w0 >> (8 * b));
-                            for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
-                        }
-                        ob += 8;
-                        until_sync = kAdpcmSyncPeriod;
-                    }
-                    const int lo = adpcm_encode_fast(S.ad, convert_s16(a0), T);
-                    const int hi = adpcm_encode_fast(S.ad, convert_s16(a1), T);
-                    if (DEBUG) {
-                        const int64_t q = i0 + i + j;
-                        if (valid && q + 1 < dcap) {
-                            dbg_dem[q] = d0;
-                            dbg_agc[q] = a0;
-                            dbg_dem[q + 1] = d1;
-                            dbg_agc[q + 1] = a1;
-                        }
-                    }
-                    if (valid && ob < cap) out[ob] = (uint8_t)(lo | (hi << 4));
-                    ob += valid ? 1 : 0;
-                    bytes += valid ? 1 : 0;
-                    until_sync -= valid ? 1 : 0;
-                    if (G && !valid) S = keep;
-                }
-            } else {
-    #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const bool valid = !G || (i + j < nrem);
-                    const SerState keep = S;
-                    float d;
-                    const float a = serial_front(cur[j], demod, alpha, beta, agcp, S, &d);
-                    if (DEBUG) {
-                        const int64_t q = i0 + i + j;
-                        if (valid && q < dcap) {
-                            dbg_dem[q] = d;
-                            dbg_agc[q] = a;
-                        }
-                    }
-                    if (OUT == 2) {
-                        if (valid && ob + 4 <= cap) *reinterpret_cast<float*>(out + ob) = a;
-                        ob += valid ? 4 : 0;
-                    } else {
-                        const int16_t s16 = convert_s16(a);
-                        if (valid && ob + 2 <= cap) *reinterpret_cast<int16_t*>(out + ob) = s16;
-                        ob += valid ? 2 : 0;
-                    }
-                    if (G && !valid) S = keep;
-                }
-            }
-    };
-    for (int i = 0; i < nmax; i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) nxt[j] = (i + 8 + j < nrem) ? src[i + 8 + j] : 0.0f;
-        if (i + 8 <= nmin)
-            block8(i, std::integral_constant<bool, false>{});
-        else
-            block8(i, std::integral_constant<bool, true>{});
-#pragma unroll
-        for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+    until_sync = (int)((kAdpcmSyncPeriod - (bytes % kAdpcmSyncPeriod)) % kAdpcmSyncPeriod);
+    // pairs (i0 + 2j, i0 + 2j + 1); a byte starts at every pair
+    const int np = (n - i0) >> 1;
+    int npmax = np, npmin = np;
+    for (int o = 32; o > 0; o >>= 1) {
+        npmax = max(npmax, __shfl_xor(npmax, o));
+        npmin = min(npmin, __shfl_xor(npmin, o));
     }
-    // ADPCM: an odd trailing sample waits for its pair
-    if (OUT == 1 && (nrem & 1)) {
-        float dv;
-        const float a = serial_front(src[nrem - 1], demod, alpha, beta, agcp, S, &dv);
-        if (DEBUG && i0 + nrem - 1 < dcap) {
-            dbg_dem[i0 + nrem - 1] = dv;
-            dbg_agc[i0 + nrem - 1] = a;
-        }
-        if (until_sync == 0) {
-            if (ob + 8 <= cap) {
-                const uint32_t w0 = 0x434e5953u;
-                const uint32_t w1 = (uint32_t)(uint16_t)S.ad.index |
-                                    ((uint32_t)(uint16_t)S.ad.pred << 16);
-                for (int b = 0; b < 4; ++b) out[ob + b] = (uint8_t)(w0 >> (8 * b));
-                for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
+    const auto x = src + i0;
+    int cur[8], nxt[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cur[q] = x[q];  // scratch slack: never out of bounds
+    auto quad = [&](int j, auto fl) {  // four pairs
+        constexpr bool FULL = decltype(fl)::value;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool valid = FULL || j + u < np;
+            const AdpcmFast keep = ad;
+            if (valid && until_sync == 0) frame();
+            const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
+            const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
+            if (FULL || valid) {
+                if (ob < cap) out[ob] = (uint8_t)(c0 | (c1 << 4));
+                ob++;
+                until_sync--;
             }
-            ob += 8;
+            if (!FULL && !valid) ad = keep;
         }
-        left_code = adpcm_encode_fast(S.ad, convert_s16(a), T);
+    };
+    for (int j = 0; j < npmax; j += 4) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * j + 8 + q];
+        if (j + 4 <= npmin) quad(j, std::true_type{});
+        else quad(j, std::false_type{});
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    }
+    bytes += np;
+    // an odd last sample starts a byte that the next block completes
+    if ((n - i0) & 1) {
+        if (until_sync == 0) frame();
+        left = adpcm_encode_tab(ad, x[2 * np], NS);
         has_left = 1;
     }
-    if (!active) return;
-    ChainStateS st = st0;
-    st.deemph_y = S.deemph_y;
-    st.dc_xp = S.dc_xp;
-    st.dc_yp = S.dc_yp;
-    st.agc = S.agc;
-    st.adpcm.index = S.ad.index;
-    st.adpcm.pred = S.ad.pred;
-    st.has_left = has_left;
-    st.left_code = left_code;
-    st.adpcm_bytes = bytes;
-    *sp = st;
+    if (!sl.active) return;
+    sp->adpcm.index = ad.index;
+    sp->adpcm.pred = ad.pred;
+    sp->has_left = has_left;
+    sp->left_code = left;
+    sp->adpcm_bytes = bytes;
     counts[c].out_bytes = ob;
-}
-
-// ADPCM output: the recurrence is split over two waves of one workgroup, pipelined by chunk:
-// wave 0 runs deemphasis / DC block + AGC + Convert for chunk c of 64 chains into an LDS ring
-// while wave 1 IMA-encodes chunk c-1 (pairs, "SYNC" headers, byte stores).  Per sample each wave
-// issues about half of the single-wave instruction stream, so a block of samples costs about
-// the longer of the two halves instead of their sum.
-constexpr int kSerChunk = 256;
-
-template <bool DEBUG>
-__global__ void __launch_bounds__(128)
-post_serial_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
-                  const int* __restrict__ sel, int nsel) {
-    __shared__ int16_t T[96];
-    __shared__ int16_t ring[2][kSerChunk][64];
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 89; i += 128) T[i] = kAdpcmStep[i];
-    const int k = blockIdx.x * 64 + lane;
-    const bool active = k < nsel;
-    const int c = sel[active ? k : nsel - 1];
-    const ChainPost* Pp = posts + c;
-    const int n = active ? (int)counts[c].n_sq : 0;
-    int nmax = n;
-    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
-    const int nchunks = (nmax + kSerChunk - 1) / kSerChunk;
-    ChainStateS* sp = Pp->sstate;
-    const ChainStateS st0 = *sp;
-    __syncthreads();
-
-    if (wave == 0) {
-        // ---- front: deemphasis / DC block, AGC, Convert -> LDS ring
-        const int demod = Pp->demod;
-        const AgcParams agcp = Pp->agc;
-        const float alpha = Pp->deemph_alpha, beta = Pp->deemph_beta;
-        float* __restrict__ dbg_dem = Pp->dbg_dem;
-        float* __restrict__ dbg_agc = Pp->dbg_agc;
-        const int64_t dcap = Pp->dbg_cap;
-        const float* __restrict__ dem = Pp->dem;
-        SerState S;
-        S.deemph_y = st0.deemph_y;
-        S.dc_xp = st0.dc_xp;
-        S.dc_yp = st0.dc_yp;
-        S.agc = st0.agc;
-        for (int ch = 0; ch <= nchunks; ++ch) {
-            if (ch < nchunks) {
-                const int base = ch * kSerChunk;
-                int16_t(*dst)[64] = ring[ch & 1];
-                float nxt[8], cur[8];
-#pragma unroll
-                for (int jj = 0; jj < 8; ++jj) cur[jj] = base + jj < n ? dem[base + jj] : 0.0f;
-                for (int i = 0; i < kSerChunk; i += 8) {
-#pragma unroll
-                    for (int jj = 0; jj < 8; ++jj)
-                        nxt[jj] = (base + i + 8 + jj < n && i + 8 < kSerChunk) ? dem[base + i + 8 + jj] : 0.0f;
-#pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) {
-                        const int q = base + i + jj;
-                        const bool valid = q < n;
-                        const SerState keep = S;
-                        float d;
-                        const float a = serial_front(cur[jj], demod, alpha, beta, agcp, S, &d);
-                        if (DEBUG && valid && q < dcap) {
-                            dbg_dem[q] = d;
-                            dbg_agc[q] = a;
-                        }
-                        dst[i + jj][lane] = convert_s16(a);
-                        if (!valid) S = keep;
-                    }
-#pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) cur[jj] = nxt[jj];
-                }
-            }
-            __syncthreads();
-        }
-        if (active) {
-            ChainStateS st = st0;
-            st.deemph_y = S.deemph_y;
-            st.dc_xp = S.dc_xp;
-            st.dc_yp = S.dc_yp;
-            st.agc = S.agc;
-            // adpcm fields are written by wave 1 (separate words of the same struct)
-            sp->deemph_y = st.deemph_y;
-            sp->dc_xp = st.dc_xp;
-            sp->dc_yp = st.dc_yp;
-            sp->agc = st.agc;
-        }
-    } else {
-        // ---- IMA-ADPCM with sync frames from the LDS ring (one chunk behind)
-        uint8_t* __restrict__ out = Pp->out;
-        const int64_t cap = Pp->out_cap;
-        AdpcmFast ad = adpcm_fast_init(st0.adpcm, T);
-        int has_left = st0.has_left;
-        int left = st0.left_code;
-        int64_t bytes = st0.adpcm_bytes;
-        int until_sync = (int)((kAdpcmSyncPeriod - (bytes % kAdpcmSyncPeriod)) % kAdpcmSyncPeriod);
-        int64_t ob = 0;
-        for (int ch = 0; ch <= nchunks; ++ch) {
-            if (ch > 0) {
-                const int base = (ch - 1) * kSerChunk;
-                const int16_t(*srcr)[64] = ring[(ch - 1) & 1];
-                for (int i = 0; i < kSerChunk; ++i) {
-                    const bool valid = base + i < n;
-                    const int v = srcr[i][lane];
-                    if (valid && !has_left && until_sync == 0) {  // rare: "SYNC" + state
-                        if (ob + 8 <= cap) {
-                            const uint32_t w1 = (uint32_t)(uint16_t)ad.index |
-                                                ((uint32_t)(uint16_t)ad.pred << 16);
-                            out[ob] = 'S';
-                            out[ob + 1] = 'Y';
-                            out[ob + 2] = 'N';
-                            out[ob + 3] = 'C';
-                            for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
-                        }
-                        ob += 8;
-                        until_sync = kAdpcmSyncPeriod;
-                    }
-                    const AdpcmFast keep = ad;
-                    const int code = adpcm_encode_fast(ad, v, T);
-                    const bool emit = valid && has_left;
-                    if (emit && ob < cap) out[ob] = (uint8_t)(left | (code << 4));
-                    ob += emit ? 1 : 0;
-                    bytes += emit ? 1 : 0;
-                    until_sync -= emit ? 1 : 0;
-                    left = (valid && !has_left) ? code : left;
-                    has_left = valid ? (has_left ^ 1) : has_left;
-                    if (!valid) ad = keep;
-                }
-            }
-            __syncthreads();
-        }
-        if (active) {
-            sp->adpcm.index = ad.index;
-            sp->adpcm.pred = ad.pred;
-            sp->has_left = has_left;
-            sp->left_code = left;
-            sp->adpcm_bytes = bytes;
-            counts[c].out_bytes = ob;
-        }
-    }
 }
 
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
@@ -631,16 +580,24 @@ hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, int output, int debug, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
-    const dim3 g((nsel + 63) / 64), b(64);
+    const dim3 g((nsel + 63) / 64), b(kFrontThreads);
     switch (output * 2 + (debug ? 1 : 0)) {
-        case 0: hipLaunchKernelGGL((post_serial<0, false>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 1: hipLaunchKernelGGL((post_serial<0, true>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 2: hipLaunchKernelGGL((post_serial_adpcm<false>), g, dim3(128), 0, st, posts, counts, sel, nsel); break;
-        case 3: hipLaunchKernelGGL((post_serial_adpcm<true>), g, dim3(128), 0, st, posts, counts, sel, nsel); break;
-        case 4: hipLaunchKernelGGL((post_serial<2, false>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 5: hipLaunchKernelGGL((post_serial<2, true>), g, b, 0, st, posts, counts, sel, nsel); break;
+        case 0: hipLaunchKernelGGL((post_serial_front<0, false>), g, b, 0, st, posts, counts, sel, nsel); break;
+        case 1: hipLaunchKernelGGL((post_serial_front<0, true>), g, b, 0, st, posts, counts, sel, nsel); break;
+        case 2: hipLaunchKernelGGL((post_serial_front<1, false>), g, b, 0, st, posts, counts, sel, nsel); break;
+        case 3: hipLaunchKernelGGL((post_serial_front<1, true>), g, b, 0, st, posts, counts, sel, nsel); break;
+        case 4: hipLaunchKernelGGL((post_serial_front<2, false>), g, b, 0, st, posts, counts, sel, nsel); break;
+        case 5: hipLaunchKernelGGL((post_serial_front<2, true>), g, b, 0, st, posts, counts, sel, nsel); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
+                              int nsel, hipStream_t st) {
+    if (nsel <= 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_adpcm, dim3((nsel + 63) / 64), dim3(64), 0, st, posts, counts, sel,
+                       nsel);
     return hipGetLastError();
 }
 

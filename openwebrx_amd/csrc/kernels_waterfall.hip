@@ -11,7 +11,9 @@
 //   re-read from L2).
 // wf_finalize: sums each row's group partials in a fixed order onto the carried accumulator
 //   (rows span blocks), 10*log10 + add_db correction, fftshift, quantise (short)(dB*100).
-// wf_adpcm_rows: IMA-ADPCM of each padded row (serial per row, one lane per row).
+// wf_adpcm_rows_spec: FftAdpcm (IMA-ADPCM of each padded row), one workgroup per row,
+//   segment-parallel and exact (adpcm_spec.h).
+#include "adpcm_spec.h"
 #include "owrx_types.h"
 
 namespace owrx {
@@ -154,141 +156,41 @@ wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
 }
 
 // FftAdpcm: 10 copies of the first value (COMPRESS_FFT_PAD_N, htdocs/openwebrx.js:845), then
-// the row; fresh codec state per row; low nibble first.  One lane per row (rows of one launch
-// have the same length, so the wave runs them in lockstep); 8 input samples per 16-B load,
-// prefetched one load ahead; step table in LDS, lookup off the dependency chain.
-__global__ void __launch_bounds__(64)
-wf_adpcm_rows(const int16_t* __restrict__ s16, int N, int nrows, uint8_t* __restrict__ out,
-              int row_bytes) {
-    __shared__ int16_t T[96];
-    for (int i = threadIdx.x; i < 89; i += 64) T[i] = kAdpcmStep[i];
-    __syncthreads();
-    const int r = blockIdx.x * 64 + threadIdx.x;
-    if (r >= nrows) return;
-    const int16_t* s = s16 + (int64_t)r * N;
-    uint8_t* o = out + (int64_t)r * row_bytes;
-    AdpcmFast st{0, 0, (int)T[0]};
-    const int first = s[0];
-    for (int t = 0; t < 10; t += 2) {
-        const int lo = adpcm_encode_fast(st, first, T);
-        const int hi = adpcm_encode_fast(st, first, T);
-        o[t >> 1] = (uint8_t)(lo | (hi << 4));
-    }
-    const int4* v4 = reinterpret_cast<const int4*>(s);
-    int4 nxt = v4[0];
-    for (int i = 0; i < N; i += 8) {
-        const int4 cur = nxt;
-        if (i + 8 < N) nxt = v4[(i >> 3) + 1];
-        const int w[4] = {cur.x, cur.y, cur.z, cur.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int a = (int)(int16_t)(w[j] & 0xffff);
-            const int b = (int)(int16_t)((uint32_t)w[j] >> 16);
-            const int lo = adpcm_encode_fast(st, a, T);
-            const int hi = adpcm_encode_fast(st, b, T);
-            o[5 + ((i >> 1) + j)] = (uint8_t)(lo | (hi << 4));
-        }
-    }
-}
+// the row; fresh codec state per row; low nibble first.  Row-parallel exact encoder: one
+// workgroup per row, the row (10 pad samples +
+// N bins) staged in LDS and encoded by the speculative segment-parallel encoder of
+// adpcm_spec.h (bit-identical to the sequential FftAdpcm restatement, oracle
+// orc_fft_adpcm_row); rows longer than kRowWin samples go window by window.  Waterfall rows
+// re-merge after ~100-900 samples from a guessed start (index 30 measured fastest), so the
+// Jacobi repair converges in a few rounds.
+constexpr int kRowWin = 16400;
 
-// FftAdpcm, row-parallel exact encoder.  IMA-ADPCM is a serial recurrence, but two encoders
-// started from different states on the same input reach the same (index, predictor) state
-// after ~100-900 samples on waterfall data and are identical from then on.  Each row is split
-// into kSeg segments, one lane each:
-//   pass 1: every segment encodes from a guessed state (segment 0 from the true state),
-//           storing its codes and its state trajectory;
-//   pass 2: a segment whose start differs from its predecessor's final state re-encodes from
-//           that state until its state equals the stored trajectory (then the stored codes are
-//           exact from there on) or to its end (then its trajectory / final state are
-//           replaced).  Jacobi iterations until no segment re-runs (<= kSeg, typically 1-2);
-//   pass 3: nibble packing.
-// The result is bit-identical to the sequential encoder (oracle orc_fft_adpcm_row).
-constexpr int kSeg = 16;
-
-OWRX_DEV uint32_t pack_state(const AdpcmFast& s) {
-    return ((uint32_t)s.index << 16) | ((uint32_t)s.pred & 0xffffu);
-}
-OWRX_DEV AdpcmFast unpack_state(uint32_t v, const int16_t* T) {
-    AdpcmFast s;
-    s.index = (int)(v >> 16);
-    s.pred = (int)(int16_t)(v & 0xffffu);
-    s.step = T[s.index];
-    return s;
-}
-
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(kSpecThreads)
 wf_adpcm_rows_spec(const int16_t* __restrict__ s16, int N, int nrows, uint8_t* __restrict__ out,
-                   int row_bytes, uint8_t* __restrict__ codes, uint32_t* __restrict__ traj) {
-    __shared__ int16_t T[96];
-    __shared__ uint32_t seg_start[4][kSeg], seg_final[4][kSeg];
-    __shared__ int any_rerun;
-    const int lane = threadIdx.x;
-    for (int i = lane; i < 89; i += 64) T[i] = kAdpcmStep[i];
-    const int rl = lane / kSeg, j = lane % kSeg;
-    const int row_raw = blockIdx.x * 4 + rl;
-    const bool active = row_raw < nrows;
-    const int row = active ? row_raw : nrows - 1;
+                   int row_bytes) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    SpecLds<kRowWin>& L = *reinterpret_cast<SpecLds<kRowWin>*>(smem);
+    const int tid = threadIdx.x;
+    const int row = blockIdx.x;
+    for (int i = tid; i < 89; i += kSpecThreads) L.T[i] = kAdpcmStep[i];
+    adpcm_tab_fill(L.NS, tid, kSpecThreads);
     const int M = N + 10;
-    const int L = ((M + kSeg - 1) / kSeg + 1) & ~1;
-    const int b0 = min(j * L, M), b1 = min(b0 + L, M);
     const int16_t* x = s16 + (int64_t)row * N;
-    uint8_t* cd = codes + (int64_t)row * M;
-    uint32_t* tr = traj + (int64_t)row * M;
-    auto sample = [&](int t) -> int { return t < 10 ? (int)x[0] : (int)x[t - 10]; };
-    __syncthreads();
-
-    // pass 1: speculative encode of every segment
-    AdpcmFast st;
-    if (j == 0) {
-        st = AdpcmFast{0, 0, (int)T[0]};
-    } else {
-        st.index = 30;  // measured to merge fastest on waterfall rows
-        st.pred = sample(b0 - 1);
-        st.step = T[30];
-    }
-    const uint32_t start0 = pack_state(st);
-    for (int t = b0; t < b1; ++t) {
-        cd[t] = (uint8_t)adpcm_encode_fast(st, sample(t), T);
-        tr[t] = pack_state(st);
-    }
-    seg_start[rl][j] = start0;
-    seg_final[rl][j] = pack_state(st);
-    __syncthreads();
-
-    // pass 2: repair from the predecessor's final state until consistent
-    for (int it = 0; it < kSeg; ++it) {
-        if (lane == 0) any_rerun = 0;
+    uint8_t* o = out + (int64_t)row * row_bytes;
+    uint32_t state = 0;  // FftAdpcm restarts every row at (index 0, predictor 0)
+    for (int w0 = 0; w0 < M; w0 += kRowWin) {
+        const int nw = min(kRowWin, M - w0);
         __syncthreads();
-        const uint32_t want = j > 0 ? seg_final[rl][j - 1] : seg_start[rl][0];
-        const bool rerun = active && j > 0 && want != seg_start[rl][j] && b0 < b1;
-        uint32_t fin = seg_final[rl][j];
-        __syncthreads();  // everyone has read the finals of this iteration
-        if (rerun) {
-            AdpcmFast r = unpack_state(want, T);
-            bool merged = false;
-            for (int t = b0; t < b1; ++t) {
-                cd[t] = (uint8_t)adpcm_encode_fast(r, sample(t), T);
-                const uint32_t ps = pack_state(r);
-                if (ps == tr[t]) {
-                    merged = true;
-                    break;
-                }
-                tr[t] = ps;
-            }
-            if (!merged) fin = pack_state(r);
-            seg_start[rl][j] = want;
-            seg_final[rl][j] = fin;
-            any_rerun = 1;
+        for (int i = tid; i < nw; i += kSpecThreads) {
+            const int t = w0 + i;
+            L.x[i] = t < 10 ? x[0] : x[t - 10];
         }
         __syncthreads();
-        if (!any_rerun) break;
-    }
-
-    // pass 3: nibbles -> bytes (low nibble first)
-    __syncthreads();
-    if (active) {
-        uint8_t* o = out + (int64_t)row * row_bytes;
-        for (int i = j; i < M / 2; i += kSeg) o[i] = (uint8_t)((cd[2 * i] & 15) | (cd[2 * i + 1] << 4));
+        adpcm_spec_window(L, nw, state, 30, 64);
+        __syncthreads();
+        for (int i = tid; i < nw / 2; i += kSpecThreads)
+            o[w0 / 2 + i] = (uint8_t)((L.code[2 * i] & 15) | (L.code[2 * i + 1] << 4));
+        state = L.traj[nw - 1];
     }
 }
 
@@ -336,14 +238,17 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
 }
 
 hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, int row_bytes,
-                           uint8_t* codes, uint32_t* traj, hipStream_t st) {
-    if (codes && traj) {
-        hipLaunchKernelGGL(wf_adpcm_rows_spec, dim3((nrows + 3) / 4), dim3(64), 0, st, s16, N,
-                           nrows, out, row_bytes, codes, traj);
-    } else {
-        hipLaunchKernelGGL(wf_adpcm_rows, dim3((nrows + 63) / 64), dim3(64), 0, st, s16, N,
-                           nrows, out, row_bytes);
+                           hipStream_t st) {
+    const size_t lds = sizeof(SpecLds<kRowWin>);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_adpcm_rows_spec,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
     }
+    hipLaunchKernelGGL(wf_adpcm_rows_spec, dim3(nrows), dim3(kSpecThreads), lds, st, s16, N,
+                       nrows, out, row_bytes);
     return hipGetLastError();
 }
 

@@ -32,6 +32,44 @@ struct AdpcmState {
     int pred;
 };
 
+// Global-address-space view of a pointer read from a descriptor.  Generic (flat) accesses
+// count against the LDS wait counter too, so a kernel mixing them with LDS traffic waits on
+// HBM latency at every LDS use; global_* accesses only wait where their data is consumed.
+// (HIP vector classes cannot be address-space qualified, so float2 goes through the native
+// ext_vector type.)
+template <typename T> struct GNative { using type = T; };
+template <> struct GNative<float2> { using type = float __attribute__((ext_vector_type(2))); };
+
+template <typename T>
+struct GRef {
+    using N = typename GNative<T>::type;
+    __attribute__((address_space(1))) N* p;
+    OWRX_DEV operator T() const { return __builtin_bit_cast(T, *p); }
+    OWRX_DEV T get() const { return __builtin_bit_cast(T, *p); }
+    OWRX_DEV const GRef& operator=(T v) const {
+        *p = __builtin_bit_cast(N, v);
+        return *this;
+    }
+    // element copy (a[i] = b[i]), never a rebinding of the reference
+    OWRX_DEV const GRef& operator=(const GRef& o) const { return *this = o.get(); }
+};
+
+template <typename T>
+struct GPtr {
+    using N = typename GNative<T>::type;
+    __attribute__((address_space(1))) N* p;
+    OWRX_DEV GRef<T> operator[](int64_t i) const { return GRef<T>{p + i}; }
+    OWRX_DEV GRef<T> operator*() const { return GRef<T>{p}; }
+    OWRX_DEV GPtr operator+(int64_t i) const { return GPtr{p + i}; }
+    OWRX_DEV GPtr operator-(int64_t i) const { return GPtr{p - i}; }
+};
+
+template <typename T>
+OWRX_DEV GPtr<T> gp(const T* q) {
+    using N = typename GNative<T>::type;
+    return GPtr<T>{(__attribute__((address_space(1))) N*)(const_cast<T*>(q))};
+}
+
 OWRX_DEV float2 cmul(float2 a, float2 b) {
     return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
@@ -216,6 +254,50 @@ OWRX_DEV int adpcm_encode_fast(AdpcmFast& s, int sample, const int16_t* __restri
     s.step = m4 ? hi_step : cm1;
     s.index = min(max(ni, 0), 88);
     return mag | (sgn & 8);
+}
+
+// Table-driven variant: NS[index * 8 + magnitude] = (next index << 16) | next step, so the
+// eight possible successors of the current index come in with two 16-byte LDS reads issued
+// before the sample is quantised, and the successor is picked by the three magnitude bits
+// (a 3-level select) -- no index clamping or table lookup on the dependency chain.
+// Bit-identical to adpcm_encode.
+constexpr int kAdpcmTabEntries = 89 * 8;
+
+OWRX_DEV void adpcm_tab_fill(uint32_t* NS, int tid, int nthreads) {
+    for (int e = tid; e < kAdpcmTabEntries; e += nthreads) {
+        const int i = e >> 3, m = e & 7;
+        int ni = i + kAdpcmIndex[m];
+        ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
+        NS[e] = ((uint32_t)ni << 16) | (uint32_t)kAdpcmStep[ni];
+    }
+}
+
+OWRX_DEV int adpcm_encode_tab(AdpcmFast& s, int sample, const uint32_t* __restrict__ NS) {
+    const uint4 r0 = *reinterpret_cast<const uint4*>(NS + s.index * 8);
+    const uint4 r1 = *reinterpret_cast<const uint4*>(NS + s.index * 8 + 4);
+    const int step = s.step;
+    int d = sample - s.pred;
+    const int sgn = d >> 31;
+    int a = (d ^ sgn) - sgn;
+    const bool m4 = a >= step;
+    const int t4 = m4 ? step : 0;
+    a -= t4;
+    const int h = step >> 1;
+    const bool m2 = a >= h;
+    const int t2 = m2 ? h : 0;
+    a -= t2;
+    const int q = step >> 2;
+    const bool m1 = a >= q;
+    const int t1 = m1 ? q : 0;
+    const int dq = (step >> 3) + t4 + t2 + t1;
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    const uint32_t lo = m2 ? (m1 ? r0.w : r0.z) : (m1 ? r0.y : r0.x);
+    const uint32_t hi = m2 ? (m1 ? r1.w : r1.z) : (m1 ? r1.y : r1.x);
+    const uint32_t rec = m4 ? hi : lo;
+    s.index = (int)(rec >> 16);
+    s.step = (int)(rec & 0xffffu);
+    return (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0) | (sgn & 8);
 }
 
 }  // namespace owrx

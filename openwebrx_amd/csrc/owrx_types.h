@@ -75,6 +75,7 @@ struct ChainPost {
     float2* fd_buf;        // [kBpHist + cap]
     float2* sq_buf;        // [sq_len + cap]
     float* dem;            // this step's demodulator output slot [cap + sq_len + 16]
+    int16_t* s16;          // Convert output feeding the ADPCM encoder [cap + sq_len + 16]
     // this step
     const float2* partial; // group partial sums [nseg][group_chains][nk]
     int32_t nseg;
