@@ -19,15 +19,11 @@ namespace owrx {
 // encoder (oracle orc_adpcm_encode / orc_fft_adpcm_row).
 constexpr int kSpecThreads = 256;
 
-OWRX_DEV uint32_t pack_state(const AdpcmFast& s) {
-    return ((uint32_t)s.index << 16) | ((uint32_t)s.pred & 0xffffu);
+OWRX_DEV uint32_t pack_state(const AdpcmTab& s) {
+    return ((uint32_t)s.index() << 16) | ((uint32_t)s.pred & 0xffffu);
 }
-OWRX_DEV AdpcmFast unpack_state(uint32_t v, const int16_t* T) {
-    AdpcmFast s;
-    s.index = (int)(v >> 16);
-    s.pred = (int)(int16_t)(v & 0xffffu);
-    s.step = T[s.index];
-    return s;
+OWRX_DEV AdpcmTab unpack_state(uint32_t v) {
+    return AdpcmTab{adpcm_tab_rec((int)(v >> 16), 0), (int)(int16_t)(v & 0xffffu)};
 }
 
 template <int WIN>
@@ -54,11 +50,11 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int gues
     const int16_t* T = L.T;
     // pass 1
     if (tid < nseg) {
-        AdpcmFast st;
+        AdpcmTab st;
         if (tid == 0) {
-            st = unpack_state(start, T);
+            st = unpack_state(start);
         } else if (guess_index >= 0) {
-            st = AdpcmFast{guess_index, (int)L.x[b0 - 1], (int)T[guess_index]};
+            st = AdpcmTab{adpcm_tab_rec(guess_index, 0), (int)L.x[b0 - 1]};
         } else {
             // predictor = previous sample, step index from the local slope
             const int d = abs((int)L.x[b0 - 1] - (int)L.x[b0 - 2]);
@@ -67,7 +63,7 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int gues
                 const int mid = (lo + hi) >> 1;
                 if (T[mid] < d) lo = mid + 1; else hi = mid;
             }
-            st = AdpcmFast{lo, (int)L.x[b0 - 1], (int)T[lo]};
+            st = AdpcmTab{adpcm_tab_rec(lo, 0), (int)L.x[b0 - 1]};
         }
         L.seg_start[tid] = pack_state(st);
         for (int t = b0; t < b1; ++t) {
@@ -89,7 +85,7 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int gues
         }
         __syncthreads();  // every start was read before any final changes
         if (rerun) {
-            AdpcmFast r = unpack_state(want, T);
+            AdpcmTab r = unpack_state(want);
             bool merged = false;
             for (int t = b0; t < b1; ++t) {
                 L.code[t] = (uint8_t)adpcm_encode_tab(r, L.x[t], L.NS);

@@ -810,14 +810,14 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const int np = (int)e->posts.size();
     if (timed) HIPCHK(hipEventRecord(S.a2, e->sA));
     if (np > 0) {
-        // stream B: post_parallel + post_serial_front, behind this block's DDC
-        HIPCHK(hipEventRecord(S.evA, e->sA));
-        HIPCHK(hipStreamWaitEvent(e->sB, S.evA, 0));
+        // stream A: post_parallel (wide); stream B: post_serial_front (serial, own CUs)
         memcpy(S.h_posts, e->posts.data(), sizeof(ChainPost) * np);
         HIPCHK(hipMemcpyAsync(S.d_posts, S.h_posts, sizeof(ChainPost) * np,
-                              hipMemcpyHostToDevice, e->sB));
-        if (timed) HIPCHK(hipEventRecord(S.b0, e->sB));
-        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sB));
+                              hipMemcpyHostToDevice, e->sA));
+        if (timed) HIPCHK(hipEventRecord(S.b0, e->sA));
+        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
+        HIPCHK(hipEventRecord(S.evA, e->sA));
+        HIPCHK(hipStreamWaitEvent(e->sB, S.evA, 0));
         // one post_serial_front launch per output format present (S16 / ADPCM / F32); within
         // a format the chains are ordered by demodulator and every demodulator's run is padded
         // to whole 64-lane workgroups (-1 = idle lane), so each wave has a uniform demodulator
@@ -917,6 +917,44 @@ int owrx_device_count(void) {
     return n;
 }
 
+// Streams B, C and R run serial recurrences (one lane per chain / row): a handful of waves
+// whose speed is their own instruction issue rate, which halves when DDC waves share their
+// SIMDs.  They get a few dedicated CUs each (OWRX_SERIAL_CUS in total, default 12, 0 = off)
+// and stream A (FFT, DDC, post_parallel) the rest of the chip.
+static hipError_t create_streams(owrx_engine* e) {
+    int ncu = 0;
+    hipError_t err = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device);
+    if (err != hipSuccess) return err;
+    int reserve = 12;
+    if (const char* v = getenv("OWRX_SERIAL_CUS")) reserve = atoi(v);
+    reserve = std::max(0, std::min(reserve, ncu / 4)) / 3 * 3;
+    if (reserve == 0) {
+        for (hipStream_t* st : {&e->sA, &e->sB, &e->sC, &e->sR}) {
+            err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+            if (err != hipSuccess) return err;
+        }
+        return hipSuccess;
+    }
+    const int words = (ncu + 31) / 32;
+    auto mask_range = [&](int lo, int hi) {  // CUs [lo, hi)
+        std::vector<uint32_t> m((size_t)words, 0u);
+        for (int c = lo; c < hi; ++c) m[(size_t)c / 32] |= 1u << (c % 32);
+        return m;
+    };
+    const int per = reserve / 3;
+    const std::vector<uint32_t> mA = mask_range(0, ncu - reserve);
+    const std::vector<uint32_t> mB = mask_range(ncu - reserve, ncu - 2 * per);
+    const std::vector<uint32_t> mC = mask_range(ncu - 2 * per, ncu - per);
+    const std::vector<uint32_t> mR = mask_range(ncu - per, ncu);
+    const std::pair<hipStream_t*, const std::vector<uint32_t>*> sm[] = {
+        {&e->sA, &mA}, {&e->sB, &mB}, {&e->sC, &mC}, {&e->sR, &mR}};
+    for (auto& x : sm) {
+        err = hipExtStreamCreateWithCUMask(x.first, (uint32_t)words, x.second->data());
+        if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+}
+
 int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_engine** out) {
     if (!out || samp_rate <= 0 || max_block <= 0) {
         set_last_error("owrx_engine_create: bad arguments");
@@ -938,11 +976,7 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
         owrx_engine_destroy(e);
         return OWRX_EIO;
     };
-    if (hipStreamCreateWithFlags(&e->sA, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->sB, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->sC, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->sR, hipStreamNonBlocking) != hipSuccess)
-        return fail("stream");
+    if (create_streams(e) != hipSuccess) return fail("stream");
     for (auto& r : e->rslots) {
         r.stream = e->sR;
         if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||

@@ -14,6 +14,7 @@
 //   cost about one chain.
 // chain_adpcm (stream C, one LANE per chain): AdpcmEncoder(sync=True).  Streams B and C run
 //   concurrently with the next blocks' stream-A work.
+#include <climits>
 #include <type_traits>
 
 #include "owrx_types.h"
@@ -347,13 +348,14 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     const int c = sl.c;
     const ChainPost* Pp = posts + c;
     const int n = sl.active ? (int)counts[c].n_sq : 0;
-    int nmax = n, nmin = n;
+    // idle lanes compute along on their workgroup's first chain and never store
+    int nmax = n, nmin = sl.active ? n : INT_MAX;
     for (int o = 32; o > 0; o >>= 1) {
         nmax = max(nmax, __shfl_xor(nmax, o));
         nmin = min(nmin, __shfl_xor(nmin, o));
     }
     const int nchunks = (nmax + kSerChunk - 1) / kSerChunk;
-    const int nfull = nmin / kSerChunk;  // chunks in which every lane has kSerChunk samples
+    const int nfull = nmin / kSerChunk;  // chunks in which every active lane has kSerChunk samples
     const AgcParams agcp = Pp->agc;
     ChainStateS* sp = Pp->sstate;
     const int demod = __builtin_amdgcn_readfirstlane(Pp->demod);  // uniform (see ser_lane)
@@ -444,7 +446,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                         a = g * q.x;
                     }
                     const int64_t qi = base + j;
-                    const bool valid = full || qi < n;
+                    const bool valid = sl.active && (full || qi < n);
                     if (OUT == 2) {
                         if (valid && 4 * qi + 4 <= Pp->out_cap) gp(reinterpret_cast<float*>(Pp->out))[qi] = a;
                     } else if (OUT == 0) {
@@ -489,19 +491,19 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     const auto src = gp(Pp->s16);
     const auto out = gp(Pp->out);
     const int64_t cap = Pp->out_cap;
-    AdpcmFast ad{st0.adpcm.index, st0.adpcm.pred, (int)kAdpcmStep[st0.adpcm.index]};
+    AdpcmTab ad = adpcm_tab_state(st0.adpcm);
     int has_left = st0.has_left;
     int left = st0.left_code;
     int64_t bytes = st0.adpcm_bytes;
     int until_sync = 0;  // data bytes before the next "SYNC" frame (set below)
-    int64_t ob = 0;
+    int ob = 0;  // bytes staged this block (< 2^31)
     auto frame = [&]() {
-        if (ob + 8 <= cap) {
+        if (sl.active && ob + 8 <= cap) {
             out[ob] = (uint8_t)'S';
             out[ob + 1] = (uint8_t)'Y';
             out[ob + 2] = (uint8_t)'N';
             out[ob + 3] = (uint8_t)'C';
-            const uint32_t w1 = (uint32_t)(uint16_t)ad.index | ((uint32_t)(uint16_t)ad.pred << 16);
+            const uint32_t w1 = (uint32_t)(uint16_t)ad.index() | ((uint32_t)(uint16_t)ad.pred << 16);
             for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
         }
         ob += 8;
@@ -520,7 +522,8 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     until_sync = (int)((kAdpcmSyncPeriod - (bytes % kAdpcmSyncPeriod)) % kAdpcmSyncPeriod);
     // pairs (i0 + 2j, i0 + 2j + 1); a byte starts at every pair
     const int np = (n - i0) >> 1;
-    int npmax = np, npmin = np;
+    // idle lanes run along on their workgroup's first chain (reads only; stores are masked)
+    int npmax = np, npmin = sl.active ? np : INT_MAX;
     for (int o = 32; o > 0; o >>= 1) {
         npmax = max(npmax, __shfl_xor(npmax, o));
         npmin = min(npmin, __shfl_xor(npmin, o));
@@ -529,30 +532,55 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     int cur[8], nxt[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) cur[q] = x[q];  // scratch slack: never out of bounds
-    auto quad = [&](int j, auto fl) {  // four pairs
-        constexpr bool FULL = decltype(fl)::value;
+    // whole quads (4 pairs) of every lane: a "SYNC" check only when some lane is within 4
+    // bytes of its next frame, no capacity checks (out_cap holds a block's worst case)
+    int j = 0;
+    for (; j + 4 <= npmin; j += 4) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const bool valid = FULL || j + u < np;
-            const AdpcmFast keep = ad;
-            if (valid && until_sync == 0) frame();
-            const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
-            const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
-            if (FULL || valid) {
-                if (ob < cap) out[ob] = (uint8_t)(c0 | (c1 << 4));
+        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * j + 8 + q];
+        if (__any(until_sync < 4)) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (until_sync == 0) frame();
+                const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
+                const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
+                if (sl.active) out[ob] = (uint8_t)(c0 | (c1 << 4));
                 ob++;
                 until_sync--;
             }
-            if (!FULL && !valid) ad = keep;
-        }
-    };
-    for (int j = 0; j < npmax; j += 4) {
+        } else {
+            int b[4];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * j + 8 + q];
-        if (j + 4 <= npmin) quad(j, std::true_type{});
-        else quad(j, std::false_type{});
+            for (int u = 0; u < 4; ++u) {
+                const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
+                const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
+                b[u] = c0 | (c1 << 4);
+            }
+            if (sl.active) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) out[ob + u] = (uint8_t)b[u];
+            }
+            ob += 4;
+            until_sync -= 4;
+        }
 #pragma unroll
         for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    }
+    // ragged tail: per pair, lanes past their end keep state
+    for (; j < npmax; ++j) {
+        const bool valid = j < np;
+        const int v0 = x[2 * j], v1 = x[2 * j + 1];
+        const AdpcmTab keep = ad;
+        if (valid && until_sync == 0) frame();
+        const int c0 = adpcm_encode_tab(ad, v0, NS);
+        const int c1 = adpcm_encode_tab(ad, v1, NS);
+        if (valid) {
+            if (ob < cap) out[ob] = (uint8_t)(c0 | (c1 << 4));
+            ob++;
+            until_sync--;
+        } else {
+            ad = keep;
+        }
     }
     bytes += np;
     // an odd last sample starts a byte that the next block completes
@@ -562,7 +590,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
         has_left = 1;
     }
     if (!sl.active) return;
-    sp->adpcm.index = ad.index;
+    sp->adpcm.index = ad.index();
     sp->adpcm.pred = ad.pred;
     sp->has_left = has_left;
     sp->left_code = left;

@@ -208,96 +208,59 @@ OWRX_DEV int adpcm_encode(AdpcmState& s, int sample) {
     return code;
 }
 
-// Same encoder with the step-table lookup taken off the dependency chain: the five possible
-// next steps (index -1, +2, +4, +6, +8, clamped) are read from an LDS copy of the table while
-// this sample's code is being formed, then selected by the code bits.  Bit-identical to
+// Table-driven variant.  NS[index * 8 + magnitude] packs everything the successor needs:
+//   bits 0..14 next step, 16..27 next index * 8 (its NS row), 28..30 the magnitude itself,
+// so the eight possible successors of the current index come in with two 16-byte LDS reads
+// issued before the sample is quantised, the successor is picked by the three magnitude bits
+// (a 3-level select, no index clamping or table lookup on the dependency chain) and the code
+// nibble falls out of the same word.  State: AdpcmTab{rec, pred}.  Bit-identical to
 // adpcm_encode.
-struct AdpcmFast {
-    int index;
-    int pred;
-    int step;
-};
-
-OWRX_DEV AdpcmFast adpcm_fast_init(AdpcmState s, const int16_t* T) {
-    return AdpcmFast{s.index, s.pred, (int)T[s.index]};
-}
-
-OWRX_DEV int adpcm_encode_fast(AdpcmFast& s, int sample, const int16_t* __restrict__ T) {
-    // branch-free: every decision is a mask / select (no exec-mask regions in the hot loops)
-    const int idx = s.index;
-    const int cm1 = T[max(idx - 1, 0)];
-    const int c2 = T[min(idx + 2, 88)];
-    const int c4 = T[min(idx + 4, 88)];
-    const int c6 = T[min(idx + 6, 88)];
-    const int c8 = T[min(idx + 8, 88)];
-    const int step = s.step;
-    int diff = sample - s.pred;
-    const int sgn = diff >> 31;        // -1 if negative
-    diff = (diff ^ sgn) - sgn;         // |diff|
-    int dq = step >> 3;
-    int ts = step;
-    const int m4 = -(int)(diff >= ts);
-    diff -= ts & m4;
-    dq += ts & m4;
-    ts >>= 1;
-    const int m2 = -(int)(diff >= ts);
-    diff -= ts & m2;
-    dq += ts & m2;
-    ts >>= 1;
-    const int m1 = -(int)(diff >= ts);
-    dq += ts & m1;
-    const int p = s.pred + ((dq ^ sgn) - sgn);
-    s.pred = min(max(p, -32768), 32767);
-    const int mag = (m4 & 4) | (m2 & 2) | (m1 & 1);
-    const int ni = m4 ? idx + 2 * ((mag & 3) + 1) : idx - 1;
-    const int hi_step = m2 ? (m1 ? c8 : c6) : (m1 ? c4 : c2);
-    s.step = m4 ? hi_step : cm1;
-    s.index = min(max(ni, 0), 88);
-    return mag | (sgn & 8);
-}
-
-// Table-driven variant: NS[index * 8 + magnitude] = (next index << 16) | next step, so the
-// eight possible successors of the current index come in with two 16-byte LDS reads issued
-// before the sample is quantised, and the successor is picked by the three magnitude bits
-// (a 3-level select) -- no index clamping or table lookup on the dependency chain.
-// Bit-identical to adpcm_encode.
 constexpr int kAdpcmTabEntries = 89 * 8;
+
+OWRX_DEV uint32_t adpcm_tab_rec(int index, int mag) {
+    return (uint32_t)kAdpcmStep[index] | ((uint32_t)(index * 8) << 16) | ((uint32_t)mag << 28);
+}
 
 OWRX_DEV void adpcm_tab_fill(uint32_t* NS, int tid, int nthreads) {
     for (int e = tid; e < kAdpcmTabEntries; e += nthreads) {
         const int i = e >> 3, m = e & 7;
         int ni = i + kAdpcmIndex[m];
         ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
-        NS[e] = ((uint32_t)ni << 16) | (uint32_t)kAdpcmStep[ni];
+        NS[e] = adpcm_tab_rec(ni, m);
     }
 }
 
-OWRX_DEV int adpcm_encode_tab(AdpcmFast& s, int sample, const uint32_t* __restrict__ NS) {
-    const uint4 r0 = *reinterpret_cast<const uint4*>(NS + s.index * 8);
-    const uint4 r1 = *reinterpret_cast<const uint4*>(NS + s.index * 8 + 4);
-    const int step = s.step;
-    int d = sample - s.pred;
+struct AdpcmTab {
+    uint32_t rec;  // step | (index * 8) << 16 | last magnitude << 28
+    int pred;
+    OWRX_DEV int index() const { return (int)((rec >> 16) & 0xfffu) >> 3; }
+};
+
+OWRX_DEV AdpcmTab adpcm_tab_state(AdpcmState s) { return AdpcmTab{adpcm_tab_rec(s.index, 0), s.pred}; }
+
+OWRX_DEV int adpcm_encode_tab(AdpcmTab& s, int sample, const uint32_t* __restrict__ NS) {
+    const uint32_t row = (s.rec >> 16) & 0xfffu;  // index * 8
+    const uint4 r0 = *reinterpret_cast<const uint4*>(NS + row);
+    const uint4 r1 = *reinterpret_cast<const uint4*>(NS + row + 4);
+    const int step = (int)(s.rec & 0x7fffu);
+    const int h = step >> 1, q = step >> 2, s3 = step >> 3;
+    const int d = sample - s.pred;
     const int sgn = d >> 31;
-    int a = (d ^ sgn) - sgn;
+    int a = max(d, -d);
     const bool m4 = a >= step;
     const int t4 = m4 ? step : 0;
     a -= t4;
-    const int h = step >> 1;
     const bool m2 = a >= h;
     const int t2 = m2 ? h : 0;
     a -= t2;
-    const int q = step >> 2;
     const bool m1 = a >= q;
-    const int t1 = m1 ? q : 0;
-    const int dq = (step >> 3) + t4 + t2 + t1;
+    const int dq = s3 + t4 + t2 + (m1 ? q : 0);
     const int p = s.pred + ((dq ^ sgn) - sgn);
     s.pred = min(max(p, -32768), 32767);
     const uint32_t lo = m2 ? (m1 ? r0.w : r0.z) : (m1 ? r0.y : r0.x);
     const uint32_t hi = m2 ? (m1 ? r1.w : r1.z) : (m1 ? r1.y : r1.x);
-    const uint32_t rec = m4 ? hi : lo;
-    s.index = (int)(rec >> 16);
-    s.step = (int)(rec & 0xffffu);
-    return (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0) | (sgn & 8);
+    s.rec = m4 ? hi : lo;
+    return (int)(s.rec >> 28) | (sgn & 8);
 }
 
 }  // namespace owrx
