@@ -23,7 +23,7 @@ OWRX_DEV uint32_t pack_state(const AdpcmTab& s) {
     return ((uint32_t)s.index() << 16) | ((uint32_t)s.pred & 0xffffu);
 }
 OWRX_DEV AdpcmTab unpack_state(uint32_t v) {
-    return AdpcmTab{adpcm_tab_rec((int)(v >> 16), 0), (int)(int16_t)(v & 0xffffu)};
+    return AdpcmTab{adpcm_tab_rec((int)(v >> 16)), (int)(int16_t)(v & 0xffffu)};
 }
 
 template <int WIN>
@@ -54,7 +54,7 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int gues
         if (tid == 0) {
             st = unpack_state(start);
         } else if (guess_index >= 0) {
-            st = AdpcmTab{adpcm_tab_rec(guess_index, 0), (int)L.x[b0 - 1]};
+            st = AdpcmTab{adpcm_tab_rec(guess_index), (int)L.x[b0 - 1]};
         } else {
             // predictor = previous sample, step index from the local slope
             const int d = abs((int)L.x[b0 - 1] - (int)L.x[b0 - 2]);
@@ -63,7 +63,7 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int gues
                 const int mid = (lo + hi) >> 1;
                 if (T[mid] < d) lo = mid + 1; else hi = mid;
             }
-            st = AdpcmTab{adpcm_tab_rec(lo, 0), (int)L.x[b0 - 1]};
+            st = AdpcmTab{adpcm_tab_rec(lo), (int)L.x[b0 - 1]};
         }
         L.seg_start[tid] = pack_state(st);
         for (int t = b0; t < b1; ++t) {

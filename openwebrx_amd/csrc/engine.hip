@@ -11,6 +11,7 @@
 // Block k's B and C work runs concurrently with block k+1's A work; staging buffers are
 // double-buffered by block parity and drained into host rings that the pycsdr binding reads.
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -917,18 +918,19 @@ int owrx_device_count(void) {
     return n;
 }
 
-// Streams B, C and R run serial recurrences (one lane per chain / row): a handful of waves
-// whose speed is their own instruction issue rate, which halves when DDC waves share their
-// SIMDs.  They get a few dedicated CUs each (OWRX_SERIAL_CUS in total, default 12, 0 = off)
-// and stream A (FFT, DDC, post_parallel) the rest of the chip.
+// Streams B, C and R run per-chain / per-row recurrences: a handful of waves whose speed is
+// their own instruction issue, which halves when DDC waves share their SIMDs.  They get
+// dedicated CUs (OWRX_SERIAL_CUS = "B,C,R" counts, default "4,4,4"; "0" = no masks) and
+// stream A (FFT, DDC, post_parallel) the rest of the chip.
 static hipError_t create_streams(owrx_engine* e) {
     int ncu = 0;
     hipError_t err = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device);
     if (err != hipSuccess) return err;
-    int reserve = 12;
-    if (const char* v = getenv("OWRX_SERIAL_CUS")) reserve = atoi(v);
-    reserve = std::max(0, std::min(reserve, ncu / 4)) / 3 * 3;
-    if (reserve == 0) {
+    int nb = 4, nc = 4, nr = 4;
+    if (const char* v = getenv("OWRX_SERIAL_CUS")) {
+        if (sscanf(v, "%d,%d,%d", &nb, &nc, &nr) != 3) nb = nc = nr = 0;
+    }
+    if (nb <= 0 || nc <= 0 || nr <= 0 || nb + nc + nr > ncu / 2) {
         for (hipStream_t* st : {&e->sA, &e->sB, &e->sC, &e->sR}) {
             err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
             if (err != hipSuccess) return err;
@@ -941,11 +943,11 @@ static hipError_t create_streams(owrx_engine* e) {
         for (int c = lo; c < hi; ++c) m[(size_t)c / 32] |= 1u << (c % 32);
         return m;
     };
-    const int per = reserve / 3;
-    const std::vector<uint32_t> mA = mask_range(0, ncu - reserve);
-    const std::vector<uint32_t> mB = mask_range(ncu - reserve, ncu - 2 * per);
-    const std::vector<uint32_t> mC = mask_range(ncu - 2 * per, ncu - per);
-    const std::vector<uint32_t> mR = mask_range(ncu - per, ncu);
+    const int a_end = ncu - nb - nc - nr;
+    const std::vector<uint32_t> mA = mask_range(0, a_end);
+    const std::vector<uint32_t> mB = mask_range(a_end, a_end + nb);
+    const std::vector<uint32_t> mC = mask_range(a_end + nb, a_end + nb + nc);
+    const std::vector<uint32_t> mR = mask_range(a_end + nb + nc, ncu);
     const std::pair<hipStream_t*, const std::vector<uint32_t>*> sm[] = {
         {&e->sA, &mA}, {&e->sB, &mB}, {&e->sC, &mC}, {&e->sR, &mR}};
     for (auto& x : sm) {

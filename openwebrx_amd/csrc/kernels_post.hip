@@ -313,15 +313,16 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
 
 // ---------------------------------------------------------------------------------------------
 // post_serial_front: the per-chain recurrences after the demodulator, one LANE per chain
-// (64 chains per workgroup), three waves pipelined by chunks of kSerChunk samples through LDS:
-//   wave 0   NfmDeemphasis | DcBlock and the AGC envelope (chunk c) -> (u, env) in LDS
-//   wave 1,2 gain = reference / env (clamped), a = u * gain, Convert (chunk c-1; even / odd
-//            samples): int16 to the output slot (S16), float (F32), or the chain's int16
-//            scratch for the ADPCM encoder (chain_adpcm below)
+// (64 chains per workgroup), four waves pipelined by chunks of kSerChunk samples through LDS:
+//   wave 0    NfmDeemphasis | DcBlock and the AGC envelope (chunk c) -> (u, env) in LDS
+//   wave 1-3  gain = reference / env (clamped), a = u * gain, Convert (chunk c-1, every third
+//             sample each -- the IEEE division makes this the heavier half): int16 to the
+//             output slot (S16), float (F32), or the chain's int16 scratch for the ADPCM
+//             encoder (chain_adpcm below)
 // The arithmetic is exactly deemph_step / dcblock_step / agc_step / convert_s16 split at the
 // AGC gain, so the result is bit-identical to the sequential order (oracle orc_agc etc.).
 constexpr int kSerChunk = 64;
-constexpr int kFrontThreads = 192;
+constexpr int kFrontThreads = 256;  // wave 0: recurrences, waves 1-3: gain + Convert
 
 // Lane -> chain for the serial kernels.  The host orders `sel` by demodulator and pads every
 // demodulator's run to whole workgroups with -1 (inactive lanes), so the demodulator is
@@ -366,19 +367,19 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
         AgcState agc = sp->agc;
         const float alpha = Pp->deemph_alpha, beta = Pp->deemph_beta;
         const auto dem = gp(Pp->dem);
+        // inputs stream through 8 registers, the next 8 always in flight (across chunks too;
+        // the demodulator slot has slack past the end)
+        float cur[8], nxt[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[j] = dem[j];
         auto run = [&](auto dm, auto fl, int ch) {
             constexpr int DM = decltype(dm)::value;
             constexpr bool FULL = decltype(fl)::value;
             const int base = ch * kSerChunk;
             float2(*dst)[64] = ue[ch & 1];
-            float cur[8], nxt[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) cur[j] = dem[base + j];  // slack: never out of bounds
             for (int i = 0; i < kSerChunk; i += 8) {
-                if (i + 8 < kSerChunk) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) nxt[j] = dem[base + i + 8 + j];
-                }
+                for (int j = 0; j < 8; ++j) nxt[j] = dem[base + i + 8 + j];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float v = cur[j];
@@ -428,7 +429,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             if (OUT == 0) counts[c].out_bytes = 2 * (int64_t)n;
         }
     } else {
-        // ---- gain + Convert (wave 1: even samples, wave 2: odd), one chunk behind
+        // ---- gain + Convert (waves 1..3 take every third sample), one chunk behind
         for (int it = 0; it < nchunks + 1; ++it) {
             const int ch = it - 1;
             if (ch >= 0) {
@@ -436,7 +437,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                 const float2(*srcu)[64] = ue[ch & 1];
                 const bool full = ch < nfull;
 #pragma unroll 8
-                for (int j = wave - 1; j < kSerChunk; j += 2) {
+                for (int j = wave - 1; j < kSerChunk; j += kFrontThreads / 64 - 1) {
                     const float2 q = srcu[j][lane];
                     float a;
                     {
@@ -529,42 +530,64 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
         npmin = min(npmin, __shfl_xor(npmin, o));
     }
     const auto x = src + i0;
-    int cur[8], nxt[8];
+    // samples stream through registers two quads ahead (scratch slack: never out of bounds)
+    int cur[8], nx1[8], nxt[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) cur[q] = x[q];  // scratch slack: never out of bounds
-    // whole quads (4 pairs) of every lane: a "SYNC" check only when some lane is within 4
-    // bytes of its next frame, no capacity checks (out_cap holds a block's worst case)
+    for (int q = 0; q < 8; ++q) {
+        cur[q] = x[q];
+        nx1[q] = x[8 + q];
+    }
+    // Whole quads (4 pairs) of every active lane, in runs that no lane's next "SYNC" frame
+    // interrupts (frames are 1001 bytes apart, so runs average ~30 pairs with 32 lanes): the
+    // run loop has no per-pair checks at all; the quad that reaches a frame is done checked.
+    // No capacity checks (out_cap holds a block's worst case).
+    auto quad_fast = [&](int jq) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * jq + 16 + q];
+        int b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
+            const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
+            b[u] = c0 | (c1 << 4);
+        }
+        if (sl.active) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) out[ob + u] = (uint8_t)b[u];
+        }
+        ob += 4;
+        until_sync -= 4;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            cur[q] = nx1[q];
+            nx1[q] = nxt[q];
+        }
+    };
     int j = 0;
-    for (; j + 4 <= npmin; j += 4) {
+    while (j + 4 <= npmin) {
+        int us = sl.active ? until_sync : INT_MAX;
+        for (int o = 32; o > 0; o >>= 1) us = min(us, __shfl_xor(us, o));
+        const int run = min(us >> 2, (npmin - j) >> 2);
+        for (int r = 0; r < run; ++r, j += 4) quad_fast(j);
+        if (j + 4 > npmin) break;
+        // a frame falls inside this quad for some lane
 #pragma unroll
-        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * j + 8 + q];
-        if (__any(until_sync < 4)) {
+        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * j + 16 + q];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (until_sync == 0) frame();
-                const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
-                const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
-                if (sl.active) out[ob] = (uint8_t)(c0 | (c1 << 4));
-                ob++;
-                until_sync--;
-            }
-        } else {
-            int b[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
-                const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
-                b[u] = c0 | (c1 << 4);
-            }
-            if (sl.active) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) out[ob + u] = (uint8_t)b[u];
-            }
-            ob += 4;
-            until_sync -= 4;
+        for (int u = 0; u < 4; ++u) {
+            if (until_sync == 0) frame();
+            const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
+            const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
+            if (sl.active) out[ob] = (uint8_t)(c0 | (c1 << 4));
+            ob++;
+            until_sync--;
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+        for (int q = 0; q < 8; ++q) {
+            cur[q] = nx1[q];
+            nx1[q] = nxt[q];
+        }
+        j += 4;
     }
     // ragged tail: per pair, lanes past their end keep state
     for (; j < npmax; ++j) {

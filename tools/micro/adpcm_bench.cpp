@@ -31,7 +31,17 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
 #pragma unroll
         for (int u = 0; u < 8; u += 2) {
             int c0, c1;
-            if (V == 0 || V == 2) {
+            if (V == 3) {
+                c0 = adpcm_encode_tab(ad, cur[u], NS);
+                c1 = adpcm_encode_tab(ad, cur[u + 1], NS);
+            } else if (V == 4) {
+                const int e0 = adpcm_encode_tab(ad, cur[u], NS);
+                const int f0 = adpcm_encode_tab(ad2, src2[j + u], NS);
+                const int e1 = adpcm_encode_tab(ad, cur[u + 1], NS);
+                const int f1 = adpcm_encode_tab(ad2, src2[j + u + 1], NS);
+                c0 = e0 ^ f0;
+                c1 = e1 ^ f1;
+            } else if (V == 0 || V == 2) {
                 c0 = adpcm_encode_tab(ad, cur[u], NS);
                 c1 = adpcm_encode_tab(ad, cur[u + 1], NS);
             } else {  // two streams per lane, interleaved
@@ -42,13 +52,13 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
                 c0 = e0 ^ f0;
                 c1 = e1 ^ f1;
             }
-            if (V < 2) o[(j + u) >> 1] = (uint8_t)(c0 | (c1 << 4));
+            if (V != 2) o[(j + u) >> 1] = (uint8_t)(c0 | (c1 << 4));
             else acc += c0 + c1;
         }
         for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
     }
     long long t1 = clock64();
-    if (V >= 2) o[0] = (uint8_t)acc;
+    if (V == 2) o[0] = (uint8_t)acc;
     if (lane == 0) *cyc = t1 - t0;
 }
 
@@ -92,5 +102,7 @@ int main(int argc, char** argv) {
     run("table encoder + byte stores", kern<0>, 1.0);
     run("x2 streams/lane (per stream)", kern<1>, 2.0);
     run("table encoder, no stores", kern<2>, 1.0);
+    run("single dependent read + stores", kern<3>, 1.0);
+    run("single read x2 streams/lane (per stream)", kern<4>, 2.0);
     return 0;
 }
