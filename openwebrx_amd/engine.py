@@ -24,6 +24,13 @@ def _scratch(nbytes):
     return b
 
 
+def nfm_deemphasis_alpha(sample_rate):
+    """NfmDeemphasis(sampleRate) coefficient (same as design.cpp nfm_deemphasis_alpha)."""
+    dt = 1.0 / float(sample_rate)
+    tau = 1.0 / (2.0 * np.pi * 300.0)
+    return float(np.float32(dt / (tau + dt)))
+
+
 def device_count():
     n = lib.owrx_device_count()
     return n if n > 0 else 0

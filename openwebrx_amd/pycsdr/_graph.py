@@ -1,0 +1,331 @@
+"""Fusion of pycsdr module graphs onto the GPU engine.
+
+A *source* buffer is a COMPLEX_FLOAT Buffer whose writer is not a fusable module (the
+wideband IQ buffer fed by TcpSource / the SDR source, owrx/source/__init__.py:307-330).
+Every reader of a source buffer that belongs to a Shift (Selector, csdr/chain/selector.py:95)
+or an Fft (FftChain, csdr/chain/fft.py:34) starts a *segment*: the modules linked through
+single-reader Buffers downstream of it.  plan_segment() recognises the two hot-path shapes
+and returns the engine parameters; one EngineDriver per source buffer owns one engine, runs
+every recognised segment on it (one DDC launch for all chains that share a FirDecimate
+design) and writes each segment's output into the writer of its last module.
+
+The graph is re-planned at the next block boundary after any (re)wiring; setters that do not
+change the shape (Shift.setRate, Bandpass.setBandpass, Squelch.setSquelchLevel,
+Fft.setEveryNSamples) are applied to the live engine objects.
+"""
+import threading
+import weakref
+
+import numpy as np
+
+_drivers = weakref.WeakValueDictionary()  # id(source buffer) -> EngineDriver
+_lock = threading.RLock()
+
+BLOCK = 1 << 18  # IQ samples per engine block (26 ms at 10 Msps)
+
+
+def changed(module, structural=True):
+    """A module was (re)wired or re-parameterised: find its source buffer's driver."""
+    from . import modules as M
+    with _lock:
+        head = _find_head(module)
+        if head is None:
+            return
+        src = head.reader._buffer
+        if src.getFormat() != M.Format.COMPLEX_FLOAT:
+            return
+        drv = _drivers.get(id(src))
+        if drv is None:
+            drv = EngineDriver(src)
+            _drivers[id(src)] = drv
+        drv.mark_dirty(structural)
+
+
+def _upstream(module):
+    r = module.reader
+    if r is None:
+        return None
+    w = r._buffer.writer_module
+    return w if (w is not None and w.fusable) else None
+
+
+def _find_head(module):
+    """Walk upstream to the module that reads a source buffer."""
+    seen = set()
+    m = module
+    while m is not None and id(m) not in seen:
+        seen.add(id(m))
+        up = _upstream(m)
+        if up is None:
+            return m if m.reader is not None else None
+        m = up
+    return None
+
+
+def _downstream(module):
+    from .modules import Buffer
+    w = module.writer
+    if not isinstance(w, Buffer):
+        return None
+    readers = [r for r in w._readers if r.module is not None and not r._stopped]
+    if len(readers) != 1:
+        return None
+    nxt = readers[0].module
+    return nxt if nxt.fusable else None
+
+
+def _walk(head):
+    mods = [head]
+    while True:
+        nxt = _downstream(mods[-1])
+        if nxt is None or nxt in mods:
+            return mods
+        mods.append(nxt)
+
+
+def plan_segment(head):
+    """(kind, params, modules) for a recognised segment starting at `head`, else None.
+
+    kind "chain": params = dict of owrx_chain_params fields (+ "power_writer");
+    kind "waterfall": params = dict(fft_size, hop, avg, add_db, adpcm)."""
+    from . import modules as M
+    from .. import _lib
+    mods = _walk(head)
+    i = 0
+
+    def take(cls):
+        nonlocal i
+        if i < len(mods) and isinstance(mods[i], cls):
+            i += 1
+            return mods[i - 1]
+        return None
+
+    if isinstance(head, M.Fft):
+        fft = take(M.Fft)
+        avg = take(M.LogAveragePower) or take(M.LogPower)
+        swap = take(M.FftSwap)
+        if avg is None or swap is None or fft.every_n_samples <= 0:
+            return None
+        if isinstance(avg, M.LogAveragePower) and avg.fft_size not in (0, fft.size):
+            return None
+        adp = take(M.FftAdpcm)
+        used = mods[:i]
+        if used[-1].writer is None:
+            return None
+        return ("waterfall",
+                dict(fft_size=fft.size, hop=fft.every_n_samples,
+                     avg=avg.avg_number if isinstance(avg, M.LogAveragePower) else 1,
+                     add_db=avg.add_db, adpcm=adp is not None), used)
+
+    if not isinstance(head, M.Shift):
+        return None
+    shift = take(M.Shift)
+    fir = take(M.FirDecimate)
+    if fir is None:
+        return None
+    frac = take(M.FractionalDecimator)
+    bp = take(M.Bandpass)
+    sq = take(M.Squelch)
+    fm = take(M.FmDemod)
+    if fm is not None:
+        lim = take(M.Limit)
+        de = take(M.NfmDeemphasis)
+        if lim is None or de is None or lim.max_amplitude != 1.0:
+            return None
+        demod, audio_rate = _lib.DEMOD_NFM, de.sample_rate
+    elif take(M.AmDemod) is not None:
+        if take(M.DcBlock) is None:
+            return None
+        demod, audio_rate = _lib.DEMOD_AM, 12000
+    elif take(M.RealPart) is not None:
+        demod, audio_rate = _lib.DEMOD_SSB, 12000
+    else:
+        return None
+    agc = take(M.Agc)
+    if agc is None:
+        return None
+    output = _lib.OUT_F32
+    if take(M.Convert) is not None:
+        output = _lib.OUT_S16
+        enc = take(M.AdpcmEncoder)
+        if enc is not None:
+            if not enc.sync:
+                return None
+            output = _lib.OUT_ADPCM
+    used = mods[:i]
+    if used[-1].writer is None:
+        return None
+    p = dict(shift_rate=shift.rate, decimation=fir.decimation, transition=fir.transition,
+             cutoff=fir.cutoff, frac_rate=frac.rate if frac is not None else 1.0,
+             bandpass=0, bp_low=0.0, bp_high=0.0, bp_transition=0.0,
+             sq_length=750, sq_decimation=5, sq_hang=0, sq_flush=0, sq_report=0, sq_level=0.0,
+             demod=demod, agc_profile=agc.profile.engine_id,
+             agc_initial_gain=-1.0 if agc.initial_gain is None else agc.initial_gain,
+             agc_max_gain=-1.0 if agc.max_gain is None else agc.max_gain,
+             audio_rate=audio_rate, output=output, power_writer=None)
+    if bp is not None and bp.low_cut is not None and bp.high_cut is not None:
+        p.update(bandpass=1, bp_low=bp.low_cut, bp_high=bp.high_cut,
+                 bp_transition=bp.transition)
+    if sq is not None:
+        p.update(sq_length=sq.length, sq_decimation=sq.decimation, sq_hang=sq.hang_length,
+                 sq_flush=sq.flush_length, sq_report=sq.report_interval, sq_level=sq.level,
+                 power_writer=sq.power_writer)
+    return ("chain", p, used)
+
+
+def chain_params_struct(p):
+    from .. import _lib
+    s = _lib.ChainParams()
+    for k, v in p.items():
+        if k != "power_writer":
+            setattr(s, k, v)
+    return s
+
+
+class EngineDriver:
+    """One engine per source buffer: reads it, runs every fused segment, writes outputs."""
+
+    def __init__(self, source):
+        self.source = source
+        self.engine = None
+        self.segments = {}  # head id -> (kind, params, modules, engine object)
+        self._dirty = True
+        self._closing = False
+        self.reader = source.getReader()  # before any further write: nothing is missed
+        self._thread = threading.Thread(target=self._run, name="owrx-engine", daemon=True)
+        self._thread.start()
+
+    def mark_dirty(self, structural=True):
+        self._dirty = True
+
+    def _heads(self):
+        from . import modules as M
+        with self.source._cond:
+            rs = list(self.source._readers)
+        return [r.module for r in rs if isinstance(r.module, (M.Shift, M.Fft))
+                and not r.module._stopped]
+
+    def _replan(self):
+        from ..engine import Engine
+        plans = {}
+        for h in self._heads():
+            seg = plan_segment(h)
+            if seg is not None:
+                plans[id(h)] = seg
+        if plans and self.engine is None:
+            self.engine = Engine(1.0, max_block=BLOCK)
+        # drop segments that vanished or changed shape / design parameters
+        for hid in list(self.segments):
+            kind, p, mods, obj = self.segments[hid]
+            new = plans.get(hid)
+            if new is None or new[0] != kind or new[2] != mods or not _compatible(kind, p, new[1]):
+                self._absorb(mods, False)
+                obj.close()
+                del self.segments[hid]
+        for hid, (kind, p, mods) in plans.items():
+            if hid in self.segments:
+                self._update(hid, p)
+                continue
+            if kind == "waterfall":
+                obj = self.engine.waterfall(p["fft_size"], p["hop"], max(1, p["avg"]),
+                                            p["add_db"], p["adpcm"])
+            else:
+                obj = self.engine.chain(chain_params_struct(p))
+            self.segments[hid] = (kind, p, mods, obj)
+            self._absorb(mods, True)
+
+    def _absorb(self, mods, on):
+        for m in mods:
+            m.absorbed = on
+            if on and m is mods[0] and m.reader is not None:
+                m.reader._detach()   # the engine reads the source through its own reader
+
+    def _update(self, hid, p):
+        kind, old, mods, obj = self.segments[hid]
+        if kind == "waterfall":
+            if (old["hop"], old["avg"], old["adpcm"]) != (p["hop"], p["avg"], p["adpcm"]):
+                obj.set(p["hop"], max(1, p["avg"]), p["adpcm"])
+        else:
+            if old["shift_rate"] != p["shift_rate"]:
+                obj.set_shift_rate(p["shift_rate"])
+            if (old["bandpass"], old["bp_low"], old["bp_high"]) != \
+                    (p["bandpass"], p["bp_low"], p["bp_high"]):
+                obj.set_bandpass(p["bp_low"], p["bp_high"]) if p["bandpass"] else \
+                    obj.set_bandpass(None, None)
+            if old["sq_level"] != p["sq_level"]:
+                obj.set_squelch_level(p["sq_level"])
+        self.segments[hid] = (kind, p, mods, obj)
+
+    def _drain(self):
+        for kind, p, mods, obj in list(self.segments.values()):
+            out = mods[-1].writer
+            if kind == "waterfall":
+                data = obj.read()
+                if data and out is not None:
+                    out.write(data)
+            else:
+                data = obj.read_audio()
+                if data and out is not None:
+                    out.write(data)
+                sm = obj.read_smeter()
+                pw = p.get("power_writer")
+                if sm.size and pw is not None:
+                    pw.write(sm.astype(np.float32).tobytes())
+
+    def close(self):
+        """Stop reading the source; the thread pushes what it holds, syncs and drains."""
+        self._closing = True
+        if self.reader is not None:
+            self.reader.stop()
+        self._thread.join()
+
+    def _run(self):
+        pending = []
+        npend = 0
+        while True:
+            data = self.reader.read()
+            if data is None:
+                if pending and self.engine is not None:
+                    with _lock:
+                        self.engine.push(np.concatenate(pending))
+                if self.engine is not None:
+                    with _lock:
+                        self.engine.sync()
+                        self._drain()
+                break
+            with _lock:
+                if self._dirty:
+                    self._dirty = False
+                    self._replan()
+            if self.engine is None:
+                continue
+            x = np.frombuffer(data, dtype=np.complex64)
+            pending.append(x)
+            npend += x.size
+            if npend < BLOCK:
+                continue
+            blk = np.concatenate(pending)
+            pending, npend = [], 0
+            with _lock:
+                self.engine.push(blk)
+                self._drain()
+
+
+def finish(source):
+    """Flush and stop the engine driver of a source buffer (end of stream / tests)."""
+    with _lock:
+        drv = _drivers.pop(id(source), None)
+    if drv is not None:
+        drv.close()
+    return drv
+
+
+def _compatible(kind, old, new):
+    """Parameters that can change on a live engine object (everything else re-creates it)."""
+    if kind == "waterfall":
+        keys = ("fft_size", "add_db")
+    else:
+        keys = ("decimation", "transition", "cutoff", "frac_rate", "bp_transition", "sq_length",
+                "sq_decimation", "sq_hang", "sq_flush", "sq_report", "demod", "agc_profile",
+                "agc_initial_gain", "agc_max_gain", "audio_rate", "output")
+    return all(old[k] == new[k] for k in keys)

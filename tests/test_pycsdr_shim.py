@@ -1,0 +1,295 @@
+"""The pycsdr drop-in (openwebrx_amd.pycsdr): API surface and error behaviour of
+pycsdr.modules / pycsdr.types as the reference calls them, the fusion planner
+against the reference's chain parameters, and (GPU) byte-identical outputs of a module graph
+wired like csdr.chain vs the engine driven directly."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from openwebrx_amd import _lib, params
+from openwebrx_amd import pycsdr
+from openwebrx_amd.pycsdr import _graph
+from openwebrx_amd.pycsdr import modules as M
+from openwebrx_amd.pycsdr.types import AgcProfile, Format
+
+
+class Chain:
+    """What csdr/chain/__init__.py:11-20 does with a worker list: one Buffer between
+    consecutive workers, typed by the producer's output format."""
+
+    def __init__(self, workers):
+        self.workers = workers
+        for a, b in zip(workers, workers[1:]):
+            buf = M.Buffer(a.getOutputFormat())
+            a.setWriter(buf)
+            b.setReader(buf.getReader())
+
+    def setReader(self, r):
+        self.workers[0].setReader(r)
+
+    def setWriter(self, w):
+        self.workers[-1].setWriter(w)
+
+
+def selector(fs, offset, mode, squelch=True):
+    """Modules of Selector(fs, 12000) + setFrequencyOffset + setBandpass
+    (csdr/chain/selector.py:89-166), parameters from openwebrx_amd.params."""
+    d, frac, tbw, cutoff = params.decimation(fs, 12000)
+    shift = M.Shift(0.0)
+    shift.setRate(params.shift_rate(offset, fs))
+    w = [shift, M.FirDecimate(d, tbw, cutoff)]
+    if frac != 1.0:
+        w.append(M.FractionalDecimator(Format.COMPLEX_FLOAT, frac))
+    bp = M.Bandpass(transition=320.0 / 12000, use_fft=True)
+    lo, hi = params.MODE_BANDPASS[mode]
+    bp.setBandpass(lo / 12000, hi / 12000)
+    w.append(bp)
+    if squelch:
+        sq = params.squelch_parameters(12000)
+        w.append(M.Squelch(Format.COMPLEX_FLOAT, length=sq["length"],
+                           decimation=sq["decimation"], hangLength=sq["hangLength"],
+                           flushLength=sq["flushLength"], reportInterval=sq["reportInterval"]))
+    return w
+
+
+def demodulator(mode):
+    """NFm / Am / Ssb (csdr/chain/analog.py:11-52, 119-127)."""
+    agc = M.Agc(Format.FLOAT)
+    if mode == "nfm":
+        agc.setProfile(AgcProfile.SLOW)
+        agc.setMaxGain(3)
+        return [M.FmDemod(), M.Limit(), M.NfmDeemphasis(12000), agc]
+    if mode == "am":
+        agc.setProfile(AgcProfile.SLOW)
+        agc.setInitialGain(200)
+        return [M.AmDemod(), M.DcBlock(), agc]
+    agc.setProfile(AgcProfile("Fast"))
+    return [M.RealPart(), agc]
+
+
+def client_audio(adpcm=True):
+    """ClientAudioChain(FLOAT, 12000, 12000, "adpcm") (csdr/chain/clientaudio.py:6-35)."""
+    w = [M.Convert(Format.FLOAT, Format.SHORT)]
+    if adpcm:
+        w.append(M.AdpcmEncoder(sync=True))
+    return w
+
+
+def fft_chain(n, hop, avg, adpcm=True):
+    """FftChain workers (csdr/chain/fft.py:25-96)."""
+    fft = M.Fft(size=n, every_n_samples=0)
+    fft.setEveryNSamples(hop)
+    w = [fft, M.LogAveragePower(add_db=-70, fft_size=n, avg_number=avg), M.FftSwap(fft_size=n)]
+    if adpcm:
+        w.append(M.FftAdpcm(fft_size=n))
+    return w
+
+
+# ---- API surface (CPU) ---------------------------------------------------------------------
+
+def test_types_and_versions():
+    assert AgcProfile("Fast") is AgcProfile.FAST
+    assert [p.value for p in AgcProfile] == ["Fast", "Slow", "Mid", "Laggy"]
+    assert {f.itemsize for f in Format} == {1, 2, 4, 8}
+    assert tuple(int(x) for x in M.csdr_version.split(".")) >= (0, 18, 0)
+    assert tuple(int(x) for x in M.version.split(".")) >= (0, 18, 0)
+
+
+def test_imports_of_the_reference_resolve():
+    """Every name the reference imports from pycsdr.modules exists."""
+    names = ("AdpcmEncoder Afc Agc AmDemod AudioResampler Bandpass BaudotDecoder Buffer "
+             "Ccir476Decoder Ccir493Decoder Convert CwDecoder DBPskDecoder DcBlock Downmix "
+             "DscDecoder ExecModule FaxDecoder Fft FftAdpcm FftSwap FirDecimate FmDemod "
+             "FractionalDecimator Gain Limit LogAveragePower LogPower Lowpass MFRttyDecoder "
+             "Module NavtexDecoder NfmDeemphasis NoiseFilter Reader RealPart RttyDecoder Shift "
+             "SitorBDecoder SnrSquelch Squelch SstvDecoder TcpSource Throttle TimingRecovery "
+             "VaricodeDecoder WfmDeemphasis Writer csdr_version version").split()
+    for n in names:
+        assert hasattr(M, n), n
+    with pytest.raises(NotImplementedError):
+        M.SstvDecoder()
+
+
+def test_install_registers_pycsdr():
+    import sys
+    pycsdr.install()
+    from pycsdr.modules import Buffer  # noqa: F401  (the reference's import lines)
+    from pycsdr.types import Format as F2
+    assert F2 is Format and sys.modules["pycsdr.modules"] is M
+
+
+def test_buffer_multireader_and_stop():
+    b = M.Buffer(Format.FLOAT)
+    r1, r2 = b.getReader(), b.getReader()
+    b.write(np.arange(5, dtype=np.float32).tobytes() + b"\x01")  # a stray byte stays pending
+    assert np.frombuffer(r1.read(), np.float32).tolist() == [0, 1, 2, 3, 4]
+    assert len(r2.read()) == 20
+    got = []
+    t = threading.Thread(target=lambda: got.append(r1.read()))
+    t.start()
+    time.sleep(0.05)
+    r1.stop()
+    t.join(2)
+    assert got == [None]
+
+
+def test_format_mismatch_raises_valueerror():
+    """setReader / setWriter raise ValueError (callers catch it, csdr/chain/__init__.py:60-84)."""
+    with pytest.raises(ValueError):
+        M.FmDemod().setReader(M.Buffer(Format.FLOAT).getReader())
+    with pytest.raises(ValueError):
+        M.FmDemod().setWriter(M.Buffer(Format.COMPLEX_FLOAT))
+    M.FmDemod().setWriter(M.Buffer(Format.FLOAT))
+
+
+@pytest.mark.parametrize("mode", ["nfm", "am", "usb"])
+def test_planner_matches_reference_chain_params(mode):
+    """A graph wired like ClientDemodulatorChain plans to exactly the engine parameters the
+    reference chain code implies (openwebrx_amd.params, pinned by tests/golden)."""
+    fs, off = 10000000, 123456
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    mods = selector(fs, off, mode) + demodulator(mode) + client_audio()
+    ch = Chain(mods)
+    out = M.Buffer(Format.CHAR)
+    ch.setWriter(out)
+    ch.setReader(wide.getReader())
+    seg = _graph.plan_segment(mods[0])
+    assert seg is not None and seg[0] == "chain" and seg[2] == mods
+    got = _graph.chain_params_struct(seg[1])
+    want = params.chain_params(fs, off, mode, output=_lib.OUT_ADPCM)
+    for name, _ in _lib.ChainParams._fields_:
+        g, w = getattr(got, name), getattr(want, name)
+        assert g == pytest.approx(w, rel=1e-6, abs=1e-12), name
+    _graph.finish(wide)
+
+
+def test_planner_waterfall_and_rewire():
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    mods = fft_chain(4096, 2867, 93)
+    ch = Chain(mods)
+    ch.setWriter(M.Buffer(Format.CHAR))
+    ch.setReader(wide.getReader())
+    kind, p, used = _graph.plan_segment(mods[0])
+    assert kind == "waterfall" and p == dict(fft_size=4096, hop=2867, avg=93, add_db=-70.0,
+                                             adpcm=True)
+    # FftAverager.setFftAverages replaces the averager (csdr/chain/fft.py:13-17)
+    new = M.LogAveragePower(add_db=-70, fft_size=4096, avg_number=10)
+    mods[1].stop()
+    buf = M.Buffer(Format.FLOAT)
+    new.setWriter(buf)
+    mods[2].setReader(buf.getReader())
+    b0 = M.Buffer(Format.COMPLEX_FLOAT)
+    mods[0].setWriter(b0)
+    new.setReader(b0.getReader())
+    kind, p, used = _graph.plan_segment(mods[0])
+    assert p["avg"] == 10 and used[1] is new
+    _graph.finish(wide)
+
+
+def test_unrecognised_graph_is_not_fused():
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    shift = M.Shift(0.1)
+    fm = M.FmDemod()
+    Chain([shift, fm])
+    shift.setReader(wide.getReader())
+    fm.setWriter(M.Buffer(Format.FLOAT))
+    assert _graph.plan_segment(shift) is None
+    _graph.finish(wide)
+
+
+# ---- end to end on the GPU -------------------------------------------------------------
+
+def _collect(buf):
+    r = buf.getReader()
+    out = []
+    t = threading.Thread(target=lambda: [out.append(bytes(x)) for x in iter(r.read, None)])
+    t.start()
+    return r, t, out
+
+
+@pytest.mark.gpu
+def test_pycsdr_graph_equals_engine():
+    """Wideband Buffer -> two ClientDemodulatorChain-shaped graphs + an FftChain graph, fed in
+    odd-sized writes: audio, s-meter and waterfall bytes equal the engine driven directly."""
+    from openwebrx_amd import Engine, synth
+    fs = 2400000
+    modes = ["nfm", "am"]
+    iq, offs = synth.make_iq(fs, 1 << 20, modes)
+    avg, hop = params.fft_parameters(fs, 4096, 9, 0.3)
+
+    wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 22)
+    outs, smeters, graphs = [], [], []
+    for off, mode in zip(offs, modes):
+        mods = selector(fs, off, mode) + demodulator(mode) + client_audio()
+        ch = Chain(mods)
+        out, pw = M.Buffer(Format.CHAR, size=1 << 22), M.Buffer(Format.FLOAT, size=1 << 20)
+        [m for m in mods if isinstance(m, M.Squelch)][0].setPowerWriter(pw)
+        outs.append(_collect(out))
+        smeters.append(_collect(pw))
+        ch.setWriter(out)
+        ch.setReader(wide.getReader())
+        graphs.append(mods)
+    wmods = fft_chain(4096, hop, avg)
+    wch = Chain(wmods)
+    wout = M.Buffer(Format.CHAR, size=1 << 22)
+    wcol = _collect(wout)
+    wch.setWriter(wout)
+    wch.setReader(wide.getReader())
+
+    i = 0
+    for s in [100003, 77777, 300001] * 10:
+        if i >= iq.size:
+            break
+        wide.write(iq[i:i + s].tobytes())
+        i += s
+    while _graph._drivers.get(id(wide)).reader.available() > 0:
+        time.sleep(0.01)
+    _graph.finish(wide)
+    for col in outs + smeters + [wcol]:
+        col[0].stop()
+        col[1].join(5)
+
+    eng = Engine(1.0, max_block=_graph.BLOCK)
+    ref_ch = [eng.chain(params.chain_params(fs, o, m, output=_lib.OUT_ADPCM))
+              for o, m in zip(offs, modes)]
+    wf = eng.waterfall(4096, hop, avg, -70.0, True)
+    for j in range(0, iq.size, _graph.BLOCK):
+        eng.push(iq[j:j + _graph.BLOCK])
+    eng.sync()
+    for k, c in enumerate(ref_ch):
+        assert b"".join(outs[k][2]) == c.read_audio()
+        sm = np.frombuffer(b"".join(smeters[k][2]), np.float32)
+        np.testing.assert_array_equal(sm, c.read_smeter())
+    assert b"".join(wcol[2]) == wf.read()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_standalone_modules_match_oracle():
+    """Modules outside a fused segment run alone on the GPU (one worker each), like csdr's
+    one-thread-per-module: FmDemod -> Limit -> Convert -> AdpcmEncoder on a Buffer graph."""
+    import oracle
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal(40000) + 1j * rng.standard_normal(40000)).astype(np.complex64)
+    src = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 20)
+    mods = [M.FmDemod(), M.Limit(), M.Convert(Format.FLOAT, Format.SHORT),
+            M.AdpcmEncoder(sync=True)]
+    ch = Chain(mods)
+    out = M.Buffer(Format.CHAR, size=1 << 20)
+    r, t, got = _collect(out)
+    ch.setWriter(out)
+    ch.setReader(src.getReader())
+    for i in range(0, x.size, 9999):
+        src.write(x[i:i + 9999].tobytes())
+    want = oracle.adpcm_encode(oracle.convert_s16(oracle.limit(oracle.fmdemod(x))), 1)
+    deadline = time.time() + 30
+    while sum(len(g) for g in got) < len(want) - 1 and time.time() < deadline:
+        time.sleep(0.05)
+    r.stop()
+    t.join(5)
+    for m in mods:
+        m.stop()
+    data = b"".join(got)
+    assert data == want[:len(data)] and len(want) - len(data) <= 1
