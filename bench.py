@@ -99,11 +99,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # ranks beyond the visible GPUs share them (rehearsal on a small box; the driver's scaling
+    # runs have one GPU per rank)
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(os.environ.get("OWRX_DIST_BACKEND", "nccl"), rank=rank,
+                                world_size=world)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -115,8 +119,12 @@ def main():
     modes = ["nfm" if c % 2 == 0 else "am" for c in range(C)]
     from openwebrx_amd.synth import carrier_offsets
     offs = carrier_offsets(fs, C)
-    # rank r listens 37 Hz * r off the carriers: different chains, identical cost
-    plist = [params.chain_params(fs, o + 37 * rank, m) for o, m in zip(offs, modes)]
+    # the job's chains: C per GPU (weak scaling), copy r listening 37 Hz * r off the carriers
+    # (different chains, identical cost), dealt to ranks within (D, taps, mode) groups
+    from openwebrx_amd.multi import IqBroadcast, shard_chains
+    everything = [(o + 37 * r, m) for r in range(world) for o, m in zip(offs, modes)]
+    mine = shard_chains(everything, world, rank, key=lambda it: it[1])
+    plist = [params.chain_params(fs, o, m) for o, m in mine]
 
     block = args.block
     eng = Engine(fs, max_block=block, device=local)
@@ -128,13 +136,11 @@ def main():
 
     nsteps = args.warmup + args.steps
     total = nsteps * block
+    stream = None
     if rank == 0:
         stream = gen_stream_torch(torch, dev, fs, hist + total, modes, offs)
         base = stream.data_ptr() + 8 * hist
-    else:
-        # two windows [history | block], alternated: the engine reads block k's window until
-        # the next process call returns, so block k+1 is assembled in the other one
-        windows = [torch.zeros(hist + block, dtype=torch.complex64, device=dev) for _ in range(2)]
+    bcast = IqBroadcast(torch, dist, dev, hist, block, stream=stream) if dist else None
     torch.cuda.synchronize(dev)
 
     def drain():
@@ -159,19 +165,10 @@ def main():
             t0 = time.perf_counter()
             eng.process_device(base + 8 * i * block, block)
             host_s["process"] += time.perf_counter() - t0
-        else:
-            if rank == 0:
-                blk = stream[hist + i * block: hist + (i + 1) * block]
-                dist.broadcast(blk, src=0)
-                torch.cuda.synchronize(dev)
-                eng.process_device(base + 8 * i * block, block)
-            else:
-                w, prev = windows[i % 2], windows[(i + 1) % 2]
-                w[:hist].copy_(prev[block:block + hist])
-                dst = w[hist:hist + block]
-                dist.broadcast(dst, src=0)
-                torch.cuda.synchronize(dev)
-                eng.process_device(dst.data_ptr(), block)
+        else:  # the one exchange step: rank 0's block to every rank over RCCL
+            t, off = bcast.step(i)
+            torch.cuda.synchronize(dev)
+            eng.process_device(t.data_ptr() + 8 * off, block)
         return drain()
 
     for i in range(args.warmup):

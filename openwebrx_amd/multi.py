@@ -1,0 +1,57 @@
+"""Multi-GPU plumbing: one process per GPU, chains sharded across ranks, the
+wideband IQ broadcast from rank 0 as the only exchange step.
+
+* shard_chains -- round-robin within (decimation, taps, demodulator) groups, so every rank's
+  DDC launch keeps the same per-group tile reuse and the ranks' loads differ by at most one
+  chain per group.
+* IqBroadcast -- rank 0 owns the stream (host ingest or an HBM-resident recording); each
+  block goes to every rank with one torch.distributed broadcast (RCCL over xGMI with the
+  "nccl" backend, gloo in the CPU tests).  Ranks > 0 assemble [history | block] windows,
+  alternating two, because the engine still reads block k (asynchronously) while k+1 arrives
+  (owrx_process_device contract, include/owrx_amd.h).
+No reduction: every rank returns its own chains' outputs to the host.
+"""
+from collections import OrderedDict
+
+
+def shard_chains(items, world, rank, key=lambda it: it):
+    """This rank's share of `items`, dealt round-robin within groups of equal key(item);
+    the dealer position carries over between groups so totals stay balanced."""
+    groups = OrderedDict()
+    for it in items:
+        groups.setdefault(key(it), []).append(it)
+    mine, pos = [], 0
+    for members in groups.values():
+        for it in members:
+            if pos % world == rank:
+                mine.append(it)
+            pos += 1
+    return mine
+
+
+class IqBroadcast:
+    """Per-block IQ distribution.  step(i) returns (tensor, offset) such that the engine can
+    process tensor[offset : offset + block] with tensor[offset - history : offset] holding
+    the preceding samples."""
+
+    def __init__(self, torch, dist, device, history, block, src=0, stream=None):
+        self.torch, self.dist = torch, dist
+        self.history, self.block, self.src = history, block, src
+        self.rank = dist.get_rank()
+        self.stream = stream  # rank src: complex64 tensor [history | blocks...]
+        if self.rank != src:
+            self.windows = [torch.zeros(history + block, dtype=torch.complex64, device=device)
+                            for _ in range(2)]
+
+    def step(self, i):
+        h, b = self.history, self.block
+        lo = 0 if i == 0 else h  # the first broadcast also carries the initial history
+        if self.rank == self.src:
+            blk = self.stream[lo + i * b if i else 0: h + (i + 1) * b]
+            self.dist.broadcast(self.torch.view_as_real(blk), src=self.src)
+            return self.stream, h + i * b
+        w, prev = self.windows[i % 2], self.windows[(i + 1) % 2]
+        if i > 0:
+            w[:h].copy_(prev[b:b + h])
+        self.dist.broadcast(self.torch.view_as_real(w[lo:h + b]), src=self.src)
+        return w, h

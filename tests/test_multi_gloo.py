@@ -1,0 +1,70 @@
+"""N > 1 path on the CPU (gloo, world size 2): chain sharding and the per-block IQ broadcast
+that bench.py / a multi-GPU server run over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from openwebrx_amd import params
+from openwebrx_amd.multi import IqBroadcast, shard_chains
+
+
+def test_shard_chains_balanced_and_disjoint():
+    fs = 10000000
+    items = [(o, m) for o, m in zip(range(0, 256 * 1000, 1000),
+                                    (["nfm", "usb", "cw"] * 100)[:256])]
+    key = lambda it: (params.decimation(fs, 12000)[0], it[1])  # (D, mode): same taps here
+    for world in (1, 2, 4, 8):
+        shards = [shard_chains(items, world, r, key) for r in range(world)]
+        flat = [it for s in shards for it in s]
+        assert sorted(flat) == sorted(items)
+        sizes = [len(s) for s in shards]
+        assert max(sizes) - min(sizes) <= 1
+        for mode in ("nfm", "usb", "cw"):
+            per = [sum(1 for it in s if it[1] == mode) for s in shards]
+            assert max(per) - min(per) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, hist, block, nblocks, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(7)
+    full = torch.complex(torch.randn(hist + nblocks * block, generator=g),
+                         torch.randn(hist + nblocks * block, generator=g))
+    bc = IqBroadcast(torch, dist, "cpu", hist, block, stream=full if rank == 0 else None)
+    ok = True
+    for i in range(nblocks):
+        t, off = bc.step(i)
+        got = t[off - hist: off + block]
+        want = full[i * block: i * block + hist + block]
+        ok &= bool(torch.equal(got, want))
+    # every rank demodulates its own shard: no reduction, only a barrier for the timing
+    dist.barrier()
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_iq_broadcast_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 5, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert res == {0: True, 1: True}
