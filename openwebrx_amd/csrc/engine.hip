@@ -2,14 +2,15 @@
 //
 // Replaces the reference's per-module native threads + ring buffers (pycsdr Buffer/Reader,
 // csdr modules; callers owrx/fft.py:36-73 and owrx/dsp.py:39-72, 835-863) with a block
-// scheduler over three HIP streams:
-//   A (main):   wf_fft_power + wf_finalize per FftChain; ddc_polyphase per (D, taps) group;
+// scheduler over four HIP streams (one hardware queue each, GPU_MAX_HW_QUEUES = 4):
+//   A (main):   wf_fft_power + wf_finalize per FftChain; DDC per (D, taps) group;
 //               post_parallel for all client chains
-//   B (serial): post_serial (deemphasis / DC block, AGC, Convert, ADPCM), then D2H of audio,
-//               s-meter and debug taps
-//   C (rows):   wf_adpcm_rows, then D2H of waterfall rows
-// Block k's B and C work runs concurrently with block k+1's A work; staging buffers are
-// double-buffered by block parity and drained into host rings that the pycsdr binding reads.
+//   B (serial): post_serial_front (deemphasis / DC block, AGC, Convert)
+//   C (serial): chain_adpcm (AdpcmEncoder), back to back: the longest serial stage
+//   R (rows):   wf_adpcm_rows + D2H of waterfall rows; D2H of audio, s-meter, debug taps
+// B, C and R have a few dedicated CUs each (OWRX_SERIAL_CUS), so block k's serial work runs
+// beside the next blocks' stream-A work; kSlots blocks are in flight and their outputs are
+// drained, in order, into the host rings that the pycsdr binding reads.
 #include <stdarg.h>
 #include <stdlib.h>
 #include <stdio.h>
@@ -52,7 +53,8 @@ hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_e
                       const float* taps_poly, const DdcChain* chains, int nchains, int D,
                       int64_t k_begin, int nk, int nseg, float2* partial, hipStream_t st);
 int ddc_padded_p(int p);
-int ddc_segments(int D, int nseg);
+int ddc_segments(int D, int nseg, int P, int nchains);
+int ddc_blocks_per_cu(int P, int nchains);
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
                                 hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
@@ -64,7 +66,7 @@ constexpr int kWfFramesPerGroup = 1;
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
 constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
-constexpr int kRowSlots = 2;  // waterfall row blocks in flight (encoded in order on stream R)
+constexpr int kRowSlots = 4;  // waterfall row blocks in flight (encoded in order on stream R)
 
 #define HIPCHK(expr)                                                                    \
     do {                                                                                \
@@ -230,7 +232,8 @@ struct Slot {  // one block's outputs in flight on streams B / C
     uint8_t* h_dbg = nullptr;
     hipEvent_t evA = nullptr;   // stream A finished this block's post_parallel
     hipEvent_t evF = nullptr;   // stream B finished this block's post_serial_front
-    hipEvent_t evB = nullptr;   // stream C finished (audio copied to host)
+    hipEvent_t evC = nullptr;   // stream C finished this block's encoder
+    hipEvent_t evB = nullptr;   // stream R finished (audio copied to host)
     // timing brackets: A: [a0 waterfall + descriptors a1 DDC kernels a2 .. a3];
     // B/C: [b0 post_parallel, post_serial_front .. chain_adpcm b1]
     hipEvent_t a0 = nullptr, a1 = nullptr, a2 = nullptr, a3 = nullptr;
@@ -258,6 +261,7 @@ struct owrx_engine {
     hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sR = nullptr;
     double samp_rate = 0;
     int64_t max_block = 0;
+    int cus_a = 0;  // CUs of stream A (DDC launch shape)
     int64_t history = kDefaultHistory;
     int64_t pos = 0;  // absolute samples processed
     int64_t block_index = 0;
@@ -540,7 +544,8 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         HIPCHK(halloc(&g->h_chains[1], (size_t)g->chains_cap));
     }
     const int64_t nk_max = e->max_block / g->D + 4;
-    // segments: enough waves to fill 256 CUs x 4 SIMDs x ~4 waves
+    // Launch shape: each tile group's D phases are split into nseg segments, one 4-wave
+    // workgroup each (kernels_ddc.hip); stream A's CUs hold ddc_blocks_per_cu of them.
     const int R = 32;
     int cpw = 1;
     while (cpw < n && cpw < 64) cpw <<= 1;
@@ -548,10 +553,17 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     const int64_t ntg = ((nk_max + R - 1) / R + tpw - 1) / tpw;
     const int64_t ncg = (n + cpw - 1) / cpw;
     const int64_t base = std::max<int64_t>(1, ntg * ncg);
-    // each segment is one 4-wave workgroup per tile group (phases split across its waves)
-    int nseg = (int)std::min<int64_t>(std::max<int64_t>(1, (1024 + base - 1) / base),
+    const int64_t slots = (int64_t)ddc_blocks_per_cu(g->P, n) * std::max(1, e->cus_a);
+    // ~4 workgroups per resident slot: measured flat from 12 to 24 segments at C2 (a
+    // rounds-quantisation model did not predict the timings; fewer segments starve the CUs,
+    // more cost post_parallel extra partials)
+    int nseg = (int)std::min<int64_t>(std::max<int64_t>(1, (2 * slots + base - 1) / base),
                                       std::max(1, g->D / 32));
-    nseg = ddc_segments(g->D, nseg);
+    nseg = ddc_segments(g->D, nseg, g->P, n);
+    if (const char* v = getenv("OWRX_DDC_NSEG")) nseg = ddc_segments(g->D, std::max(1, atoi(v)), g->P, n);
+    if (getenv("OWRX_VERBOSE"))
+        fprintf(stderr, "owrx: DDC group D=%d P=%d chains=%d: %lld tile groups x %d segments, "
+                "%lld resident workgroups\n", g->D, g->P, n, (long long)base, nseg, (long long)slots);
     const size_t need = (size_t)nseg * std::max(1, n) * nk_max;
     if (need > g->partial_elems) {
         RCCHK(drain_all(e));
@@ -851,17 +863,21 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         HIPCHK(hipStreamWaitEvent(e->sC, S.evF, 0));
         HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + off[1], nsel[1], e->sC));
         if (timed) HIPCHK(hipEventRecord(S.b1, e->sC));
+        // the copies to host go on stream R (behind this block's encoder), so stream C runs
+        // encoders back to back: its kernel is the pipeline's longest serial stage
+        HIPCHK(hipEventRecord(S.evC, e->sC));
+        HIPCHK(hipStreamWaitEvent(e->sR, S.evC, 0));
         HIPCHK(hipMemcpyAsync(S.h_counts, S.d_counts, sizeof(ChainCounts) * np,
-                              hipMemcpyDeviceToHost, e->sC));
+                              hipMemcpyDeviceToHost, e->sR));
         HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, (size_t)np * e->out_stride,
-                              hipMemcpyDeviceToHost, e->sC));
+                              hipMemcpyDeviceToHost, e->sR));
         HIPCHK(hipMemcpyAsync(S.h_sm, S.d_sm, sizeof(float) * np * e->sm_stride,
-                              hipMemcpyDeviceToHost, e->sC));
+                              hipMemcpyDeviceToHost, e->sR));
         S.debug = e->debug && S.d_dbg;
         if (S.debug)
             HIPCHK(hipMemcpyAsync(S.h_dbg, S.d_dbg, (size_t)np * kDebugStages * e->dbg_stride,
-                                  hipMemcpyDeviceToHost, e->sC));
-        HIPCHK(hipEventRecord(S.evB, e->sC));
+                                  hipMemcpyDeviceToHost, e->sR));
+        HIPCHK(hipEventRecord(S.evB, e->sR));
         S.chains_pending = true;
     }
     if (timed) {
@@ -930,6 +946,7 @@ static hipError_t create_streams(owrx_engine* e) {
     if (const char* v = getenv("OWRX_SERIAL_CUS")) {
         if (sscanf(v, "%d,%d,%d", &nb, &nc, &nr) != 3) nb = nc = nr = 0;
     }
+    e->cus_a = ncu;
     if (nb <= 0 || nc <= 0 || nr <= 0 || nb + nc + nr > ncu / 2) {
         for (hipStream_t* st : {&e->sA, &e->sB, &e->sC, &e->sR}) {
             err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
@@ -944,6 +961,7 @@ static hipError_t create_streams(owrx_engine* e) {
         return m;
     };
     const int a_end = ncu - nb - nc - nr;
+    e->cus_a = a_end;
     const std::vector<uint32_t> mA = mask_range(0, a_end);
     const std::vector<uint32_t> mB = mask_range(a_end, a_end + nb);
     const std::vector<uint32_t> mC = mask_range(a_end + nb, a_end + nb + nc);
@@ -989,6 +1007,7 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
         if (hipEventCreateWithFlags(&s.evA, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.evF, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.evB, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.evC, hipEventDisableTiming) != hipSuccess ||
             hipEventCreate(&s.a0) != hipSuccess || hipEventCreate(&s.a1) != hipSuccess ||
             hipEventCreate(&s.a2) != hipSuccess || hipEventCreate(&s.a3) != hipSuccess ||
             hipEventCreate(&s.b0) != hipSuccess || hipEventCreate(&s.b1) != hipSuccess)
@@ -1024,7 +1043,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     if (e->evIn) hipEventDestroy(e->evIn);
     for (auto& s : e->slots) {
         free_slot_staging(s);
-        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1})
+        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1})
             if (ev) hipEventDestroy(ev);
     }
     for (auto& r : e->rslots) {

@@ -1,6 +1,6 @@
 // DDC kernel variant microbenchmark (diagnostic; not part of the product).  Builds the real
 // kernel template from kernels_ddc.hip and times tuning variants on a C2-sized block.
-#include "../../openwebrx_amd/csrc/kernels_ddc.hip"
+#include "../../openwebrx_amd/csrc/ddc_kernels.h"
 
 #include <cmath>
 #include <cstdio>
@@ -16,6 +16,7 @@ struct Variant {
     const char* name;
     LaunchFn fn;
     int R;
+    bool lds;
 };
 
 int main(int argc, char** argv) {
@@ -54,24 +55,12 @@ int main(int argc, char** argv) {
     hipMalloc(&d_part, sizeof(float2) * part_elems);
 
     Variant vs[] = {
-        {"R24 W1 flat SB12", launch_ddc_p<27, 24, 1, 12>, 24},
-        {"R24 W1 flat SB16", launch_ddc_p<27, 24, 1, 16>, 24},
-        {"R24 W1 flat SB24", launch_ddc_p<27, 24, 1, 24>, 24},
-        {"R24 W2 flat SB12", launch_ddc_p<27, 24, 2, 12>, 24},
-        {"R24 W2 flat SB16", launch_ddc_p<27, 24, 2, 16>, 24},
-        {"R24 W2 flat SB24", launch_ddc_p<27, 24, 2, 24>, 24},
-        {"R28 W1 flat SB12", launch_ddc_p<27, 28, 1, 12>, 28},
-        {"R28 W1 flat SB16", launch_ddc_p<27, 28, 1, 16>, 28},
-        {"R28 W1 flat SB24", launch_ddc_p<27, 28, 1, 24>, 28},
-        {"R28 W2 flat SB12", launch_ddc_p<27, 28, 2, 12>, 28},
-        {"R28 W2 flat SB16", launch_ddc_p<27, 28, 2, 16>, 28},
-        {"R28 W2 flat SB24", launch_ddc_p<27, 28, 2, 24>, 28},
-        {"R32 W1 flat SB12", launch_ddc_p<27, 32, 1, 12>, 32},
-        {"R32 W1 flat SB16", launch_ddc_p<27, 32, 1, 16>, 32},
-        {"R32 W1 flat SB24", launch_ddc_p<27, 32, 1, 24>, 32},
-        {"R32 W2 flat SB12", launch_ddc_p<27, 32, 2, 12>, 32},
-        {"R32 W2 flat SB16", launch_ddc_p<27, 32, 2, 16>, 32},
-        {"R32 W2 flat SB24", launch_ddc_p<27, 32, 2, 24>, 32},
+        {"flat R32 W2 SB16", launch_ddc_p<27, 32, 2, 16>, 32, false},
+        {"lds R32 W2", launch_ddc_lds_p<27, 2>, 32, true},
+        {"lds R32 W3", launch_ddc_lds_p<27, 3>, 32, true},
+        {"lds R48 W2", launch_ddc_lds_p<27, 2, 48>, 48, true},
+        {"lds R40 W3", launch_ddc_lds_p<27, 3, 40>, 40, true},
+        {"lds R64 W2", launch_ddc_lds_p<27, 2, 64>, 64, true},
     };
     std::vector<float2> ref, out;
     hipEvent_t e0, e1;
@@ -85,7 +74,14 @@ int main(int argc, char** argv) {
         const int ncg = (C + cpw - 1) / cpw;
         const int base = ntg * ncg;
         int nseg = std::min(std::max(1, (1024 + base - 1) / base), std::max(1, D / 32));
-        nseg = ddc_segments(D, nseg);
+        if (argc > 2) nseg = atoi(argv[2]);
+        if (v.lds) {  // segments actually launched for the request
+            const int len = ddc_seg_len(D, nseg);
+            nseg = (D + len - 1) / len;
+        } else {
+            const int pps = (D + kDdcWaves * nseg - 1) / (kDdcWaves * nseg);
+            nseg = ((D + pps - 1) / pps + kDdcWaves - 1) / kDdcWaves;
+        }
         hipMemset(d_part, 0, sizeof(float2) * part_elems);
         v.fn(d_in + hist, blk_start, blk_end, d_taps, d_ch, C, D, k_begin, nk, nseg, d_part, 0);
         hipDeviceSynchronize();
@@ -100,6 +96,19 @@ int main(int argc, char** argv) {
             }
         double err = 0, nrm = 0;
         if (ref.empty()) ref = out;
+        {   // where do the variants differ (diagnostic)
+            double worst = 0;
+            size_t wi = 0;
+            long nbad = 0;
+            for (size_t i = 0; i < out.size(); ++i) {
+                const double d = hypot(out[i].x - ref[i].x, out[i].y - ref[i].y);
+                const double m = hypot(ref[i].x, ref[i].y) + 1e-6;
+                if (d > 1e-4 * m) nbad++;
+                if (d > worst) { worst = d; wi = i; }
+            }
+            printf("   worst |diff| %.3e at chain %zu k %zu of %d (ref %.3e), %ld outputs off\n", worst,
+                   wi / nk, wi % nk, nk, hypot(ref[wi].x, ref[wi].y), nbad);
+        }
         for (size_t i = 0; i < out.size(); ++i) {
             err += pow(out[i].x - ref[i].x, 2) + pow(out[i].y - ref[i].y, 2);
             nrm += pow(ref[i].x, 2) + pow(ref[i].y, 2);
