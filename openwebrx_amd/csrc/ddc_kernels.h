@@ -366,4 +366,29 @@ hipError_t launch_ddc_p(const float2* blk, int64_t blk_start, int64_t blk_end,
     return hipGetLastError();
 }
 
+// Resident workgroups per CU of one instantiation (registers / LDS bound).
+template <int P>
+int ddc_occ(bool flat, int tpw) {
+    int nb = 0;
+    hipError_t e = flat
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &nb, reinterpret_cast<const void*>(&ddc_polyphase<P, 32, 2, 16>), 64 * kDdcWaves, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &nb, reinterpret_cast<const void*>(&ddc_lds<P, kLdsR, 2>), 64 * kDdcWaves,
+              ddc_lds_bytes(P, tpw));
+    if (e != hipSuccess) return 2;
+    return nb > 0 ? nb : 1;
+}
+
+// Explicit instantiation, one translation unit per group of depths (kernels_ddc_p*.hip) so
+// the fully unrolled kernels compile in parallel; kernels_ddc.hip only dispatches.
+#define OWRX_DDC_SIG                                                                         \
+    (const float2*, int64_t, int64_t, const float*, const DdcChain*, int, int, int64_t, int, \
+     int, float2*, hipStream_t)
+#define OWRX_DDC_INSTANTIATE(EXT, P)                                                         \
+    EXT template hipError_t launch_ddc_p<P, 32, 2, 16> OWRX_DDC_SIG;                         \
+    EXT template hipError_t launch_ddc_lds_p<P, 2, kLdsR> OWRX_DDC_SIG;                      \
+    EXT template int ddc_occ<P>(bool, int);
+#define OWRX_DDC_DEPTHS(X, EXT) X(EXT, 8) X(EXT, 16) X(EXT, 27) X(EXT, 28) X(EXT, 32) X(EXT, 48) X(EXT, 64)
+
 }  // namespace owrx

@@ -49,40 +49,28 @@ static bool ddc_uses_flat(int P, int nchains) {
     return (P == 27 && ddc_flat()) || ddc_tiles_per_wave(nchains) > 4;
 }
 
-// Resident workgroups per CU of the production instantiation (registers / LDS bound), for
-// the launch-shape choice in engine.hip.
-template <int P>
-static int ddc_occupancy_p(int nchains) {
-    int nb = 0;
-    hipError_t e = ddc_uses_flat(P, nchains)
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &nb, reinterpret_cast<const void*>(&ddc_polyphase<P, 32, 2, 16>), 64 * kDdcWaves, 0)
-        : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &nb, reinterpret_cast<const void*>(&ddc_lds<P, kLdsR, 2>), 64 * kDdcWaves,
-              ddc_lds_bytes(P, ddc_tiles_per_wave(nchains)));
-    if (e != hipSuccess) return 2;
-    return nb > 0 ? nb : 1;
-}
+OWRX_DDC_DEPTHS(OWRX_DDC_INSTANTIATE, extern)
 
+// Resident workgroups per CU of the kernel a group of nchains runs (launch-shape choice in
+// engine.hip).
 int ddc_blocks_per_cu(int P, int nchains) {
+    const bool flat = ddc_uses_flat(P, nchains);
+    const int tpw = ddc_tiles_per_wave(nchains);
     switch (P) {
-        case 8: return ddc_occupancy_p<8>(nchains);
-        case 16: return ddc_occupancy_p<16>(nchains);
-        case 27: return ddc_occupancy_p<27>(nchains);
-        case 28: return ddc_occupancy_p<28>(nchains);
-        case 30: return ddc_occupancy_p<30>(nchains);
-        case 32: return ddc_occupancy_p<32>(nchains);
-        case 36: return ddc_occupancy_p<36>(nchains);
-        case 40: return ddc_occupancy_p<40>(nchains);
-        case 48: return ddc_occupancy_p<48>(nchains);
-        case 64: return ddc_occupancy_p<64>(nchains);
+        case 8: return ddc_occ<8>(flat, tpw);
+        case 16: return ddc_occ<16>(flat, tpw);
+        case 27: return ddc_occ<27>(flat, tpw);
+        case 28: return ddc_occ<28>(flat, tpw);
+        case 32: return ddc_occ<32>(flat, tpw);
+        case 48: return ddc_occ<48>(flat, tpw);
+        case 64: return ddc_occ<64>(flat, tpw);
         default: return 2;
     }
 }
 
 // Supported polyphase depths; taps are zero padded up to the instantiated P.
 int ddc_padded_p(int p) {
-    static const int ps[] = {8, 16, 27, 28, 30, 32, 36, 40, 48, 64};
+    static const int ps[] = {8, 16, 27, 28, 32, 48, 64};
     for (int v : ps)
         if (p <= v) return v;
     return -1;
@@ -119,10 +107,7 @@ hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_e
         OWRX_DDC_CASE(16)
         OWRX_DDC_CASE(27)
         OWRX_DDC_CASE(28)
-        OWRX_DDC_CASE(30)
         OWRX_DDC_CASE(32)
-        OWRX_DDC_CASE(36)
-        OWRX_DDC_CASE(40)
         OWRX_DDC_CASE(48)
         OWRX_DDC_CASE(64)
         default:
