@@ -81,6 +81,21 @@ def cpu_baseline(fs, n_fft, hop, avg, plist, seconds_target=15.0):
                       % (n, n / fs, len(plist), threads, dt)}
 
 
+def pmc_traffic(prefix):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc passes
+    of this same bench command); (None, reason) when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, "no PMC summary committed"
+    d = json.load(open(files[-1]))
+    for k, v in d["kernels"].items():
+        if k.startswith(prefix):
+            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, "kernel absent from " + os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,6 +239,7 @@ def main():
     post_ms = s1["gpu_ms_post"] - s0["gpu_ms_post"]
     wf_launches = s1["waterfall_launches"] - s0["waterfall_launches"]
 
+    traffic, traffic_src = pmc_traffic("ddc_lds<")
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -255,14 +271,17 @@ def main():
             "chains_total": C * world,
             "roofline": {
                 "bound": "valu",
-                "kernel": "ddc_polyphase (fused Shift + FirDecimate, all chains)",
+                "kernel": "ddc_lds (fused Shift + FirDecimate, all chains of the group)",
                 "achieved": round(achieved_tf, 3),
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
-                "traffic": None,
-                "note": "algorithmic flops per launch = chains*outputs*(4*taps+6*D); HIP events "
-                        "on the engine stream; FP32-VALU peak (no MFMA by design)",
+                "traffic": traffic,
+                "note": "algorithmic flops per launch = chains*outputs*(4*taps+6*D); average launch "
+                        "time from HIP events on the engine stream; FP32 vector peak (the DDC is a "
+                        "1-D stencil on VALU, SURVEY.md 8d; no MFMA by design). traffic = HBM "
+                        "bytes per launch from separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
+                        "and WRITE_SIZE passes, " + traffic_src,
             },
             "kernels_ms_per_step": {
                 "ddc": round(ddc_ms / args.steps, 3),

@@ -171,6 +171,7 @@ ddc_polyphase(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end
 // to ddc_polyphase's fma(x.im, j*rot, x.re * rot) order.
 constexpr int kPhW = 4;                       // phases per wave per chunk
 constexpr int kChunk = kPhW * kDdcWaves;      // phases per chunk (LDS row length)
+constexpr int kLdsMaxTiles = 2;               // tiles per wave the staging registers cover
 
 // (re, im) * (re, im): two packed instructions
 OWRX_DEV f2v cmul_pk(f2v x, f2v r) {
@@ -211,7 +212,8 @@ ddc_lds(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end,
 
     // staging: element e -> (row q = e / kChunk, column c = e % kChunk); per thread at most
     // kFill elements per chunk, held in registers while the previous chunk is computed
-    constexpr int kFill = ((2 * R + P - 1) * kChunk + 64 * kDdcWaves - 1) / (64 * kDdcWaves);
+    constexpr int kFill =
+        ((kLdsMaxTiles * R + P - 1) * kChunk + 64 * kDdcWaves - 1) / (64 * kDdcWaves);
     const int nel = Q * kChunk;
     float2 st[kFill];
     auto fetch = [&](int c) {

@@ -46,7 +46,7 @@ static int ddc_tiles_per_wave(int nchains) {
 }
 
 static bool ddc_uses_flat(int P, int nchains) {
-    return (P == 27 && ddc_flat()) || ddc_tiles_per_wave(nchains) > 4;
+    return (P == 27 && ddc_flat()) || ddc_tiles_per_wave(nchains) > kLdsMaxTiles;
 }
 
 OWRX_DDC_DEPTHS(OWRX_DDC_INSTANTIATE, extern)
@@ -91,9 +91,9 @@ int ddc_segments(int D, int nseg, int P, int nchains) {
 hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_end,
                       const float* taps_poly, const DdcChain* chains, int nchains, int D,
                       int64_t k_begin, int nk, int nseg, float2* partial, hipStream_t st) {
-    // ddc_lds stages (tiles per wave x R + P - 1) sample rows: with fewer than 16 chains a wave
-    // holds more than 4 tiles and the window outgrows LDS, so small groups (where the DDC is
-    // cheap anyway) run the register-direct kernel
+    // ddc_lds stages (tiles per wave x R + P - 1) sample rows and is built for at most
+    // kLdsMaxTiles tiles per wave (32+ chains); smaller groups, where the DDC is cheap anyway,
+    // run the register-direct kernel
     const bool flat = ddc_uses_flat(P, nchains);
 #define OWRX_DDC_CASE(v)                                                                    \
     case v:                                                                                 \

@@ -229,6 +229,31 @@ def test_modes_2400k_grouped(amd, mode):
     eng.close()
 
 
+@pytest.mark.parametrize("nch", [32, 40, 65])
+def test_ddc_large_groups(amd, nch):
+    """Groups of 32+ chains run the LDS-staged DDC kernel (two tiles per wave at 32 chains, one
+    at 33-64, two chain groups per launch at 65): DDC stage of sampled chains vs the oracle,
+    and their int16 audio within +-1 LSB."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    modes = [("nfm", "am", "usb", "cw")[c % 4] for c in range(nch)]
+    n = 1 << 19
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16)
+             for o, m in zip(offs, modes)]
+    eng, chains = _run_chains(amd, iq, fs, plist, 1 << 17)
+    for c in sorted({0, nch // 2, nch - 1}):
+        ref = oracle.stages(iq, plist[c])
+        ddc = chains[c].read_debug(0)
+        assert ddc.size == ref["ddc"].size, (c, ddc.size, ref["ddc"].size)
+        assert rel_rms(ddc, ref["ddc"]) < 1e-5, c
+        s16 = np.frombuffer(chains[c].read_audio(), np.int16)
+        assert s16.size == ref["s16"].size
+        d = np.abs(s16.astype(np.int32) - ref["s16"])
+        assert np.mean(d <= 1) > 0.999, (c, np.mean(d <= 1))
+    eng.close()
+
+
 def test_adpcm_chain_output_decodes(amd):
     """AdpcmEncoder(sync=True) stream: SYNC frames every 1001 data bytes, decodable."""
     from openwebrx_amd import synth

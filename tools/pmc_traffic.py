@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the engine kernels from two rocprofv3 --pmc passes
+(tools/gpu_round.sh ... pmc): FETCH_SIZE and WRITE_SIZE (KB per dispatch), averaged over
+dispatches.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half of
+the bytes of wide coalesced streaming reads, so fetched bytes = 2 x FETCH_SIZE; WRITE_SIZE is
+taken as is.  Writes profiles/<tag>_pmc_traffic.json, which bench.py reports as
+roofline.traffic for the dominant kernel.
+
+usage: tools/pmc_traffic.py TAG FETCH_DIR WRITE_DIR"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+tag, fdir, wdir = sys.argv[1:4]
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for d in (fdir, wdir):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            if "owrx::" not in name:
+                continue
+            short = name.split("(")[0].replace("void ", "").replace("owrx::", "")
+            vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
+                 "'python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-timing'",
+       "correction": "fetch_bytes = 2 x FETCH_SIZE (gfx950), write_bytes = WRITE_SIZE",
+       "kernels": {}}
+for k, cs in sorted(vals.items()):
+    f = sum(cs["FETCH_SIZE"]) / max(1, len(cs["FETCH_SIZE"]))
+    w = sum(cs["WRITE_SIZE"]) / max(1, len(cs["WRITE_SIZE"]))
+    out["kernels"][k] = {"fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1),
+                         "hbm_bytes_per_launch": int(round((2 * f + w) * 1024))}
+path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                    "%s_pmc_traffic.json" % tag)
+json.dump(out, open(path, "w"), indent=1)
+print(path)
+for k, v in out["kernels"].items():
+    print("%-28s %s" % (k, v))
