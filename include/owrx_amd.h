@@ -64,6 +64,11 @@ int64_t owrx_engine_max_block(owrx_engine* e);
 /* Host cf32 (interleaved little-endian float I,Q) -> device; processes whole blocks.
  * Equivalent of Writer.write() on the wideband Buffer. */
 int owrx_push_iq(owrx_engine* e, const float* iq_cf32, int64_t nsamples);
+/* Host cs16 (interleaved little-endian int16 I,Q) -> cf32 on the GPU, as the reference's
+ * ingest conversion Chain([Convert(COMPLEX_SHORT, COMPLEX_FLOAT), Gain(COMPLEX_FLOAT, gain)])
+ * (owrx/source/direct.py:51-71 getBuffer, fifi_sdr.py:27-28): x / 32767 * gain.  Half the
+ * PCIe bytes of owrx_push_iq; the conversion kernel writes straight into the engine window. */
+int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq_cs16, int64_t nsamples, float gain);
 /* Device-resident cf32 block; iq_dev[-history, 0) must hold the previous samples of the stream
  * (e.g. a contiguous HBM recording, or an RCCL-broadcast window).  Zero-copy and asynchronous:
  * the block (with its history) must stay unmodified until the next owrx_process_device /
@@ -170,6 +175,8 @@ int owrx_set_timing(owrx_engine* e, int enable);
 #define OWRX_MOD_ADPCM 9          /* p0 = sync (0/1); input s16 */
 #define OWRX_MOD_FFTSWAP 10       /* p0 = fft size; input f32 rows */
 #define OWRX_MOD_FFTADPCM 11      /* p0 = fft size; input f32 rows (already swapped) */
+#define OWRX_MOD_CONVERT_CS16_CF32 12  /* Convert(COMPLEX_SHORT, COMPLEX_FLOAT); n = samples */
+#define OWRX_MOD_GAIN 13          /* Gain(format, p0); p1 = 1 complex (n samples), 0 float */
 typedef struct owrx_module owrx_module;
 int owrx_module_create(int device, int type, double p0, double p1, double p2,
                        owrx_module** out);

@@ -34,6 +34,8 @@ MOD_CONVERT_F_S16 = 8
 MOD_ADPCM = 9
 MOD_FFTSWAP = 10
 MOD_FFTADPCM = 11
+MOD_CONVERT_CS16_CF32 = 12
+MOD_GAIN = 13
 
 
 class ChainParams(ctypes.Structure):
@@ -96,6 +98,7 @@ PROTOTYPES = {
     "owrx_engine_history": (_i64, [_vp]),
     "owrx_engine_max_block": (_i64, [_vp]),
     "owrx_push_iq": (_i32, [_vp, _vp, _i64]),
+    "owrx_push_iq_cs16": (_i32, [_vp, _vp, _i64, _f32]),
     "owrx_process_device": (_i32, [_vp, _vp, _i64]),
     "owrx_ingest_buffer": (_i32, [_vp, ctypes.POINTER(_vp), _pi64]),
     "owrx_commit": (_i32, [_vp, _i64]),

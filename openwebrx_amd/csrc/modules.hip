@@ -128,6 +128,8 @@ __global__ void mod_parallel(ModParams p, const void* __restrict__ in, int64_t n
             case OWRX_MOD_REALPART: of[k] = ic[k].x; break;
             case OWRX_MOD_LIMIT: of[k] = limit_step(iff[k], p.f0); break;
             case OWRX_MOD_CONVERT_F_S16: os[k] = convert_s16(iff[k]); break;
+            case OWRX_MOD_CONVERT_CS16_CF32: of[k] = s16_to_f32(((const int16_t*)in)[k]); break;
+            case OWRX_MOD_GAIN: of[k] = gain_step(iff[k], p.f0); break;
             case OWRX_MOD_FFTSWAP: {
                 const int N = p.fft_size;
                 const int64_t r = k / N, i = k % N;
@@ -161,13 +163,14 @@ static int in_item_bytes(int type) {
         case OWRX_MOD_AMDEMOD:
         case OWRX_MOD_REALPART: return 8;
         case OWRX_MOD_ADPCM: return 2;
+        case OWRX_MOD_CONVERT_CS16_CF32: return 4;
         default: return 4;
     }
 }
 
 extern "C" int owrx_module_create(int device, int type, double p0, double p1, double p2,
                                   owrx_module** out) {
-    if (!out || type < OWRX_MOD_FMDEMOD || type > OWRX_MOD_FFTADPCM) {
+    if (!out || type < OWRX_MOD_FMDEMOD || type > OWRX_MOD_GAIN) {
         set_last_error("owrx_module_create: bad type %d", type);
         return OWRX_EINVAL;
     }
@@ -194,6 +197,10 @@ extern "C" int owrx_module_create(int device, int type, double p0, double p1, do
             s.agc.env = m->p.agc.reference / m->p.agc.initial_gain;
             break;
         case OWRX_MOD_ADPCM: m->p.i0 = (int)p0; break;
+        case OWRX_MOD_GAIN:
+            m->p.f0 = (float)p0;
+            m->p.i0 = p1 > 0 ? 1 : 0;  // complex: n samples = 2n floats
+            break;
         case OWRX_MOD_FFTSWAP:
         case OWRX_MOD_FFTADPCM:
             m->p.fft_size = (int)p0;
@@ -235,7 +242,7 @@ extern "C" int64_t owrx_module_process(owrx_module* m, const void* in, int64_t n
     std::lock_guard<std::mutex> lk(m->mu);
     if (n == 0) return 0;
     hipSetDevice(m->device);
-    const int64_t in_bytes = n * in_item_bytes(m->p.type);
+    const int64_t in_bytes = n * in_item_bytes(m->p.type) * (m->p.type == OWRX_MOD_GAIN && m->p.i0 ? 2 : 1);
     if (in_bytes > m->in_cap) {
         if (m->d_in) hipFree(m->d_in);
         m->d_in = nullptr;
@@ -252,9 +259,11 @@ extern "C" int64_t owrx_module_process(owrx_module* m, const void* in, int64_t n
     int64_t produced = 0;
     const int t = m->p.type;
     const bool parallel = t == OWRX_MOD_AMDEMOD || t == OWRX_MOD_REALPART || t == OWRX_MOD_LIMIT ||
-                          t == OWRX_MOD_CONVERT_F_S16 || t == OWRX_MOD_FFTSWAP;
+                          t == OWRX_MOD_CONVERT_F_S16 || t == OWRX_MOD_FFTSWAP ||
+                          t == OWRX_MOD_CONVERT_CS16_CF32 || t == OWRX_MOD_GAIN;
     if (parallel) {
-        int64_t items = n;
+        int64_t items = n;  // scalar items of the elementwise kernel
+        if (t == OWRX_MOD_CONVERT_CS16_CF32 || (t == OWRX_MOD_GAIN && m->p.i0)) items = 2 * n;
         const int64_t item_out = (t == OWRX_MOD_CONVERT_F_S16) ? 2 : 4;
         if (t == OWRX_MOD_FFTSWAP) items = (n / m->p.fft_size) * m->p.fft_size;
         if (items * item_out > out_cap_bytes) return OWRX_EINVAL;

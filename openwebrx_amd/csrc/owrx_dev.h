@@ -156,6 +156,18 @@ OWRX_DEV int16_t convert_s16(float x) {
     return f_to_s16(v);
 }
 
+// Convert(COMPLEX_SHORT, COMPLEX_FLOAT) then Gain(COMPLEX_FLOAT, g) per component
+// (owrx/source/direct.py:51-71): x / 32767 (csdr's short -> float scale, the inverse of
+// convert_s16), then * g, two roundings as the two modules apply them.
+OWRX_DEV float s16_to_f32(int16_t x) {
+#pragma clang fp contract(off)
+    return (float)x / 32767.0f;
+}
+OWRX_DEV float gain_step(float x, float g) {
+#pragma clang fp contract(off)
+    return x * g;
+}
+
 // FftAdpcm quantiser: (short)(dB*100) (csdr/chain/fft.py:43-45, htdocs/openwebrx.js:1118-1126)
 OWRX_DEV int16_t db_to_s16(float db) {
 #pragma clang fp contract(off)

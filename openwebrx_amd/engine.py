@@ -73,6 +73,15 @@ class Engine:
             raise ValueError("IQ must be complex64 / interleaved float32")
         check(lib.owrx_push_iq(self._h, a.ctypes.data, n), "owrx_push_iq")
 
+    def push_cs16(self, iq, gain=1.0):
+        """Host cs16 samples (interleaved int16 I,Q) through the ingest conversion
+        Convert(COMPLEX_SHORT, COMPLEX_FLOAT) + Gain(COMPLEX_FLOAT, gain) on the GPU."""
+        a = np.ascontiguousarray(iq)
+        if a.dtype != np.int16 or a.size % 2:
+            raise ValueError("cs16 IQ must be an even-length int16 array")
+        check(lib.owrx_push_iq_cs16(self._h, a.ctypes.data, a.size // 2, float(gain)),
+              "owrx_push_iq_cs16")
+
     def process_device(self, ptr, n):
         check(lib.owrx_process_device(self._h, ctypes.c_void_p(ptr), int(n)), "owrx_process_device")
 

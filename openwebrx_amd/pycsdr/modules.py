@@ -535,16 +535,42 @@ class Agc(_Unary):
 
 
 class Convert(_Unary):
+    """Convert(FLOAT, SHORT) (csdr/chain/clientaudio.py:18) and Convert(COMPLEX_SHORT,
+    COMPLEX_FLOAT), the SDR ingest conversion (owrx/source/direct.py:51-71)."""
     _mod = "MOD_CONVERT_F_S16"
     _out_size = 2
 
     def __init__(self, inFormat, outFormat):
         super().__init__()
-        if (inFormat, outFormat) != (Format.FLOAT, Format.SHORT):
+        if (inFormat, outFormat) == (Format.COMPLEX_SHORT, Format.COMPLEX_FLOAT):
+            self._mod = "MOD_CONVERT_CS16_CF32"
+            self._in_dtype = np.int32      # one (I, Q) int16 pair per item
+            self._out_size = 8
+        elif (inFormat, outFormat) != (Format.FLOAT, Format.SHORT):
             raise NotImplementedError("Convert(%s, %s) is not on the GPU path yet"
                                       % (inFormat, outFormat))
         self.input_format = inFormat
         self.output_format = outFormat
+
+
+class Gain(_Unary):
+    """Gain(format, gain): FLOAT (csdr/chain/analog.py:29) or COMPLEX_FLOAT (the ingest
+    conversion, owrx/source/direct.py:51-71, fifi_sdr.py:27-28)."""
+    _mod = "MOD_GAIN"
+
+    def __init__(self, format, gain):
+        super().__init__()
+        if format == Format.FLOAT:
+            self._in_dtype, self._out_size, self._complex = np.float32, 4, 0.0
+        elif format == Format.COMPLEX_FLOAT:
+            self._in_dtype, self._out_size, self._complex = np.complex64, 8, 1.0
+        else:
+            raise NotImplementedError("Gain(%s) is not on the GPU path yet" % (format,))
+        self.input_format = self.output_format = format
+        self.gain = float(gain)
+
+    def _params(self):
+        return (self.gain, self._complex)
 
 
 class AdpcmEncoder(_Unary):
@@ -620,7 +646,7 @@ def _unsupported(name):
 
 for _name in ("Afc", "AudioResampler", "BaudotDecoder", "Ccir476Decoder", "Ccir493Decoder",
               "CwDecoder", "DBPskDecoder", "Downmix", "DscDecoder", "ExecModule", "FaxDecoder",
-              "Gain", "Lowpass", "MFRttyDecoder", "NavtexDecoder", "NoiseFilter", "RttyDecoder",
+              "Lowpass", "MFRttyDecoder", "NavtexDecoder", "NoiseFilter", "RttyDecoder",
               "SitorBDecoder", "SnrSquelch", "SstvDecoder", "Throttle", "TimingRecovery",
               "VaricodeDecoder", "WfmDeemphasis"):
     globals()[_name] = _unsupported(_name)

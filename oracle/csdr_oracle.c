@@ -367,6 +367,17 @@ void orc_convert_f_s16(const float* in, int64_t n, int16_t* out) {
     }
 }
 
+/* Ingest conversion Chain([Convert(COMPLEX_SHORT, COMPLEX_FLOAT), Gain(COMPLEX_FLOAT, g)])
+ * (owrx/source/direct.py:51-71, fifi_sdr.py:27-28).  csdr scales short -> float by 1/SHRT_MAX
+ * (the inverse of convert_f_s16 above; recalled, parity unpinned), then Gain multiplies. */
+void orc_convert_s16_f(const int16_t* in, int64_t n, float* out) {
+    for (int64_t k = 0; k < n; k++) out[k] = (float)in[k] / 32767.0f;
+}
+
+void orc_gain(const float* in, int64_t n, float gain, float* out) {
+    for (int64_t k = 0; k < n; k++) out[k] = in[k] * gain;
+}
+
 /* ---- IMA ADPCM (AdpcmEncoder(sync=True) csdr/chain/clientaudio.py:34, FftAdpcm) ---- */
 static const int adpcm_index_table[16] = {-1, -1, -1, -1, 2, 4, 6, 8,
                                           -1, -1, -1, -1, 2, 4, 6, 8};

@@ -59,6 +59,8 @@ typedef struct {
 void orc_agc_profile(int profile, orc_agc_params* p);
 void orc_agc(const float* in, int64_t n, const orc_agc_params* p, float* out);
 void orc_convert_f_s16(const float* in, int64_t n, int16_t* out);
+void orc_convert_s16_f(const int16_t* in, int64_t n, float* out);   /* n scalars */
+void orc_gain(const float* in, int64_t n, float gain, float* out);
 
 /* IMA-ADPCM.  sync=1: "SYNC" + s16 stepIndex + s16 predictor before data byte 0 and then
  * after every 1001 data bytes (the period htdocs/lib/AudioEngine.js:449-491 decodes). */

@@ -54,6 +54,8 @@ PROTOS = {
     "orc_amdemod": (None, [_P, _L, _P]),
     "orc_realpart": (None, [_P, _L, _P]),
     "orc_limit": (None, [_P, _L, _F, _P]),
+    "orc_convert_s16_f": (None, [_P, _L, _P]),
+    "orc_gain": (None, [_P, _L, _F, _P]),
     "orc_dcblock": (None, [_P, _L, _P]),
     "orc_deemphasis": (None, [_P, _L, _F, _P]),
     "orc_nfm_deemphasis_alpha": (_F, [_I]),
@@ -180,6 +182,22 @@ def realpart(x):
 
 def dcblock(x):
     return _unary("orc_dcblock", x)
+
+
+def convert_s16_f(x):
+    """Convert(COMPLEX_SHORT | SHORT, COMPLEX_FLOAT | FLOAT): int16 scalars -> float32."""
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    y = np.empty(x.size, np.float32)
+    lib().orc_convert_s16_f(x.ctypes.data, x.size, y.ctypes.data)
+    return y
+
+
+def gain(x, g):
+    """Gain(FLOAT | COMPLEX_FLOAT, g) on float32 scalars."""
+    x = _f32(x)
+    y = np.empty_like(x)
+    lib().orc_gain(x.ctypes.data, x.size, g, y.ctypes.data)
+    return y
 
 
 def limit(x, m=1.0):

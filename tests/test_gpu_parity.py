@@ -68,6 +68,50 @@ def test_am_real_limit_convert_bit_exact(amd):
     assert np.array_equal(g, oracle.convert_s16(f))
 
 
+def test_ingest_convert_gain_bit_exact(amd):
+    """Convert(COMPLEX_SHORT, COMPLEX_FLOAT) and Gain(FLOAT | COMPLEX_FLOAT, g) modules."""
+    raw = RNG.integers(-32768, 32768, size=2 * 20001, dtype=np.int64).astype(np.int16)
+    raw[:4] = [-32768, 32767, 0, -1]
+    g = np.frombuffer(run_module(amd, amd._lib.MOD_CONVERT_CS16_CF32, raw.view(np.int32),
+                                 8 * (raw.size // 2)), np.float32)
+    ref = oracle.convert_s16_f(raw)
+    assert np.array_equal(g, ref)
+    x = ref.view(np.complex64)
+    g = np.frombuffer(run_module(amd, amd._lib.MOD_GAIN, x, 8 * x.size, 5.0, 1.0), np.float32)
+    assert np.array_equal(g, oracle.gain(ref, 5.0))
+    f = ref[:30001]
+    g = np.frombuffer(run_module(amd, amd._lib.MOD_GAIN, f, 4 * f.size, 100.0, 0.0), np.float32)
+    assert np.array_equal(g, oracle.gain(f, 100.0))
+
+
+def test_engine_cs16_ingest_equals_float_ingest(amd):
+    """owrx_push_iq_cs16 (conversion fused into the engine window) gives byte-identical
+    waterfall rows and chain audio to pushing the oracle-converted cf32 stream."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    n = 1 << 19
+    iq, offs = synth.make_iq(fs, n, ["nfm", "am"], amp=0.02)
+    raw = np.clip(np.round(np.stack([iq.real, iq.imag], 1).ravel() * 6000), -32768, 32767)
+    raw = raw.astype(np.int16)
+    conv = oracle.gain(oracle.convert_s16_f(raw), 5.0).view(np.complex64)
+    avg, hop = amd.params.fft_parameters(fs, 4096, 9, 0.3)
+    outs = []
+    for mode in ("cs16", "cf32"):
+        eng = amd.Engine(fs, max_block=1 << 17)
+        wf = eng.waterfall(4096, hop, avg, adpcm=True)
+        chs = [eng.chain(amd.params.chain_params(fs, o, m)) for o, m in zip(offs, ["nfm", "am"])]
+        for i in range(0, n, 100000):
+            if mode == "cs16":
+                eng.push_cs16(raw[2 * i:2 * min(n, i + 100000)], 5.0)
+            else:
+                eng.push(conv[i:i + 100000])
+        eng.sync()
+        outs.append([wf.read()] + [c.read_audio() for c in chs])
+        eng.close()
+    assert len(outs[0][0]) > 0 and all(len(a) > 0 for a in outs[0][1:])
+    assert outs[0] == outs[1]
+
+
 def test_dcblock_deemph_bit_exact(amd):
     f = (RNG.standard_normal(25000) * 0.2 + 0.1).astype(np.float32)
     g = np.frombuffer(run_module(amd, amd._lib.MOD_DCBLOCK, f, 4 * f.size), np.float32)

@@ -293,3 +293,15 @@ def test_standalone_modules_match_oracle():
         m.stop()
     data = b"".join(got)
     assert data == want[:len(data)] and len(want) - len(data) <= 1
+
+
+def test_ingest_modules_formats():
+    """The ingest conversion Chain of owrx/source/direct.py:51-71 builds on the shim."""
+    conv = M.Convert(Format.COMPLEX_SHORT, Format.COMPLEX_FLOAT)
+    gain = M.Gain(Format.COMPLEX_FLOAT, 5.0)
+    assert conv.getInputFormat() == Format.COMPLEX_SHORT
+    assert conv.getOutputFormat() == Format.COMPLEX_FLOAT == gain.getInputFormat()
+    with pytest.raises(ValueError):
+        conv.setReader(M.Buffer(Format.COMPLEX_FLOAT).getReader())
+    with pytest.raises(NotImplementedError):
+        M.Convert(Format.COMPLEX_FLOAT, Format.COMPLEX_SHORT)
