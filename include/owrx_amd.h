@@ -40,6 +40,8 @@ extern "C" {
 #define OWRX_OUT_S16 0      /* Convert(FLOAT, SHORT) */
 #define OWRX_OUT_ADPCM 1    /* Convert + AdpcmEncoder(sync=True) */
 #define OWRX_OUT_F32 2      /* raw float audio (no Convert) */
+#define OWRX_OUT_IQ 3       /* Shift + FirDecimate output only, cf32 at in/D: the service
+                               Resampler (owrx/source/resampler.py:11-26) */
 
 #define OWRX_AGC_FAST 0
 #define OWRX_AGC_SLOW 1

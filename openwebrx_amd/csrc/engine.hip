@@ -217,6 +217,7 @@ struct Chain {
 struct Slot {  // one block's outputs in flight on streams B / C
     bool chains_pending = false;
     std::vector<int> post_ids;
+    std::vector<int64_t> out_off;  // per post: byte offset of its output region
     bool debug = false;
     ChainPost* d_posts = nullptr;
     ChainPost* h_posts = nullptr;
@@ -304,7 +305,7 @@ struct owrx_engine {
     int next_handle = 1;
     // post staging (all chains), per block parity
     int post_cap = 0;
-    int64_t out_stride = 0, sm_stride = 0, dbg_stride = 0;
+    int64_t out_total = 0, sm_stride = 0, dbg_stride = 0;  // out: sum of per-chain regions
     Slot slots[kSlots];
     RowSlot rslots[kRowSlots];
     int64_t row_head = 0;  // next row slot to fill
@@ -316,6 +317,8 @@ struct owrx_engine {
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
+
+static int64_t out_region(int64_t cap) { return (cap + 255) & ~(int64_t)255; }
 
 static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
     int64_t nk = e->max_block / D + 4;
@@ -387,9 +390,9 @@ static int drain_slot(owrx_engine* e, int si) {
             if (it == e->chains.end()) continue;
             Chain* c = it->second.get();
             const ChainCounts& cc = s.h_counts[k];
-            const int64_t nb = std::min<int64_t>(cc.out_bytes, e->out_stride);
-            if (cc.out_bytes > e->out_stride) e->stats.overruns++;
-            c->audio.push(s.h_out + (int64_t)k * e->out_stride, (size_t)nb);
+            const int64_t nb = std::min<int64_t>(cc.out_bytes, c->out_cap);
+            if (cc.out_bytes > c->out_cap) e->stats.overruns++;
+            c->audio.push(s.h_out + s.out_off[k], (size_t)nb);
             e->stats.audio_bytes += nb;
             e->stats.ddc_outputs += cc.n_ddc;
             c->smeter.push((const uint8_t*)(s.h_sm + (int64_t)k * e->sm_stride),
@@ -516,18 +519,21 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
 
 static int ensure_post_capacity(owrx_engine* e) {
     const int n = (int)e->chains.size();
-    int64_t need_out = 64, need_sm = 4, need_dbg = 64;
+    // output staging: one region per chain, sized by that chain's own worst case (ADPCM audio
+    // is ~2.6 KB per C2 block, a service resampler's cf32 IF up to 8 B per decimated sample)
+    int64_t need_out = 256, need_sm = 4, need_dbg = 64;
     for (auto& kv : e->chains) {
-        need_out = std::max(need_out, kv.second->out_cap);
+        need_out += out_region(kv.second->out_cap);
         need_sm = std::max<int64_t>(need_sm, kv.second->sm_cap);
         need_dbg = std::max<int64_t>(need_dbg, kv.second->cap * 8 + 64);
     }
-    if (n <= e->post_cap && need_out <= e->out_stride && need_sm <= e->sm_stride &&
+    if (n <= e->post_cap && need_out <= e->out_total && need_sm <= e->sm_stride &&
         (!e->debug || need_dbg <= e->dbg_stride))
         return OWRX_OK;
     RCCHK(drain_all(e));
-    const int cap = std::max(n, e->post_cap ? e->post_cap * 2 : 16);
-    e->out_stride = (need_out + 255) & ~(int64_t)255;
+    // posts capacity grows geometrically; the output region total is re-derived every time
+    const int cap = n <= e->post_cap ? e->post_cap : std::max(n, e->post_cap ? e->post_cap * 2 : 16);
+    e->out_total = need_out + need_out / 2;  // headroom: adding a chain rarely reallocates
     e->sm_stride = need_sm;
     e->dbg_stride = e->debug ? (need_dbg + 255) & ~(int64_t)255 : 0;
     for (int si = 0; si < kSlots; ++si) {
@@ -538,10 +544,10 @@ static int ensure_post_capacity(owrx_engine* e) {
         HIPCHK(dalloc(&s.d_sel, (size_t)cap + 64 * 3 * 4));  // + demodulator-run padding
         HIPCHK(halloc(&s.h_sel, (size_t)cap + 64 * 3 * 4));
         HIPCHK(dalloc(&s.d_counts, cap));
-        HIPCHK(dalloc(&s.d_out, (size_t)cap * e->out_stride));
+        HIPCHK(dalloc(&s.d_out, (size_t)e->out_total));
         HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
         HIPCHK(halloc(&s.h_counts, (size_t)cap));
-        HIPCHK(halloc(&s.h_out, (size_t)cap * e->out_stride));
+        HIPCHK(halloc(&s.h_out, (size_t)e->out_total));
         HIPCHK(halloc(&s.h_sm, (size_t)cap * e->sm_stride));
         if (e->debug) {
             HIPCHK(dalloc(&s.d_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
@@ -740,6 +746,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     // ---- chains: DDC per group (A); post_parallel + post_serial_front (B); ADPCM + copies (C)
     e->posts.clear();
     S.post_ids.clear();
+    S.out_off.clear();
+    int64_t out_off = 0;
     struct GroupWork {
         ChainGroup* g;
         int64_t k_end;
@@ -822,8 +830,10 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.k_begin = g->k_next;
             p.k_first = c->k_first;
             const int slot = (int)e->posts.size();
-            p.out = S.d_out + (int64_t)slot * e->out_stride;
-            p.out_cap = e->out_stride;
+            p.out = S.d_out + out_off;
+            p.out_cap = c->out_cap;
+            S.out_off.push_back(out_off);
+            out_off += out_region(c->out_cap);
             p.smeter = S.d_sm + (int64_t)slot * e->sm_stride;
             p.smeter_cap = (int)e->sm_stride;
             p.debug = (e->debug && S.d_dbg) ? 1 : 0;
@@ -891,7 +901,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         HIPCHK(hipStreamWaitEvent(e->sR, S.evC, 0));
         HIPCHK(hipMemcpyAsync(S.h_counts, S.d_counts, sizeof(ChainCounts) * np,
                               hipMemcpyDeviceToHost, e->sR));
-        HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, (size_t)np * e->out_stride,
+        HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, (size_t)out_off,
                               hipMemcpyDeviceToHost, e->sR));
         HIPCHK(hipMemcpyAsync(S.h_sm, S.d_sm, sizeof(float) * np * e->sm_stride,
                               hipMemcpyDeviceToHost, e->sR));
@@ -1285,6 +1295,9 @@ int64_t owrx_waterfall_read(owrx_engine* e, int handle, uint8_t* dst, int64_t ma
 // ---- chains -----------------------------------------------------------------------------
 
 static int chain_validate(const owrx_chain_params* p) {
+    if (p && p->output == OWRX_OUT_IQ)  // DDC only: the rest of the struct is unused
+        return (p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate != 1.0)
+                   ? OWRX_EINVAL : OWRX_OK;
     if (!p || p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate <= 0 ||
         p->sq_length <= 0 || p->sq_length > 3072 || p->sq_decimation <= 0 || p->demod < 0 ||
         p->demod > 2 || p->output < 0 || p->output > 2 || p->audio_rate <= 0 ||
@@ -1371,8 +1384,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     c->rate_fx = rate_to_fx(p->shift_rate);
     c->cap = chain_stage_cap(e, D, p->frac_rate);
     const int64_t scap = c->cap + p->sq_length + 16;
-    c->out_cap = 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
-    c->sm_cap = (int)(scap / p->sq_length + 4);
+    c->out_cap = p->output == OWRX_OUT_IQ ? 8 * c->cap + 64
+                                          : 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
+    c->sm_cap = p->output == OWRX_OUT_IQ ? 4 : (int)(scap / p->sq_length + 4);
     ChainStateP ps;
     memset(&ps, 0, sizeof(ps));
     ChainStateS ss;

@@ -17,6 +17,7 @@
 #include <climits>
 #include <type_traits>
 
+#include "../../include/owrx_amd.h"
 #include "owrx_types.h"
 
 namespace owrx {
@@ -84,9 +85,25 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
                 y.x += v.x;
                 y.y += v.y;
             }
-            ddc_buf[kFdHist + i] = y;
             if (P.debug && i < P.dbg_cap) P.dbg_ddc[i] = y;
+            if (P.output == OWRX_OUT_IQ) {  // service Resampler: the DDC output is the product
+                reinterpret_cast<float2*>(P.out)[i] = y;
+                continue;
+            }
+            ddc_buf[kFdHist + i] = y;
         }
+    }
+    if (P.output == OWRX_OUT_IQ) {
+        if (tid == 0) {
+            S.ddc_count += n_new;
+            *P.pstate = S;
+            ChainCounts& c = counts[blockIdx.x];
+            c.out_bytes = (int64_t)n_new * 8;
+            c.smeter = 0;
+            c.n_ddc = n_new;
+            c.n_fd = c.n_bp = c.n_sq = 0;
+        }
+        return;
     }
     __syncthreads();
     const int64_t ddc_base = S.ddc_count - kFdHist;  // local index of ddc_buf[0]

@@ -7,6 +7,7 @@ exact module arguments the reference would construct (pinned by tests/golden/cha
   -- csdr/chain/selector.py:115-147, 159-166
 * NFm / Am / Ssb / ClientAudioChain module choices -- csdr/chain/analog.py, clientaudio.py
 * mode bandpass table -- owrx/modes.py:124-129
+* service Resampler (Shift + FirDecimate to a band) -- owrx/source/resampler.py:11-26
 """
 import math
 
@@ -102,3 +103,20 @@ def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=Non
     p.audio_rate = output_rate
     p.output = output
     return p
+
+
+def resampler_params(sdr_samp_rate, sdr_center_freq, center_freq, samp_rate):
+    """(owrx_chain_params, if_samp_rate) for the service Resampler (owrx/source/resampler.py:11-26):
+    Shift((sdr_cf - cf) / sdr_rate) -> FirDecimate(int(sdr_rate / rate), 0.15 * if_rate / sdr_rate)
+    with FirDecimate's default cutoff 0.5; the output is the cf32 IF at sdr_rate / decimation."""
+    shift = (sdr_center_freq - center_freq) / sdr_samp_rate
+    d = int(float(sdr_samp_rate) / samp_rate)
+    if_rate = sdr_samp_rate / d
+    p = _lib.ChainParams()
+    p.shift_rate = f32(shift)
+    p.decimation = d
+    p.transition = f32(0.15 * (if_rate / float(sdr_samp_rate)))
+    p.cutoff = f32(0.5)
+    p.frac_rate = 1.0
+    p.output = _lib.OUT_IQ
+    return p, if_rate

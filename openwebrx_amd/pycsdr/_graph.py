@@ -123,6 +123,14 @@ def plan_segment(head):
     fir = take(M.FirDecimate)
     if fir is None:
         return None
+    chain_next = (M.FractionalDecimator, M.Bandpass, M.Squelch, M.FmDemod, M.AmDemod,
+                  M.RealPart)
+    if fir.writer is not None and (i == len(mods) or not isinstance(mods[i], chain_next)):
+        # Shift -> FirDecimate -> Buffer(COMPLEX_FLOAT): the service Resampler
+        # (owrx/source/resampler.py:11-26); the engine emits the cf32 DDC output itself
+        p = dict(shift_rate=shift.rate, decimation=fir.decimation, transition=fir.transition,
+                 cutoff=fir.cutoff, frac_rate=1.0, output=_lib.OUT_IQ, power_writer=None)
+        return ("chain", p, mods[:i])
     frac = take(M.FractionalDecimator)
     bp = take(M.Bandpass)
     sq = take(M.Squelch)
@@ -248,11 +256,11 @@ class EngineDriver:
         else:
             if old["shift_rate"] != p["shift_rate"]:
                 obj.set_shift_rate(p["shift_rate"])
-            if (old["bandpass"], old["bp_low"], old["bp_high"]) != \
-                    (p["bandpass"], p["bp_low"], p["bp_high"]):
+            if (old.get("bandpass"), old.get("bp_low"), old.get("bp_high")) != \
+                    (p.get("bandpass"), p.get("bp_low"), p.get("bp_high")):
                 obj.set_bandpass(p["bp_low"], p["bp_high"]) if p["bandpass"] else \
                     obj.set_bandpass(None, None)
-            if old["sq_level"] != p["sq_level"]:
+            if old.get("sq_level") != p.get("sq_level"):
                 obj.set_squelch_level(p["sq_level"])
         self.segments[hid] = (kind, p, mods, obj)
 
@@ -328,4 +336,4 @@ def _compatible(kind, old, new):
         keys = ("decimation", "transition", "cutoff", "frac_rate", "bp_transition", "sq_length",
                 "sq_decimation", "sq_hang", "sq_flush", "sq_report", "demod", "agc_profile",
                 "agc_initial_gain", "agc_max_gain", "audio_rate", "output")
-    return all(old[k] == new[k] for k in keys)
+    return all(old.get(k) == new.get(k) for k in keys)

@@ -298,6 +298,30 @@ def test_ddc_large_groups(amd, nch):
     eng.close()
 
 
+@pytest.mark.parametrize("fs,bw", [(2400000, 48000), (10000000, 250000)])
+def test_service_resampler_iq(amd, fs, bw):
+    """Service Resampler (owrx/source/resampler.py:11-26): Shift + FirDecimate to a band, the cf32
+    IF is the product (OWRX_OUT_IQ), next to a client chain on the same engine."""
+    from openwebrx_amd import synth
+    n = 1 << 20
+    iq, offs = synth.make_iq(fs, n, ["nfm", "usb", "am"])
+    sdr_cf = 145000000
+    p, if_rate = amd.params.resampler_params(fs, sdr_cf, sdr_cf + offs[1] + 3000, bw)
+    assert p.decimation == int(fs / bw) and abs(if_rate - fs / p.decimation) < 1e-6
+    audio = amd.params.chain_params(fs, offs[0], "nfm", output=amd._lib.OUT_S16)
+    eng, (rs, ch) = _run_chains(amd, iq, fs, [p, audio], 1 << 18, debug=False)
+    got = np.frombuffer(rs.read_audio(), np.complex64)
+    c = oracle.chain_from_engine_params(p)
+    ref = oracle.fir_decimate(oracle.shift(iq, p.shift_rate), c._keep[0], p.decimation)
+    assert got.size == ref.size, (got.size, ref.size)
+    assert rel_rms(got, ref) < 1e-5
+    s16 = np.frombuffer(ch.read_audio(), np.int16)
+    ref_a = oracle.stages(iq, audio)["s16"]
+    assert s16.size == ref_a.size
+    assert np.mean(np.abs(s16.astype(np.int32) - ref_a) <= 1) > 0.999
+    eng.close()
+
+
 def test_adpcm_chain_output_decodes(amd):
     """AdpcmEncoder(sync=True) stream: SYNC frames every 1001 data bytes, decodable."""
     from openwebrx_amd import synth

@@ -88,3 +88,17 @@ def test_chain_params_struct(gold):
     nfm_mods = [e["module"] for e in gold["nfm"] if e["op"] == "new"]
     assert nfm_mods == ["Agc", "FmDemod", "Limit", "NfmDeemphasis"]
     assert [e["method"] for e in gold["nfm"] if e["op"] == "call"] == ["setProfile", "setMaxGain"]
+
+
+def test_resampler_params_follow_reference_math():
+    """owrx/source/resampler.py:11-26: shift = (sdr_cf - cf) / sdr_rate, decimation =
+    int(sdr_rate / rate), if rate = sdr_rate / decimation, transition = 0.15 * if / sdr_rate,
+    FirDecimate default cutoff 0.5."""
+    from openwebrx_amd import _lib
+    p, if_rate = params.resampler_params(2400000, 145000000, 145300000, 48000)
+    assert p.decimation == 50 and if_rate == 48000.0
+    assert p.shift_rate == np.float32(-300000 / 2400000)
+    assert p.transition == np.float32(0.15 * 48000 / 2400000)
+    assert p.cutoff == 0.5 and p.frac_rate == 1.0 and p.output == _lib.OUT_IQ
+    p, if_rate = params.resampler_params(10000000, 14100000, 14074000, 300000)
+    assert p.decimation == 33 and abs(if_rate - 10e6 / 33) < 1e-9

@@ -305,3 +305,21 @@ def test_ingest_modules_formats():
         conv.setReader(M.Buffer(Format.COMPLEX_FLOAT).getReader())
     with pytest.raises(NotImplementedError):
         M.Convert(Format.COMPLEX_FLOAT, Format.COMPLEX_SHORT)
+
+
+def test_planner_recognises_service_resampler():
+    """Shift -> FirDecimate -> Buffer (owrx/source/resampler.py) plans as an OUT_IQ chain even
+    with a (non-fusable) consumer on the IF buffer."""
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    p, _ = params.resampler_params(2400000, 145000000, 145300000, 48000)
+    shift = M.Shift(p.shift_rate)
+    fir = M.FirDecimate(p.decimation, p.transition)
+    Chain([shift, fir])
+    shift.setReader(wide.getReader())
+    out = M.Buffer(Format.COMPLEX_FLOAT)
+    fir.setWriter(out)
+    out.getReader()
+    kind, q, used = _graph.plan_segment(shift)
+    assert kind == "chain" and used == [shift, fir]
+    assert q["output"] == _lib.OUT_IQ and q["decimation"] == 50 and q["cutoff"] == 0.5
+    _graph.finish(wide)
