@@ -85,7 +85,9 @@ int owrx_sync(owrx_engine* e);
 /* ---- waterfall: FftChain (csdr/chain/fft.py:25-96) --------------------------------------
  * Fft(size=fft_size, every_n_samples) -> LogAveragePower(add_db, fft_size, avg_number) or
  * LogPower(add_db) when avg_number == 0 (fft.py:18-22) -> FftSwap -> FftAdpcm if compression.
- * fft_size: power of two, 256..16384 (owrx/controllers/settings/general.py:181). */
+ * fft_size: power of two, 256..65536.  The reference UI validates 256..16384
+ * (owrx/controllers/settings/general.py:181); BASELINE config 4 asks for 65536 bins (sizes
+ * above 16384 run a two-launch four-step FFT). */
 int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int avg_number,
                           float add_db, int adpcm, int* handle);
 /* FftChain._setBlockSize / setFftAverages / setCompression (fft.py:51-55, 11-16, 87-96) */

@@ -43,7 +43,7 @@ void set_last_error(const char* fmt, ...) {
 // kernel launchers (kernels_*.hip)
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, const float* window, const float2* tw, float* partial,
-                         hipStream_t st);
+                         float2* scratch, hipStream_t st);
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st);
@@ -62,7 +62,9 @@ hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st);
 
-constexpr int kWfFramesPerGroup = 1;
+constexpr int kWfFramesPerGroup = 1;  // the four-step FFT (N > kWfLdsMaxN) relies on it
+constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
+constexpr int kWfMaxN = 65536;
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
 constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
@@ -148,6 +150,7 @@ struct Waterfall {
     float* d_window = nullptr;
     float2* d_tw = nullptr;
     float* d_partial = nullptr;
+    float2* d_y4 = nullptr;  // four-step FFT scratch (N > 16384): one cf32 frame per group
     int partial_groups = 0;
     WfGroup* h_groups[2] = {};  // pinned copy sources, per block parity
     WfRow* h_rows[2] = {};
@@ -341,6 +344,7 @@ static void free_wf(Waterfall* w) {
     dfree(w->d_window);
     dfree(w->d_tw);
     dfree(w->d_partial);
+    dfree(w->d_y4);
     dfree(w->d_carry[0]);
     dfree(w->d_carry[1]);
     dfree(w->d_groups);
@@ -487,7 +491,9 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
     if (groups > w->partial_groups) {
         dfree(w->d_partial);
         dfree(w->d_groups);
+        dfree(w->d_y4);
         HIPCHK(dalloc(&w->d_partial, (size_t)groups * w->N));
+        if (w->N > kWfLdsMaxN) HIPCHK(dalloc(&w->d_y4, (size_t)groups * w->N));
         HIPCHK(dalloc(&w->d_groups, (size_t)groups));
         for (int b = 0; b < 2; ++b) {
             hfree(w->h_groups[b]);
@@ -674,7 +680,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     HIPCHK(hipMemcpyAsync(w->d_rows, w->h_rows[bp], sizeof(WfRow) * w->rowdesc.size(),
                           hipMemcpyHostToDevice, e->sA));
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(),
-                         w->d_window, w->d_tw, w->d_partial, e->sA));
+                         w->d_window, w->d_tw, w->d_partial, w->d_y4, e->sA));
     const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
     const int cin = w->carry_idx, cout = 1 - w->carry_idx;
     HIPCHK(launch_wf_finalize(w->d_partial, w->d_rows, (int)w->rowdesc.size(), w->d_carry[cin],
@@ -1204,9 +1210,9 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
     ENGINE_GUARD(e);
     int logn = 0;
     while ((1 << logn) < fft_size) logn++;
-    if (!handle || fft_size < 256 || fft_size > 16384 || (1 << logn) != fft_size ||
+    if (!handle || fft_size < 256 || fft_size > kWfMaxN || (1 << logn) != fft_size ||
         every_n_samples <= 0 || avg_number < 0) {
-        set_last_error("owrx_waterfall_create: fft_size must be a power of two in [256, 16384], "
+        set_last_error("owrx_waterfall_create: fft_size must be a power of two in [256, 65536], "
                        "every_n_samples > 0");
         return OWRX_EINVAL;
     }

@@ -130,6 +130,141 @@ wf_fft_power(const float2* __restrict__ blk, int64_t blk_start,
     }
 }
 
+// ---- FFT sizes above one CU's LDS (32768, 65536): four-step, two launches ------------------
+// N = N1 * N2, n = N2*n1 + n2, k = k1 + N1*k2:
+//   X[k1 + N1 k2] = sum_n2 W_N2^(n2 k2) * W_N^(n2 k1) * sum_n1 x[N2 n1 + n2] W_N1^(n1 k1).
+// wf_fft4_cols: 32 columns n2 of one frame per workgroup -- windowed loads (32 consecutive
+//   samples = 256 B per n1), N1-point FFTs in LDS, twiddle W_N^(n2 k1), store Y[k1][n2]
+//   (256 B runs).  wf_fft4_rows: 32 rows k1 per workgroup -- contiguous loads of Y, N2-point
+//   FFTs in LDS, |X|^2 stored in natural bin order (32 consecutive bins = 128 B runs).  Y is a
+//   per-frame scratch of N cf32 (L2/HBM); the frame is read once from HBM like the LDS kernel.
+constexpr int kF4Rows = 32;    // columns (pass 1) / rows (pass 2) per workgroup
+constexpr int kF4Threads = 256;
+
+// R rows of length 2^LOGL in LDS (row stride RS float2), in-place Stockham radix-4 (+ one
+// radix-2 pass for odd LOGL); W_L^m = tw[m * twstep] (tw: the N-point table).
+template <int LOGL, int R, int NT>
+OWRX_DEV void lds_fft_rows(float2* sm, int RS, const float2* __restrict__ tw, int twstep) {
+    constexpr int L = 1 << LOGL;
+    constexpr int NB = R * (L / 4) / NT;
+    static_assert(NB >= 1 && NB * NT == R * (L / 4), "rows x butterflies must tile the threads");
+    const int tid = threadIdx.x;
+    int lns = 0;
+#pragma unroll
+    for (int pass = 0; pass < LOGL / 2; ++pass) {
+        float2 a[NB][4];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int idx = tid + b * NT;
+            const int base = (idx / (L / 4)) * RS;
+            const int j = idx % (L / 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[b][r] = sm[base + j + r * (L / 4)];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int idx = tid + b * NT;
+            const int base = (idx / (L / 4)) * RS;
+            const int j = idx % (L / 4);
+            const int k = j & ((1 << lns) - 1);
+            const int ts = (k << (LOGL - 2 - lns)) * twstep;
+            const float2 a0 = a[b][0];
+            const float2 a1 = cmul(a[b][1], tw[ts]);
+            const float2 a2 = cmul(a[b][2], tw[2 * ts]);
+            const float2 a3 = cmul(a[b][3], tw[3 * ts]);
+            const float2 t0 = make_float2(a0.x + a2.x, a0.y + a2.y);
+            const float2 t1 = make_float2(a0.x - a2.x, a0.y - a2.y);
+            const float2 t2 = make_float2(a1.x + a3.x, a1.y + a3.y);
+            const float2 t3 = make_float2(a1.y - a3.y, a3.x - a1.x);  // -i (a1 - a3)
+            const int d = base + ((j >> lns) << (lns + 2)) + k;
+            const int ns = 1 << lns;
+            sm[d] = make_float2(t0.x + t2.x, t0.y + t2.y);
+            sm[d + ns] = make_float2(t1.x + t3.x, t1.y + t3.y);
+            sm[d + 2 * ns] = make_float2(t0.x - t2.x, t0.y - t2.y);
+            sm[d + 3 * ns] = make_float2(t1.x - t3.x, t1.y - t3.y);
+        }
+        __syncthreads();
+        lns += 2;
+    }
+    if constexpr (LOGL & 1) {
+        constexpr int NB2 = R * (L / 2) / NT;
+        float2 a[NB2][2];
+#pragma unroll
+        for (int b = 0; b < NB2; ++b) {
+            const int idx = tid + b * NT;
+            const int base = (idx / (L / 2)) * RS;
+            const int j = idx % (L / 2);
+            a[b][0] = sm[base + j];
+            a[b][1] = sm[base + j + L / 2];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < NB2; ++b) {
+            const int idx = tid + b * NT;
+            const int base = (idx / (L / 2)) * RS;
+            const int j = idx % (L / 2);
+            const int k = j & ((1 << lns) - 1);
+            const float2 a1 = cmul(a[b][1], tw[(k << (LOGL - 1 - lns)) * twstep]);
+            const int d = base + ((j >> lns) << (lns + 1)) + k;
+            sm[d] = make_float2(a[b][0].x + a1.x, a[b][0].y + a1.y);
+            sm[d + (1 << lns)] = make_float2(a[b][0].x - a1.x, a[b][0].y - a1.y);
+        }
+        __syncthreads();
+    }
+}
+
+template <int LOG1, int LOG2>
+__global__ void __launch_bounds__(kF4Threads)
+wf_fft4_cols(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+             const float* __restrict__ window, const float2* __restrict__ tw,
+             float2* __restrict__ Y) {
+    constexpr int N1 = 1 << LOG1, N2 = 1 << LOG2, N = N1 * N2, C = kF4Rows, RS = N1 + 1;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int tid = threadIdx.x;
+    const int c0 = blockIdx.x * C;
+    const WfGroup g = groups[blockIdx.y];
+    const float2* x = blk + (g.start - blk_start);
+    for (int i = tid; i < N1 * C; i += kF4Threads) {
+        const int n1 = i / C, cc = i % C;
+        const int n = N2 * n1 + c0 + cc;
+        const float2 v = x[n];
+        const float w = window[n];
+        sm[cc * RS + n1] = make_float2(v.x * w, v.y * w);
+    }
+    __syncthreads();
+    lds_fft_rows<LOG1, C, kF4Threads>(sm, RS, tw, N2);
+    float2* y = Y + (int64_t)blockIdx.y * N;
+    for (int i = tid; i < N1 * C; i += kF4Threads) {
+        const int k1 = i / C, cc = i % C;
+        const int n2 = c0 + cc;
+        y[k1 * N2 + n2] = cmul(sm[cc * RS + k1], tw[(n2 * k1) & (N - 1)]);
+    }
+}
+
+template <int LOG1, int LOG2>
+__global__ void __launch_bounds__(kF4Threads)
+wf_fft4_rows(const float2* __restrict__ Y, const float2* __restrict__ tw,
+             float* __restrict__ partial) {
+    constexpr int N1 = 1 << LOG1, N2 = 1 << LOG2, N = N1 * N2, R = kF4Rows, RS = N2 + 1;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * R;
+    const float2* y = Y + (int64_t)blockIdx.y * N;
+    for (int i = tid; i < R * N2; i += kF4Threads) {
+        const int r = i / N2, n2 = i % N2;
+        sm[r * RS + n2] = y[(r0 + r) * N2 + n2];
+    }
+    __syncthreads();
+    lds_fft_rows<LOG2, R, kF4Threads>(sm, RS, tw, N1);
+    float* out = partial + (int64_t)blockIdx.y * N;
+    for (int i = tid; i < R * N2; i += kF4Threads) {
+        const int r = i % R, k2 = i / R;
+        const float2 X = sm[r * RS + k2];
+        out[r0 + r + N1 * k2] = X.x * X.x + X.y * X.y;
+    }
+}
+
 __global__ void __launch_bounds__(256)
 wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
             const float* __restrict__ carry_in, float* __restrict__ carry_out, int N,
@@ -214,9 +349,35 @@ static hipError_t launch_fft_t(const float2* blk, int64_t blk_start, const WfGro
     return hipGetLastError();
 }
 
+template <int LOG1, int LOG2>
+static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                int ngroups, const float* window, const float2* tw,
+                                float* partial, float2* scratch, hipStream_t st) {
+    constexpr int N1 = 1 << LOG1, N2 = 1 << LOG2;
+    const size_t lds1 = sizeof(float2) * kF4Rows * (N1 + 1);
+    const size_t lds2 = sizeof(float2) * kF4Rows * (N2 + 1);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft4_cols<LOG1, LOG2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)wf_fft4_rows<LOG1, LOG2>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    if (!scratch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((wf_fft4_cols<LOG1, LOG2>), dim3(N2 / kF4Rows, ngroups), dim3(kF4Threads),
+                       lds1, st, blk, blk_start, groups, window, tw, scratch);
+    hipLaunchKernelGGL((wf_fft4_rows<LOG1, LOG2>), dim3(N1 / kF4Rows, ngroups), dim3(kF4Threads),
+                       lds2, st, scratch, tw, partial);
+    return hipGetLastError();
+}
+
+// scratch: ngroups * N cf32, used for N > 16384 (groups hold one frame each there)
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, const float* window, const float2* tw, float* partial,
-                         hipStream_t st) {
+                         float2* scratch, hipStream_t st) {
     switch (logn) {
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
@@ -225,6 +386,10 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
         case 12: return launch_fft_t<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 13: return launch_fft_t<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 14: return launch_fft_t<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 15: return launch_fft4_t<7, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
+                                            scratch, st);
+        case 16: return launch_fft4_t<8, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
+                                            scratch, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -171,7 +171,8 @@ def _wf(amd, iq, fs, N, hop, avg, adpcm, block):
     return rows
 
 
-@pytest.mark.parametrize("N,fs", [(4096, 2400000), (16384, 10000000), (2048, 1000000), (512, 48000)])
+@pytest.mark.parametrize("N,fs", [(4096, 2400000), (16384, 10000000), (2048, 1000000), (512, 48000),
+                                  (32768, 20000000), (65536, 61440000)])
 def test_waterfall_float_rows(amd, N, fs):
     avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
     avg = min(avg, 6)  # keep the double-precision oracle quick; avg semantics unchanged
@@ -336,7 +337,7 @@ def test_adpcm_chain_output_decodes(amd):
     eng.close()
 
 
-@pytest.mark.parametrize("N,fs", [(4096, 2400000), (16384, 10000000)])
+@pytest.mark.parametrize("N,fs", [(4096, 2400000), (16384, 10000000), (65536, 61440000)])
 def test_waterfall_adpcm_rows_bit_exact(amd, N, fs):
     """The row-parallel speculative IMA-ADPCM encoder is bit-identical to the sequential
     FftAdpcm restatement: two FftChains on one engine (float and ADPCM output) see the same
@@ -357,4 +358,47 @@ def test_waterfall_adpcm_rows_bit_exact(amd, N, fs):
     assert rf.shape[0] == ra.shape[0] == 5
     for r in range(rf.shape[0]):
         assert ra[r].tobytes() == oracle.fft_adpcm_row(rf[r])
+    eng.close()
+
+
+def _check_sampled_chains(iq, plist, chains, sample):
+    for c in sample:
+        ref = oracle.stages(iq, plist[c])
+        ddc = chains[c].read_debug(0)
+        assert ddc.size == ref["ddc"].size, (c, ddc.size, ref["ddc"].size)
+        assert rel_rms(ddc, ref["ddc"]) < 1e-5, c
+        s16 = np.frombuffer(chains[c].read_audio(), np.int16)
+        assert s16.size == ref["s16"].size, (c, s16.size, ref["s16"].size)
+        d = np.abs(s16.astype(np.int32) - ref["s16"])
+        assert np.mean(d <= 1) > 0.999, (c, np.mean(d <= 1))
+
+
+def test_c3_256_mixed_chains_10msps(amd):
+    """BASELINE config 3 shape: 10 Msps, 256 chains (86 NFM + 85 USB + 85 CW), one
+    (D=833, 22223-tap) design in one DDC group; sampled chains vs the oracle."""
+    from openwebrx_amd import synth
+    fs = 10000000
+    modes = ["nfm"] * 86 + ["usb"] * 85 + ["cw"] * 85
+    n = 1 << 20
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16)
+             for o, m in zip(offs, modes)]
+    eng, chains = _run_chains(amd, iq, fs, plist, 1 << 19)
+    _check_sampled_chains(iq, plist, chains, [0, 100, 255])
+    eng.close()
+
+
+def test_c4_chains_61msps(amd):
+    """BASELINE config 4 chain design at 61.44 Msps: D=5120, 136533 taps, no fractional
+    decimator (61.44 MHz / 5120 = 12 kHz exactly); DDC and audio vs the oracle."""
+    from openwebrx_amd import synth
+    fs = 61440000
+    modes = ["nfm", "usb", "am"]
+    n = 1 << 23  # 1612 outputs per chain: two 750-sample squelch blocks of audio
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16)
+             for o, m in zip(offs, modes)]
+    assert plist[0].decimation == 5120 and plist[0].frac_rate == 1.0
+    eng, chains = _run_chains(amd, iq, fs, plist, 1 << 19)
+    _check_sampled_chains(iq, plist, chains, range(3))
     eng.close()
