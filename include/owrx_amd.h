@@ -137,6 +137,21 @@ int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level);
 int64_t owrx_chain_read_audio(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes);
 /* Squelch power writer values (owrx/connection.py:483-489) */
 int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t max_values);
+/* Secondary FFT of the chain's Selector output: ClientDemodulatorChain._createSecondaryFftChain
+ * (owrx/dsp.py:220-225) = FftChain(selectorOutputRate, digimodes_fft_size, 0.3, 9, "adpcm")
+ * reading selectorBuffer, i.e. Fft(size, every_n_samples) -> LogAveragePower(add_db, size,
+ * avg_number) | LogPower when avg_number == 0 -> FftSwap -> FftAdpcm if adpcm
+ * (csdr/chain/fft.py:25-96).  fft_size: 0 (remove) or a power of two in [1024, 8192];
+ * setSecondaryFftSize / setSampleRate re-create it (owrx/dsp.py:357-363, :216-217), which
+ * restarts the row stream.  Rows are owrx_chain_secondary_fft_row_bytes() each:
+ * (fft_size+10)/2 ADPCM bytes or fft_size f32 dB. */
+int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int every_n_samples,
+                                 int avg_number, float add_db, int adpcm);
+int64_t owrx_chain_secondary_fft_row_bytes(owrx_engine* e, int handle);
+/* whole rows only (<= max_bytes); the secondary FFT Writer (frame type 0x03,
+ * owrx/connection.py:500-501) */
+int64_t owrx_chain_read_secondary_fft(owrx_engine* e, int handle, uint8_t* dst,
+                                      int64_t max_bytes);
 /* absolute stream sample index of the chain's sample 0 (aligned to the decimation grid) */
 int64_t owrx_chain_origin(owrx_engine* e, int handle);
 

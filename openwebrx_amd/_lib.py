@@ -116,6 +116,9 @@ PROTOTYPES = {
     "owrx_chain_read_audio": (_i64, [_vp, _i32, _vp, _i64]),
     "owrx_chain_read_smeter": (_i64, [_vp, _i32, _vp, _i64]),
     "owrx_chain_origin": (_i64, [_vp, _i32]),
+    "owrx_chain_set_secondary_fft": (_i32, [_vp, _i32, _i32, _i32, _i32, _f32, _i32]),
+    "owrx_chain_secondary_fft_row_bytes": (_i64, [_vp, _i32]),
+    "owrx_chain_read_secondary_fft": (_i64, [_vp, _i32, _vp, _i64]),
     "owrx_set_debug": (_i32, [_vp, _i32]),
     "owrx_chain_read_debug": (_i64, [_vp, _i32, _i32, _vp, _i64]),
     "owrx_get_stats": (_i32, [_vp, ctypes.POINTER(Stats)]),

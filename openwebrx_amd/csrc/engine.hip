@@ -59,6 +59,8 @@ hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts
                                 hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, int output, int debug, hipStream_t st);
+hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, ChainCounts* counts,
+                             hipStream_t st);
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st);
 
@@ -129,6 +131,10 @@ struct ByteRing {  // host-side output queue
         }
     }
     size_t avail() const { return buf.size() - rd; }
+    void clear() {
+        buf.clear();
+        rd = 0;
+    }
     size_t pop(uint8_t* dst, size_t n) {
         n = std::min(n, avail());
         memcpy(dst, buf.data() + rd, n);
@@ -215,6 +221,17 @@ struct Chain {
     ByteRing audio;
     ByteRing smeter;
     ByteRing dbg[kDebugStages];
+    // secondary FFT (FftChain on the Selector output, owrx/dsp.py:220-225); sf_n == 0: none
+    int sf_n = 0, sf_logn = 0, sf_hop = 0, sf_avg = 1, sf_adpcm = 0;
+    float sf_add_db = -70.0f;
+    bool sf_reset = false;
+    float2* d_sf = nullptr;      // [sf_n + scap]
+    float* d_sf_acc = nullptr;   // [sf_n]
+    float* d_sf_window = nullptr;
+    float2* d_sf_tw = nullptr;
+    int64_t sf_out_cap = 0;      // staging bytes per step
+    ByteRing sfft;
+    int64_t sf_row_bytes() const { return sf_adpcm ? (sf_n + 10) / 2 : 4 * (int64_t)sf_n; }
 };
 
 struct Slot {  // one block's outputs in flight on streams B / C
@@ -338,6 +355,10 @@ static void free_chain(Chain* c) {
     for (int i = 0; i < kSlots; ++i) dfree(c->d_dem[i]);
     for (int i = 0; i < kSlots; ++i) dfree(c->d_s16[i]);
     dfree(c->d_bp_taps);
+    dfree(c->d_sf);
+    dfree(c->d_sf_acc);
+    dfree(c->d_sf_window);
+    dfree(c->d_sf_tw);
 }
 
 static void free_wf(Waterfall* w) {
@@ -397,6 +418,11 @@ static int drain_slot(owrx_engine* e, int si) {
             const int64_t nb = std::min<int64_t>(cc.out_bytes, c->out_cap);
             if (cc.out_bytes > c->out_cap) e->stats.overruns++;
             c->audio.push(s.h_out + s.out_off[k], (size_t)nb);
+            if (cc.sf_bytes > 0) {
+                const int64_t sb = std::min<int64_t>(cc.sf_bytes, c->sf_out_cap);
+                if (cc.sf_bytes > c->sf_out_cap) e->stats.overruns++;
+                c->sfft.push(s.h_out + s.out_off[k] + out_region(c->out_cap), (size_t)sb);
+            }
             e->stats.audio_bytes += nb;
             e->stats.ddc_outputs += cc.n_ddc;
             c->smeter.push((const uint8_t*)(s.h_sm + (int64_t)k * e->sm_stride),
@@ -529,7 +555,7 @@ static int ensure_post_capacity(owrx_engine* e) {
     // is ~2.6 KB per C2 block, a service resampler's cf32 IF up to 8 B per decimated sample)
     int64_t need_out = 256, need_sm = 4, need_dbg = 64;
     for (auto& kv : e->chains) {
-        need_out += out_region(kv.second->out_cap);
+        need_out += out_region(kv.second->out_cap) + out_region(kv.second->sf_out_cap);
         need_sm = std::max<int64_t>(need_sm, kv.second->sm_cap);
         need_dbg = std::max<int64_t>(need_dbg, kv.second->cap * 8 + 64);
     }
@@ -760,6 +786,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         int nk;
     };
     std::vector<GroupWork> work;
+    uint32_t sf_sizes = 0;  // secondary FFT sizes (log2 bit set) present this step
     for (auto& gp : e->groups) {  // descriptors first, so the DDC bracket holds only kernels
         ChainGroup* g = gp.get();
         if (g->members.empty()) continue;
@@ -840,6 +867,23 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.out_cap = c->out_cap;
             S.out_off.push_back(out_off);
             out_off += out_region(c->out_cap);
+            if (c->sf_n > 0 && q.output != OWRX_OUT_IQ) {
+                p.sf_n = c->sf_n;
+                p.sf_hop = c->sf_hop;
+                p.sf_avg = std::max(1, c->sf_avg);
+                p.sf_adpcm = c->sf_adpcm;
+                p.sf_reset = c->sf_reset ? 1 : 0;
+                c->sf_reset = false;
+                p.sf_corr = (float)((double)c->sf_add_db - 10.0 * std::log10((double)p.sf_avg));
+                p.sf_buf = c->d_sf;
+                p.sf_acc = c->d_sf_acc;
+                p.sf_window = c->d_sf_window;
+                p.sf_tw = c->d_sf_tw;
+                p.sf_out = S.d_out + out_off;
+                p.sf_out_cap = c->sf_out_cap;
+                sf_sizes |= 1u << c->sf_logn;
+            }
+            out_off += out_region(c->sf_out_cap);
             p.smeter = S.d_sm + (int64_t)slot * e->sm_stride;
             p.smeter_cap = (int)e->sm_stride;
             p.debug = (e->debug && S.d_dbg) ? 1 : 0;
@@ -867,6 +911,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                               hipMemcpyHostToDevice, e->sA));
         if (timed) HIPCHK(hipEventRecord(S.b0, e->sA));
         HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
+        for (int lg = 0; lg < 32; ++lg)
+            if (sf_sizes & (1u << lg)) HIPCHK(launch_chain_sfft(lg, S.d_posts, np, S.d_counts, e->sA));
         HIPCHK(hipEventRecord(S.evA, e->sA));
         HIPCHK(hipStreamWaitEvent(e->sB, S.evA, 0));
         // one post_serial_front launch per output format present (S16 / ADPCM / F32); within
@@ -1484,6 +1530,80 @@ int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t m
     if (it == e->chains.end() || !dst || max_values < 0) return OWRX_EINVAL;
     return (int64_t)it->second->smeter.pop((uint8_t*)dst, sizeof(float) * (size_t)max_values) /
            (int64_t)sizeof(float);
+}
+
+int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int every_n_samples,
+                                 int avg_number, float add_db, int adpcm) {
+    ENGINE_GUARD(e);
+    auto it = e->chains.find(handle);
+    if (it == e->chains.end()) return OWRX_EINVAL;
+    Chain* c = it->second.get();
+    int logn = 0;
+    while ((1 << logn) < fft_size) logn++;
+    if (fft_size != 0 && (fft_size < 1024 || fft_size > 8192 || (1 << logn) != fft_size ||
+                          every_n_samples <= 0 || avg_number < 0 ||
+                          c->prm.output == OWRX_OUT_IQ)) {
+        set_last_error("owrx_chain_set_secondary_fft: fft_size must be 0 or a power of two in "
+                       "[1024, 8192], every_n_samples > 0, on an audio chain");
+        return OWRX_EINVAL;
+    }
+    RC_FAIL(e, drain_all(e));
+    if (fft_size != c->sf_n) {
+        dfree(c->d_sf);
+        dfree(c->d_sf_acc);
+        dfree(c->d_sf_window);
+        dfree(c->d_sf_tw);
+        c->sf_n = 0;
+        c->sf_out_cap = 0;
+        if (fft_size > 0) {
+            const int64_t scap = c->cap + c->prm.sq_length + 16;
+            HIPCHK(dalloc(&c->d_sf, (size_t)(fft_size + scap + 64)));
+            HIPCHK(dalloc(&c->d_sf_acc, (size_t)fft_size));
+            HIPCHK(dalloc(&c->d_sf_window, (size_t)fft_size));
+            HIPCHK(dalloc(&c->d_sf_tw, (size_t)fft_size));
+            std::vector<float> win = hamming_window(fft_size);
+            std::vector<float> tw = fft_twiddles(fft_size);
+            HIPCHK(hipMemcpy(c->d_sf_window, win.data(), sizeof(float) * fft_size,
+                             hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(c->d_sf_tw, tw.data(), sizeof(float) * 2 * fft_size,
+                             hipMemcpyHostToDevice));
+        }
+    }
+    c->sf_n = fft_size;
+    c->sf_logn = logn;
+    c->sf_hop = every_n_samples;
+    c->sf_avg = avg_number;
+    c->sf_add_db = add_db;
+    c->sf_adpcm = adpcm ? 1 : 0;
+    c->sf_reset = true;
+    c->sfft.clear();
+    if (fft_size > 0) {
+        // rows per step: frames over (carried < N) + this step's samples, one row per avg frames
+        const int64_t scap = c->cap + c->prm.sq_length + 16;
+        const int64_t frames = (scap + fft_size) / every_n_samples + 2;
+        const int64_t rows = frames / std::max(1, avg_number) + 2;
+        c->sf_out_cap = rows * c->sf_row_bytes();
+    }
+    RC_FAIL(e, ensure_post_capacity(e));
+    return OWRX_OK;
+}
+
+int64_t owrx_chain_secondary_fft_row_bytes(owrx_engine* e, int handle) {
+    ENGINE_GUARD(e);
+    auto it = e->chains.find(handle);
+    if (it == e->chains.end() || it->second->sf_n == 0) return OWRX_EINVAL;
+    return it->second->sf_row_bytes();
+}
+
+int64_t owrx_chain_read_secondary_fft(owrx_engine* e, int handle, uint8_t* dst,
+                                      int64_t max_bytes) {
+    ENGINE_GUARD(e);
+    auto it = e->chains.find(handle);
+    if (it == e->chains.end() || !dst || max_bytes < 0) return OWRX_EINVAL;
+    Chain* c = it->second.get();
+    if (c->sf_n == 0) return 0;
+    const int64_t rb = c->sf_row_bytes();
+    return (int64_t)c->sfft.pop(dst, (size_t)((max_bytes / rb) * rb));
 }
 
 int64_t owrx_chain_origin(owrx_engine* e, int handle) {

@@ -57,6 +57,29 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     const auto smeter = gp(P.smeter);
     if (tid == 0) S = *P.pstate;
     __syncthreads();
+    // secondary FFT input: drop the samples chain_sfft has consumed (keep [sf_next, sf_fill))
+    int sf_fill = 0;
+    if (P.sf_n > 0) {
+        const auto sf = gp(P.sf_buf);
+        const int next = P.sf_reset ? 0 : S.sf_next;
+        const int keep = P.sf_reset ? 0 : S.sf_fill - next;
+        // chunked move through registers: a chunk's reads all precede its writes, and later
+        // chunks read at or beyond next + base + NT >= every index written before them
+        for (int base = 0; base < keep; base += NT) {
+            const int i = base + tid;
+            float2 v = make_float2(0.0f, 0.0f);
+            if (i < keep) v = sf[next + i];
+            __syncthreads();
+            if (i < keep) sf[i] = v;
+        }
+        sf_fill = keep > 0 ? keep : 0;
+        __syncthreads();
+        if (tid == 0) {
+            S.sf_fill = sf_fill;
+            S.sf_next = keep > 0 ? 0 : -keep;  // hop > N: the next frame starts past the data
+            if (P.sf_reset) S.sf_row_frame = 0;
+        }
+    }
 
     // ---- 0. FirDecimate output: fixed-order sum of the phase-segment partials ----------
     const int64_t kb = P.k_begin > P.k_first ? P.k_begin : P.k_first;
@@ -282,6 +305,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     for (int i = tid; i < nsq; i += NT) {
         const float2 x = sh_pass[i / L] ? sq_buf[i] : make_float2(0.0f, 0.0f);
         if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
+        if (P.sf_n > 0) P.sf_buf[sf_fill + i] = x;  // Selector output -> secondary FFT
         float v;
         if (P.demod == 0) {
             float2 prev = fm_prev0;
@@ -318,6 +342,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
             if (P.frac_enabled) S.fd_next += n_fd;
             S.fd_count += n_fd;
             S.sq_blocks += nb;
+            if (P.sf_n > 0) S.sf_fill = sf_fill + nsq;
             *P.pstate = S;
             ChainCounts& c = counts[blockIdx.x];
             c.n_ddc = n_new;

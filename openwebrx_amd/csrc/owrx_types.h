@@ -43,6 +43,13 @@ struct ChainStateP {
     int32_t flush_ctr;
     int32_t pad;
     float2 fm_last;
+    // secondary FFT input (squelch output history): sf_buf[0, sf_fill) holds samples, the next
+    // frame starts at sf_next (may exceed sf_fill when hop > N); post_parallel compacts and
+    // appends, chain_sfft consumes frames
+    int32_t sf_fill;
+    int32_t sf_next;
+    int32_t sf_row_frame;  // frames already summed into the open row (sf_acc)
+    int32_t sf_pad;
 };
 // Owned by post_serial (stream B).
 struct ChainStateS {
@@ -97,13 +104,26 @@ struct ChainPost {
     float* dbg_dem;
     float* dbg_agc;
     int64_t dbg_cap;
+    // secondary FFT on the Selector output (owrx/dsp.py:220-225): FftChain(rate, sf_n, ...)
+    int32_t sf_n;          // 0 => none
+    int32_t sf_hop;        // Fft every_n_samples
+    int32_t sf_avg;        // LogAveragePower avg_number (>= 1; LogPower == 1)
+    int32_t sf_adpcm;      // FftAdpcm
+    int32_t sf_reset;      // restart the secondary FFT stream this step
+    float sf_corr;         // add_db - 10 log10(avg)
+    float2* sf_buf;        // [sf_n + stage capacity]
+    float* sf_acc;         // [sf_n] open-row accumulator
+    const float* sf_window;
+    const float2* sf_tw;
+    uint8_t* sf_out;       // staging (rows of FftAdpcm bytes or f32 dB)
+    int64_t sf_out_cap;
 };
 
 // Per-chain counters written by the post kernels for the host (and n_sq for post_serial).
 struct ChainCounts {
     int64_t out_bytes;
     int32_t smeter;
-    int32_t pad;
+    int32_t sf_bytes;      // secondary FFT bytes staged this step
     int64_t n_ddc, n_fd, n_bp, n_sq;  // stage sample counts this step
 };
 

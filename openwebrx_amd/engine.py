@@ -211,6 +211,36 @@ class Chain:
                                              max_values), "read_smeter")
         return buf[:n].copy()
 
+    def set_secondary_fft(self, fft_size, every_n_samples=0, avg_number=0, add_db=-70.0,
+                          adpcm=True):
+        """FftChain on this chain's Selector output (owrx/dsp.py:220-225); fft_size 0 removes
+        it.  every_n_samples / avg_number as FftChain derives them (params.fft_parameters)."""
+        check(lib.owrx_chain_set_secondary_fft(self.engine.handle, self.id, int(fft_size),
+                                               int(every_n_samples), int(avg_number),
+                                               float(add_db), 1 if adpcm else 0),
+              "set_secondary_fft")
+        self._sf = (int(fft_size), bool(adpcm))
+
+    def read_secondary_fft(self):
+        """Whole secondary FFT rows produced so far: uint8 [rows, (N+10)/2] (ADPCM) or
+        float32 [rows, N] dB."""
+        n_fft, adpcm = getattr(self, "_sf", (0, True))
+        rb = check(lib.owrx_chain_secondary_fft_row_bytes(self.engine.handle, self.id),
+                   "secondary_fft_row_bytes")
+        buf = _scratch(max(rb, ((1 << 20) // rb) * rb))
+        out = []
+        while True:
+            n = check(lib.owrx_chain_read_secondary_fft(self.engine.handle, self.id,
+                                                        buf.ctypes.data, buf.size),
+                      "read_secondary_fft")
+            if n <= 0:
+                break
+            out.append(buf[:n].tobytes())
+        data = b"".join(out)
+        if adpcm:
+            return np.frombuffer(data, np.uint8).reshape(-1, rb)
+        return np.frombuffer(data, np.float32).reshape(-1, n_fft)
+
     def read_debug(self, stage, max_bytes=1 << 26):
         buf = np.empty(max_bytes, dtype=np.uint8)
         n = check(lib.owrx_chain_read_debug(self.engine.handle, self.id, stage, buf.ctypes.data,

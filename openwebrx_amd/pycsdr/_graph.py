@@ -62,16 +62,66 @@ def _find_head(module):
     return None
 
 
+def _readers_of(buf):
+    return [r.module for r in buf._readers if r.module is not None and not r._stopped]
+
+
 def _downstream(module):
-    from .modules import Buffer
+    """The single module a segment continues into.  An Fft reading the same buffer is a tap,
+    not the continuation: ClientDemodulatorChain hangs its secondary FftChain on the Selector
+    output next to the demodulator (owrx/dsp.py:220-225)."""
+    from .modules import Buffer, Fft
     w = module.writer
     if not isinstance(w, Buffer):
         return None
-    readers = [r for r in w._readers if r.module is not None and not r._stopped]
+    readers = [m for m in _readers_of(w) if not isinstance(m, Fft)]
     if len(readers) != 1:
         return None
-    nxt = readers[0].module
+    nxt = readers[0]
     return nxt if nxt.fusable else None
+
+
+def _plan_fft(mods):
+    """FftChain shape at the start of `mods`: (params, modules used) or None."""
+    from . import modules as M
+    if not mods or not isinstance(mods[0], M.Fft):
+        return None
+    fft, i = mods[0], 1
+
+    def take(cls):
+        nonlocal i
+        if i < len(mods) and isinstance(mods[i], cls):
+            i += 1
+            return mods[i - 1]
+        return None
+
+    avg = take(M.LogAveragePower) or take(M.LogPower)
+    swap = take(M.FftSwap)
+    if avg is None or swap is None or fft.every_n_samples <= 0:
+        return None
+    if isinstance(avg, M.LogAveragePower) and avg.fft_size not in (0, fft.size):
+        return None
+    adp = take(M.FftAdpcm)
+    used = mods[:i]
+    if used[-1].writer is None:
+        return None
+    return (dict(fft_size=fft.size, hop=fft.every_n_samples,
+                 avg=avg.avg_number if isinstance(avg, M.LogAveragePower) else 1,
+                 add_db=avg.add_db, adpcm=adp is not None), used)
+
+
+def _secondary_fft(selector_last):
+    """An FftChain reading the Selector output buffer (the secondary FFT), or None."""
+    from . import modules as M
+    w = selector_last.writer
+    if not isinstance(w, M.Buffer):
+        return None
+    for m in _readers_of(w):
+        if isinstance(m, M.Fft) and not m._stopped:
+            got = _plan_fft(_walk(m))
+            if got is not None:
+                return got
+    return None
 
 
 def _walk(head):
@@ -101,21 +151,8 @@ def plan_segment(head):
         return None
 
     if isinstance(head, M.Fft):
-        fft = take(M.Fft)
-        avg = take(M.LogAveragePower) or take(M.LogPower)
-        swap = take(M.FftSwap)
-        if avg is None or swap is None or fft.every_n_samples <= 0:
-            return None
-        if isinstance(avg, M.LogAveragePower) and avg.fft_size not in (0, fft.size):
-            return None
-        adp = take(M.FftAdpcm)
-        used = mods[:i]
-        if used[-1].writer is None:
-            return None
-        return ("waterfall",
-                dict(fft_size=fft.size, hop=fft.every_n_samples,
-                     avg=avg.avg_number if isinstance(avg, M.LogAveragePower) else 1,
-                     add_db=avg.add_db, adpcm=adp is not None), used)
+        got = _plan_fft(mods)
+        return None if got is None else ("waterfall", got[0], got[1])
 
     if not isinstance(head, M.Shift):
         return None
@@ -134,6 +171,7 @@ def plan_segment(head):
     frac = take(M.FractionalDecimator)
     bp = take(M.Bandpass)
     sq = take(M.Squelch)
+    selector_last = mods[i - 1]
     fm = take(M.FmDemod)
     if fm is not None:
         lim = take(M.Limit)
@@ -178,6 +216,10 @@ def plan_segment(head):
         p.update(sq_length=sq.length, sq_decimation=sq.decimation, sq_hang=sq.hang_length,
                  sq_flush=sq.flush_length, sq_report=sq.report_interval, sq_level=sq.level,
                  power_writer=sq.power_writer)
+    sec = _secondary_fft(selector_last)
+    p["secondary_fft"] = sec[0] if sec is not None else None
+    p["secondary_modules"] = sec[1] if sec is not None else []
+    p["secondary_writer"] = sec[1][-1].writer if sec is not None else None
     return ("chain", p, used)
 
 
@@ -185,7 +227,7 @@ def chain_params_struct(p):
     from .. import _lib
     s = _lib.ChainParams()
     for k, v in p.items():
-        if k != "power_writer":
+        if k not in ("power_writer", "secondary_fft", "secondary_modules", "secondary_writer"):
             setattr(s, k, v)
     return s
 
@@ -228,6 +270,7 @@ class EngineDriver:
             new = plans.get(hid)
             if new is None or new[0] != kind or new[2] != mods or not _compatible(kind, p, new[1]):
                 self._absorb(mods, False)
+                self._absorb(p.get("secondary_modules", []), False)
                 obj.close()
                 del self.segments[hid]
         for hid, (kind, p, mods) in plans.items():
@@ -239,8 +282,11 @@ class EngineDriver:
                                             p["add_db"], p["adpcm"])
             else:
                 obj = self.engine.chain(chain_params_struct(p))
+                if p.get("secondary_fft") is not None:
+                    _apply_secondary(obj, p["secondary_fft"])
             self.segments[hid] = (kind, p, mods, obj)
             self._absorb(mods, True)
+            self._absorb(p.get("secondary_modules", []), True)
 
     def _absorb(self, mods, on):
         for m in mods:
@@ -262,6 +308,12 @@ class EngineDriver:
                     obj.set_bandpass(None, None)
             if old.get("sq_level") != p.get("sq_level"):
                 obj.set_squelch_level(p["sq_level"])
+            if old.get("secondary_fft") != p.get("secondary_fft"):
+                _apply_secondary(obj, p.get("secondary_fft"))
+            olds, news = old.get("secondary_modules", []), p.get("secondary_modules", [])
+            if olds != news:
+                self._absorb([m for m in olds if m not in news], False)
+                self._absorb(news, True)
         self.segments[hid] = (kind, p, mods, obj)
 
     def _drain(self):
@@ -279,6 +331,11 @@ class EngineDriver:
                 pw = p.get("power_writer")
                 if sm.size and pw is not None:
                     pw.write(sm.astype(np.float32).tobytes())
+                sw = p.get("secondary_writer")
+                if p.get("secondary_fft") and sw is not None:
+                    rows = obj.read_secondary_fft()
+                    if rows.size:
+                        sw.write(rows.tobytes())
 
     def close(self):
         """Stop reading the source; the thread pushes what it holds, syncs and drains."""
@@ -326,6 +383,13 @@ def finish(source):
     if drv is not None:
         drv.close()
     return drv
+
+
+def _apply_secondary(obj, sf):
+    if sf is None:
+        obj.set_secondary_fft(0)
+    else:
+        obj.set_secondary_fft(sf["fft_size"], sf["hop"], sf["avg"], sf["add_db"], sf["adpcm"])
 
 
 def _compatible(kind, old, new):

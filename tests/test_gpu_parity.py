@@ -402,3 +402,47 @@ def test_c4_chains_61msps(amd):
     eng, chains = _run_chains(amd, iq, fs, plist, 1 << 19)
     _check_sampled_chains(iq, plist, chains, range(3))
     eng.close()
+
+
+@pytest.mark.parametrize("avg", [1, 3])
+def test_secondary_fft_rows(amd, avg):
+    """Secondary FFT (owrx/dsp.py:220-225): FftChain(12000, 2048, ...) on the Selector output.
+    Float rows vs the oracle's waterfall of the chain's own squelch output (debug tap 3), and the
+    ADPCM rows of an identical chain bit-exact against oracle.fft_adpcm_row of those rows."""
+    from openwebrx_amd import synth
+    fs, N = 2400000, 2048
+    a0, hop = amd.params.fft_parameters(12000, N, 9, 0.3)
+    assert (a0, hop) == (1, 1333)  # the reference's digimodes defaults
+    if avg != 1:
+        hop = 444
+    iq, offs = synth.make_iq(fs, (1 << 21) + 12345, ["usb"])
+    p = amd.params.chain_params(fs, offs[0], "usb", output=amd._lib.OUT_S16)
+    eng = amd.Engine(fs, max_block=1 << 18)
+    eng.set_debug(True)
+    cf, ca = eng.chain(p), eng.chain(p)
+    cf.set_secondary_fft(N, hop, avg, -70.0, adpcm=False)
+    ca.set_secondary_fft(N, hop, avg, -70.0, adpcm=True)
+    for i, s in enumerate(range(0, iq.size, 77777)):
+        eng.push(iq[s:s + 77777])
+    eng.sync()
+    rows = cf.read_secondary_fft()
+    rows_a = ca.read_secondary_fft()
+    sq = cf.read_debug(3)
+    ref = np.stack([oracle.fftswap(r) for r in oracle.waterfall_rows(sq, N, hop, avg)])
+    assert rows.shape[0] >= 5 and rows.shape == ref.shape, (rows.shape, ref.shape)
+    # the Selector output is band-limited (USB 150..3000 Hz of 12 kHz): stop-band bins sit
+    # ~80 dB under the peak, where fp32 FFT rounding (relative to the row's energy) shows in dB.
+    # Bar: linear power rel-RMS <= 1e-5 per row, and <= 2e-3 dB on bins within 50 dB of the peak
+    for g, r in zip(rows, ref):
+        assert rel_rms(10.0 ** (g / 10.0), 10.0 ** (r / 10.0)) < 1e-5
+        strong = r > r.max() - 50.0
+        assert np.max(np.abs(g - r)[strong]) < 2e-3
+    assert rows_a.shape == (rows.shape[0], (N + 10) // 2)
+    for r in range(rows.shape[0]):
+        assert rows_a[r].tobytes() == oracle.fft_adpcm_row(rows[r])
+    # removing it stops the rows; the audio is untouched by the tap
+    ca.set_secondary_fft(0)
+    eng.push(iq[:1 << 18])
+    eng.sync()
+    assert cf.read_audio() == ca.read_audio()
+    eng.close()

@@ -188,6 +188,28 @@ def test_planner_waterfall_and_rewire():
     _graph.finish(wide)
 
 
+def test_planner_secondary_fft_tap():
+    """ClientDemodulatorChain with a secondary FftChain on the Selector output buffer
+    (owrx/dsp.py:220-225): the chain still fuses and carries the FftChain parameters."""
+    fs, off = 2400000, 50000
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    sel = selector(fs, off, "usb")
+    mods = sel + demodulator("usb") + client_audio()
+    ch = Chain(mods)
+    ch.setWriter(M.Buffer(Format.CHAR))
+    ch.setReader(wide.getReader())
+    avg, hop = params.fft_parameters(12000, 2048, 9, 0.3)
+    fmods = fft_chain(2048, hop, avg)
+    Chain(fmods)
+    fmods[-1].setWriter(M.Buffer(Format.CHAR))
+    fmods[0].setReader(sel[-1].writer.getReader())
+    kind, p, used = _graph.plan_segment(mods[0])
+    assert kind == "chain" and used == mods
+    assert p["secondary_fft"] == dict(fft_size=2048, hop=1333, avg=1, add_db=-70.0, adpcm=True)
+    assert p["secondary_modules"] == fmods
+    _graph.finish(wide)
+
+
 def test_unrecognised_graph_is_not_fused():
     wide = M.Buffer(Format.COMPLEX_FLOAT)
     shift = M.Shift(0.1)
@@ -231,6 +253,14 @@ def test_pycsdr_graph_equals_engine():
         ch.setWriter(out)
         ch.setReader(wide.getReader())
         graphs.append(mods)
+    # secondary FftChain on the first chain's Selector output (owrx/dsp.py:220-225)
+    sel_out = [m for m in graphs[0] if isinstance(m, M.Squelch)][0].writer
+    smods = fft_chain(2048, 1333, 1)
+    Chain(smods)
+    sfout = M.Buffer(Format.CHAR, size=1 << 22)
+    sfcol = _collect(sfout)
+    smods[-1].setWriter(sfout)
+    smods[0].setReader(sel_out.getReader())
     wmods = fft_chain(4096, hop, avg)
     wch = Chain(wmods)
     wout = M.Buffer(Format.CHAR, size=1 << 22)
@@ -247,7 +277,7 @@ def test_pycsdr_graph_equals_engine():
     while _graph._drivers.get(id(wide)).reader.available() > 0:
         time.sleep(0.01)
     _graph.finish(wide)
-    for col in outs + smeters + [wcol]:
+    for col in outs + smeters + [wcol, sfcol]:
         col[0].stop()
         col[1].join(5)
 
@@ -255,6 +285,7 @@ def test_pycsdr_graph_equals_engine():
     ref_ch = [eng.chain(params.chain_params(fs, o, m, output=_lib.OUT_ADPCM))
               for o, m in zip(offs, modes)]
     wf = eng.waterfall(4096, hop, avg, -70.0, True)
+    ref_ch[0].set_secondary_fft(2048, 1333, 1, -70.0, True)
     for j in range(0, iq.size, _graph.BLOCK):
         eng.push(iq[j:j + _graph.BLOCK])
     eng.sync()
@@ -263,6 +294,8 @@ def test_pycsdr_graph_equals_engine():
         sm = np.frombuffer(b"".join(smeters[k][2]), np.float32)
         np.testing.assert_array_equal(sm, c.read_smeter())
     assert b"".join(wcol[2]) == wf.read()
+    sf = b"".join(sfcol[2])
+    assert len(sf) >= 2 * 1029 and sf == ref_ch[0].read_secondary_fft().tobytes()
     eng.close()
 
 
