@@ -36,6 +36,10 @@ extern "C" {
 #define OWRX_DEMOD_NFM 0
 #define OWRX_DEMOD_AM 1
 #define OWRX_DEMOD_SSB 2    /* RealPart: usb / lsb / cw (owrx/dsp.py:617-619) */
+#define OWRX_DEMOD_WFM 3    /* WFm (csdr/chain/analog.py:55-116): FmDemod, Limit,
+                               FractionalDecimator(FLOAT, IF/audio_rate, prefilter=True),
+                               WfmDeemphasis(audio_rate, deemph_tau); no AGC.  The Selector
+                               runs at the fixed 250 kHz IF (analog.py:81-82). */
 
 #define OWRX_OUT_S16 0      /* Convert(FLOAT, SHORT) */
 #define OWRX_OUT_ADPCM 1    /* Convert + AdpcmEncoder(sync=True) */
@@ -125,6 +129,10 @@ typedef struct {
     float   agc_max_gain;    /* < 0 => profile default; NFm: 3 (analog.py:40) */
     int32_t audio_rate;      /* NfmDeemphasis(sampleRate) (analog.py:45) */
     int32_t output;          /* OWRX_OUT_* */
+    float   deemph_tau;      /* WFM: WfmDeemphasis tau (wfm_deemphasis_tau, default 50e-6,
+                                owrx/config/defaults.py:21); 0 => 50e-6 */
+    double  if_rate;         /* WFM: the Selector output rate (250000); audio_rate is the HD
+                                output rate (48000, owrx/dsp.py:494) */
 } owrx_chain_params;
 
 int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle);

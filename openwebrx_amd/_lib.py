@@ -19,7 +19,7 @@ OWRX_EINVAL = -22
 OWRX_ENOSPC = -28
 OWRX_ENODEV = -19
 
-DEMOD_NFM, DEMOD_AM, DEMOD_SSB = 0, 1, 2
+DEMOD_NFM, DEMOD_AM, DEMOD_SSB, DEMOD_WFM = 0, 1, 2, 3
 OUT_S16, OUT_ADPCM, OUT_F32, OUT_IQ = 0, 1, 2, 3
 AGC_FAST, AGC_SLOW, AGC_MID, AGC_LAGGY = 0, 1, 2, 3
 
@@ -61,6 +61,8 @@ class ChainParams(ctypes.Structure):
         ("agc_max_gain", ctypes.c_float),
         ("audio_rate", ctypes.c_int32),
         ("output", ctypes.c_int32),
+        ("deemph_tau", ctypes.c_float),
+        ("if_rate", ctypes.c_double),
     ]
 
 

@@ -57,6 +57,8 @@ int ddc_segments(int D, int nseg, int P, int nchains);
 int ddc_blocks_per_cu(int P, int nchains);
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
                                 hipStream_t st);
+hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const int* idx,
+                            int nlong, int64_t max_fd, int max_taps, hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, int output, int debug, hipStream_t st);
 hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, ChainCounts* counts,
@@ -67,6 +69,7 @@ hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const
 constexpr int kWfFramesPerGroup = 1;  // the four-step FFT (N > kWfLdsMaxN) relies on it
 constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
 constexpr int kWfMaxN = 65536;
+constexpr int kBlMaxTaps = 4095;       // longest bandpass of the bp_long path (kernels_post.hip)
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
 constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
@@ -215,6 +218,13 @@ struct Chain {
     int16_t* d_s16[kSlots] = {};  // ADPCM encoder input, per slot (B -> C)
     float2* d_bp_taps = nullptr;
     int bp_ntaps = 0;
+    int bp_hist = kBpHist;      // fd_buf history; > kBpHist => long bandpass (bp_long kernel)
+    int bp_design_taps = 0;     // taps of the chain's bandpass design (bp_transition)
+    // WFM audio decimator (OWRX_DEMOD_WFM)
+    float* d_wf = nullptr;
+    float* d_pf = nullptr;
+    float* d_pf_taps = nullptr;
+    int pf_ntaps = 0;
     int64_t cap = 0;      // per-step sample capacity of stage buffers
     int64_t out_cap = 0;  // staging bytes per step
     int sm_cap = 0;
@@ -241,8 +251,9 @@ struct Slot {  // one block's outputs in flight on streams B / C
     bool debug = false;
     ChainPost* d_posts = nullptr;
     ChainPost* h_posts = nullptr;
-    int* d_sel = nullptr;   // post indices grouped by output mode
+    int* d_sel = nullptr;   // post indices grouped by output mode, then long-bandpass posts
     int* h_sel = nullptr;
+    int long_off = 0;
     ChainCounts* d_counts = nullptr;
     ChainCounts* h_counts = nullptr;
     uint8_t* d_out = nullptr;
@@ -355,6 +366,9 @@ static void free_chain(Chain* c) {
     for (int i = 0; i < kSlots; ++i) dfree(c->d_dem[i]);
     for (int i = 0; i < kSlots; ++i) dfree(c->d_s16[i]);
     dfree(c->d_bp_taps);
+    dfree(c->d_wf);
+    dfree(c->d_pf);
+    dfree(c->d_pf_taps);
     dfree(c->d_sf);
     dfree(c->d_sf_acc);
     dfree(c->d_sf_window);
@@ -429,8 +443,8 @@ static int drain_slot(owrx_engine* e, int si) {
                            sizeof(float) * (size_t)std::min<int64_t>(cc.smeter, e->sm_stride));
             if (s.debug && s.h_dbg) {
                 const uint8_t* base = s.h_dbg + (int64_t)k * kDebugStages * e->dbg_stride;
-                const int64_t cnt[kDebugStages] = {cc.n_ddc, cc.n_fd, cc.n_bp,
-                                                   cc.n_sq,  cc.n_sq, cc.n_sq};
+                const int64_t cnt[kDebugStages] = {cc.n_ddc,  cc.n_fd, cc.n_bp,
+                                                   cc.n_gate, cc.n_sq, cc.n_sq};
                 const int64_t isz[kDebugStages] = {8, 8, 8, 8, 4, 4};
                 for (int st = 0; st < kDebugStages; ++st) {
                     const int64_t bytes = std::min(cnt[st] * isz[st], e->dbg_stride);
@@ -557,7 +571,8 @@ static int ensure_post_capacity(owrx_engine* e) {
     for (auto& kv : e->chains) {
         need_out += out_region(kv.second->out_cap) + out_region(kv.second->sf_out_cap);
         need_sm = std::max<int64_t>(need_sm, kv.second->sm_cap);
-        need_dbg = std::max<int64_t>(need_dbg, kv.second->cap * 8 + 64);
+        // squelch / demod taps hold up to cap + sq_length samples per step
+        need_dbg = std::max<int64_t>(need_dbg, (kv.second->cap + kv.second->prm.sq_length + 16) * 8 + 64);
     }
     if (n <= e->post_cap && need_out <= e->out_total && need_sm <= e->sm_stride &&
         (!e->debug || need_dbg <= e->dbg_stride))
@@ -573,8 +588,9 @@ static int ensure_post_capacity(owrx_engine* e) {
         free_slot_staging(s);
         HIPCHK(dalloc(&s.d_posts, cap));
         HIPCHK(halloc(&s.h_posts, cap));
-        HIPCHK(dalloc(&s.d_sel, (size_t)cap + 64 * 3 * 4));  // + demodulator-run padding
-        HIPCHK(halloc(&s.h_sel, (size_t)cap + 64 * 3 * 4));
+        // serial lane lists (+ demodulator-run padding), then the long-bandpass post list
+        HIPCHK(dalloc(&s.d_sel, (size_t)2 * cap + 64 * 4 * 4));
+        HIPCHK(halloc(&s.h_sel, (size_t)2 * cap + 64 * 4 * 4));
         HIPCHK(dalloc(&s.d_counts, cap));
         HIPCHK(dalloc(&s.d_out, (size_t)e->out_total));
         HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
@@ -844,6 +860,19 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.sq_report = q.sq_report;
             p.sq_level = q.sq_level;
             p.deemph_alpha = nfm_deemphasis_alpha(q.audio_rate);
+            p.bp_hist = c->bp_hist;
+            p.bp_long = c->bp_hist > kBpHist ? 1 : 0;
+            if (q.demod == OWRX_DEMOD_WFM) {
+                // WfmDeemphasis(rate, tau): y += dt/(tau+dt) * (x - y) (csdr deemphasis_wfm_ff)
+                const double dt = 1.0 / (double)q.audio_rate;
+                const double tau = q.deemph_tau > 0 ? (double)q.deemph_tau : 50e-6;
+                p.deemph_alpha = (float)(dt / (tau + dt));
+                p.wfm_rate = q.if_rate / (double)q.audio_rate;
+                p.pf_taps = c->d_pf_taps;
+                p.pf_ntaps = c->pf_ntaps;
+                p.wf_buf = c->d_wf;
+                p.pf_buf = c->d_pf;
+            }
             p.deemph_beta = 1.0f - p.deemph_alpha;
             p.agc = agc_profile(q.agc_profile);
             if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
@@ -907,10 +936,26 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     if (np > 0) {
         // stream A: post_parallel (wide); stream B: post_serial_front (serial, own CUs)
         memcpy(S.h_posts, e->posts.data(), sizeof(ChainPost) * np);
+        // long-bandpass chains (indices after the serial lane lists in the sel buffer)
+        int nlong = 0, long_taps = 0;
+        int64_t long_fd = 0;
+        S.long_off = e->post_cap + 64 * 4 * 4;
+        for (int i = 0; i < np; ++i)
+            if (e->posts[i].bp_long && e->posts[i].output != OWRX_OUT_IQ) {
+                S.h_sel[S.long_off + nlong++] = i;
+                long_taps = std::max(long_taps, e->posts[i].bp_ntaps);
+                long_fd = std::max<int64_t>(long_fd, e->chains[S.post_ids[i]]->cap);
+            }
         HIPCHK(hipMemcpyAsync(S.d_posts, S.h_posts, sizeof(ChainPost) * np,
                               hipMemcpyHostToDevice, e->sA));
         if (timed) HIPCHK(hipEventRecord(S.b0, e->sA));
         HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
+        if (nlong > 0) {  // long bandpass chains: bp_long + post_tail (after post_parallel)
+            HIPCHK(hipMemcpyAsync(S.d_sel + S.long_off, S.h_sel + S.long_off, sizeof(int) * nlong,
+                                  hipMemcpyHostToDevice, e->sA));
+            HIPCHK(launch_post_long(S.d_posts, S.d_counts, S.d_sel + S.long_off, nlong, long_fd,
+                                    long_taps, e->sA));
+        }
         for (int lg = 0; lg < 32; ++lg)
             if (sf_sizes & (1u << lg)) HIPCHK(launch_chain_sfft(lg, S.d_posts, np, S.d_counts, e->sA));
         HIPCHK(hipEventRecord(S.evA, e->sA));
@@ -1351,9 +1396,11 @@ static int chain_validate(const owrx_chain_params* p) {
         return (p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate != 1.0)
                    ? OWRX_EINVAL : OWRX_OK;
     if (!p || p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate <= 0 ||
-        p->sq_length <= 0 || p->sq_length > 3072 || p->sq_decimation <= 0 || p->demod < 0 ||
-        p->demod > 2 || p->output < 0 || p->output > 2 || p->audio_rate <= 0 ||
+        p->sq_length <= 0 || p->sq_length > (1 << 20) || p->sq_decimation <= 0 || p->demod < 0 ||
+        p->demod > OWRX_DEMOD_WFM || p->output < 0 || p->output > 2 || p->audio_rate <= 0 ||
         p->agc_profile < 0 || p->agc_profile > 3)
+        return OWRX_EINVAL;
+    if (p->demod == OWRX_DEMOD_WFM && (p->if_rate <= 0 || p->if_rate / p->audio_rate < 1.0))
         return OWRX_EINVAL;
     if (p->bandpass && (p->bp_transition <= 0 || p->bp_low >= p->bp_high)) return OWRX_EINVAL;
     return OWRX_OK;
@@ -1362,13 +1409,14 @@ static int chain_validate(const owrx_chain_params* p) {
 static int chain_set_bandpass_taps(owrx_engine* e, Chain* c) {
     if (!c->prm.bandpass) return OWRX_OK;
     const int T = firdes_filter_len(c->prm.bp_transition);
-    if (T > kBpHist + 1) {
-        set_last_error("bandpass transition too narrow (%d taps > %d)", T, kBpHist + 1);
+    if (T > c->bp_hist + 1 || T > kBlMaxTaps) {
+        set_last_error("bandpass transition too narrow (%d taps > %d)", T,
+                       std::min(c->bp_hist + 1, kBlMaxTaps));
         return OWRX_EINVAL;
     }
     std::vector<float> taps = firdes_bandpass_c(T, c->prm.bp_low, c->prm.bp_high);
     RCCHK(drain_all(e));
-    if (!c->d_bp_taps) HIPCHK(dalloc(&c->d_bp_taps, (size_t)kBpHist + 1));
+    if (!c->d_bp_taps) HIPCHK(dalloc(&c->d_bp_taps, (size_t)c->bp_hist + 1));
     HIPCHK(hipMemcpy(c->d_bp_taps, taps.data(), sizeof(float) * 2 * T, hipMemcpyHostToDevice));
     c->bp_ntaps = T;
     return OWRX_OK;
@@ -1439,6 +1487,21 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     c->out_cap = p->output == OWRX_OUT_IQ ? 8 * c->cap + 64
                                           : 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
     c->sm_cap = p->output == OWRX_OUT_IQ ? 4 : (int)(scap / p->sq_length + 4);
+    if (p->output != OWRX_OUT_IQ && scap / p->sq_length + 2 > 1024) {  // kMaxSqBlocks
+        set_last_error("owrx_chain_create: squelch length %d too short for the block size",
+                       p->sq_length);
+        return OWRX_EINVAL;
+    }
+    // a bandpass design longer than the in-kernel FIR's history runs in bp_long (WFM)
+    if (p->bp_transition > 0 && p->output != OWRX_OUT_IQ) {
+        c->bp_design_taps = firdes_filter_len(p->bp_transition);
+        if (c->bp_design_taps > kBlMaxTaps) {
+            set_last_error("owrx_chain_create: bandpass of %d taps > %d", c->bp_design_taps,
+                           kBlMaxTaps);
+            return OWRX_EINVAL;
+        }
+        if (c->bp_design_taps - 1 > kBpHist) c->bp_hist = (c->bp_design_taps - 1 + 255) & ~255;
+    }
     ChainStateP ps;
     memset(&ps, 0, sizeof(ps));
     ChainStateS ss;
@@ -1451,7 +1514,19 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     HIPCHK(hipMemcpy(c->d_pstate, &ps, sizeof(ps), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_sstate, &ss, sizeof(ss), hipMemcpyHostToDevice));
     HIPCHK(dalloc(&c->d_ddc, (size_t)(kFdHist + c->cap)));
-    HIPCHK(dalloc(&c->d_fd, (size_t)(kBpHist + c->cap)));
+    HIPCHK(dalloc(&c->d_fd, (size_t)(c->bp_hist + c->cap)));
+    if (p->demod == OWRX_DEMOD_WFM && p->output != OWRX_OUT_IQ) {
+        // FractionalDecimator(FLOAT, if_rate / audio_rate, prefilter=True): prefilter lowpass
+        // at 0.5 / rate (output Nyquist), transition 0.03 (csdr's default; recalled, unpinned)
+        const double r = p->if_rate / (double)p->audio_rate;
+        c->pf_ntaps = firdes_filter_len(0.03f);
+        std::vector<float> pf = firdes_lowpass(c->pf_ntaps, 0.5 / r);
+        HIPCHK(dalloc(&c->d_pf_taps, (size_t)c->pf_ntaps));
+        HIPCHK(hipMemcpy(c->d_pf_taps, pf.data(), sizeof(float) * pf.size(),
+                         hipMemcpyHostToDevice));
+        HIPCHK(dalloc(&c->d_wf, (size_t)(kWfHist + scap)));
+        HIPCHK(dalloc(&c->d_pf, (size_t)(kWfHist + scap)));
+    }
     HIPCHK(dalloc(&c->d_sq, (size_t)scap));
     // slack: the serial kernels read whole 64-sample chunks / 8-sample prefetches unguarded
     for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_dem[i], (size_t)scap + 160));

@@ -14,6 +14,7 @@
 //   cost about one chain.
 // chain_adpcm (stream C, one LANE per chain): AdpcmEncoder(sync=True).  Streams B and C run
 //   concurrently with the next blocks' stream-A work.
+#include <algorithm>
 #include <climits>
 #include <type_traits>
 
@@ -35,11 +36,106 @@ OWRX_DEV float lagrange_den(int i) {
     return ((11 - i) & 1) ? -1.0f / d : 1.0f / d;
 }
 
-__global__ void __launch_bounds__(kPostThreads)
-post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts) {
-    const ChainPost P = posts[blockIdx.x];
+// chunked in-place move dst[0, n) = src[0, n) with src = dst + off, off >= 0: every chunk's
+// reads precede its writes, and later chunks read at or beyond off + base + NT, past every index
+// written before them
+template <typename T, typename PTR>
+OWRX_DEV void move_front(PTR buf, int64_t off, int n) {
+    const int tid = threadIdx.x;
+    for (int base = 0; base < n; base += kPostThreads) {
+        const int i = base + tid;
+        T v{};
+        if (i < n) v = buf[off + i];
+        __syncthreads();
+        if (i < n) buf[i] = v;
+    }
+    __syncthreads();
+}
+
+// WFM audio: FractionalDecimator(FLOAT, IF/audio, prefilter=True) (csdr/chain/analog.py:69)
+// on the FmDemod + Limit output the block appended at wf_buf[kWfHist, +nsq): a causal lowpass
+// prefilter, then the 12-point Lagrange interpolator of the Selector's FractionalDecimator at
+// positions 6 + k * rate.  Writes the audio-rate samples to `dem` (the serial kernels' input)
+// and returns their count.
+OWRX_DEV int wfm_audio(const ChainPost& P, ChainStateP& S, int nsq) {
     const int tid = threadIdx.x;
     constexpr int NT = kPostThreads;
+    static_assert(kWfHist == NT, "history moves assume one sample per thread");
+    __shared__ float sh_pf[kWfHist];
+    __shared__ int sh_n;
+    const auto wf = gp(P.wf_buf);
+    const auto pf = gp(P.pf_buf);
+    const auto dem = gp(P.dem);
+    const int nt = P.pf_ntaps;
+    for (int t = tid; t < nt; t += NT) sh_pf[t] = P.pf_taps[t];
+    __syncthreads();
+    for (int i = tid; i < nsq; i += NT) {
+        const auto x = wf + (kWfHist + i);
+        float acc = 0.0f;
+        for (int t = 0; t < nt; ++t) acc = fmaf(sh_pf[t], x[-t], acc);
+        pf[kWfHist + i] = acc;
+    }
+    const int64_t total = S.wf_count + nsq;
+    const double r = P.wfm_rate;
+    if (tid == 0) {
+        auto valid = [&](int64_t k) { return (int64_t)ceil(6.0 + (double)k * r) + 5 < total; };
+        int64_t ke = (int64_t)floor(((double)total - 12.0) / r);
+        if (ke < S.wf_next) ke = S.wf_next;
+        while (valid(ke)) ++ke;
+        while (ke > S.wf_next && !valid(ke - 1)) --ke;
+        sh_n = (int)(ke - S.wf_next);
+    }
+    __syncthreads();
+    const int n = sh_n;
+    const int64_t base = S.wf_count - kWfHist;  // absolute IF index of pf[0]
+    for (int j = tid; j < n; j += NT) {
+        const int64_t k = S.wf_next + j;
+        const double w = 6.0 + (double)k * r;
+        const int64_t hi = (int64_t)ceil(w);
+        const int64_t lo = hi - 6;
+        const float u = (float)((w - (double)lo) - 5.5);
+        float d[kFdPoints], pre[kFdPoints], suf[kFdPoints];
+#pragma unroll
+        for (int i = 0; i < kFdPoints; ++i) d[i] = u - ((float)i - 5.5f);
+        pre[0] = 1.0f;
+#pragma unroll
+        for (int i = 1; i < kFdPoints; ++i) pre[i] = pre[i - 1] * d[i - 1];
+        suf[kFdPoints - 1] = 1.0f;
+#pragma unroll
+        for (int i = kFdPoints - 2; i >= 0; --i) suf[i] = suf[i + 1] * d[i + 1];
+        const auto x = pf + (lo - base);
+        float acc = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kFdPoints; ++i) acc = fmaf(pre[i] * suf[i] * lagrange_den(i), x[i], acc);
+        dem[j] = acc;
+    }
+    __syncthreads();
+    {   // keep the last kWfHist IF samples of both streams
+        const float a = wf[nsq + tid], b = pf[nsq + tid];
+        __syncthreads();
+        wf[tid] = a;
+        pf[tid] = b;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        S.wf_count = total;
+        S.wf_next += n;
+    }
+    __syncthreads();
+    return n;
+}
+
+// One chain-block after the DDC: sections 0-1 (segment reduce, FractionalDecimator), 2
+// (Bandpass), 3 (Squelch), 4 (demodulator front; WFM: prefilter + Lagrange to the audio rate).
+// PHASE 0 runs a chain whole, except that a chain with a long bandpass (bp_long: WFM's
+// 3125-tap complex FIR at 250 kHz) stops after section 1; bp_long then filters it across many
+// workgroups and PHASE 2 (post_tail) runs sections 3-4.
+template <int PHASE>
+OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
+    const ChainPost P = Pin;
+    const int tid = threadIdx.x;
+    constexpr int NT = kPostThreads;
+    const int H = P.bp_hist;  // fd_buf[0, H) = bandpass history
 
     __shared__ ChainStateP S;
     __shared__ int sh_n_fd;
@@ -57,34 +153,14 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
     const auto smeter = gp(P.smeter);
     if (tid == 0) S = *P.pstate;
     __syncthreads();
-    // secondary FFT input: drop the samples chain_sfft has consumed (keep [sf_next, sf_fill))
-    int sf_fill = 0;
-    if (P.sf_n > 0) {
-        const auto sf = gp(P.sf_buf);
-        const int next = P.sf_reset ? 0 : S.sf_next;
-        const int keep = P.sf_reset ? 0 : S.sf_fill - next;
-        // chunked move through registers: a chunk's reads all precede its writes, and later
-        // chunks read at or beyond next + base + NT >= every index written before them
-        for (int base = 0; base < keep; base += NT) {
-            const int i = base + tid;
-            float2 v = make_float2(0.0f, 0.0f);
-            if (i < keep) v = sf[next + i];
-            __syncthreads();
-            if (i < keep) sf[i] = v;
-        }
-        sf_fill = keep > 0 ? keep : 0;
-        __syncthreads();
-        if (tid == 0) {
-            S.sf_fill = sf_fill;
-            S.sf_next = keep > 0 ? 0 : -keep;  // hop > N: the next frame starts past the data
-            if (P.sf_reset) S.sf_row_frame = 0;
-        }
-    }
+    int n_new, n_fd;
+    int64_t ddc_total;
+    if constexpr (PHASE == 0) {
 
     // ---- 0. FirDecimate output: fixed-order sum of the phase-segment partials ----------
     const int64_t kb = P.k_begin > P.k_first ? P.k_begin : P.k_first;
     const int64_t nn = P.k_begin + P.nk - kb;
-    const int n_new = nn > 0 ? (int)nn : 0;
+    n_new = nn > 0 ? (int)nn : 0;
     const int col0 = (int)(kb - P.k_begin);
     {   // segment partials: 8 independent loads in flight per thread, summed in segment order
         const int64_t sstride = (int64_t)P.group_chains * P.nk;
@@ -120,17 +196,17 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         if (tid == 0) {
             S.ddc_count += n_new;
             *P.pstate = S;
-            ChainCounts& c = counts[blockIdx.x];
+            ChainCounts& c = cnt;
             c.out_bytes = (int64_t)n_new * 8;
             c.smeter = 0;
             c.n_ddc = n_new;
-            c.n_fd = c.n_bp = c.n_sq = 0;
+            c.n_fd = c.n_bp = c.n_sq = c.n_gate = 0;
         }
         return;
     }
     __syncthreads();
     const int64_t ddc_base = S.ddc_count - kFdHist;  // local index of ddc_buf[0]
-    const int64_t ddc_total = S.ddc_count + n_new;
+    ddc_total = S.ddc_count + n_new;
 
     // ---- 1. FractionalDecimator ------------------------------------------------------------
     if (P.frac_enabled) {
@@ -173,31 +249,62 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
                 acc.x = fmaf(L, xi.x, acc.x);
                 acc.y = fmaf(L, xi.y, acc.y);
             }
-            fd_buf[kBpHist + j] = acc;
+            fd_buf[H + j] = acc;
         }
     } else {
         if (tid == 0) sh_n_fd = n_new;
-        for (int j = tid; j < n_new; j += NT) fd_buf[kBpHist + j] = ddc_buf[kFdHist + j];
+        for (int j = tid; j < n_new; j += NT) fd_buf[H + j] = ddc_buf[kFdHist + j];
     }
     __syncthreads();
-    const int n_fd = sh_n_fd;
+    n_fd = sh_n_fd;
     {   // keep the last kFdHist DDC outputs as interpolator history
         float2 t = make_float2(0.0f, 0.0f);
         if (tid < kFdHist) t = ddc_buf[n_new + tid];
         __syncthreads();
         if (tid < kFdHist) ddc_buf[tid] = t;
     }
+    if (P.bp_long) {  // the bandpass and everything after it run in bp_long / post_tail
+        if (tid == 0) {
+            S.ddc_count = ddc_total;
+            if (P.frac_enabled) S.fd_next += n_fd;
+            S.fd_count += n_fd;
+            *P.pstate = S;
+            cnt.n_ddc = n_new;
+            cnt.n_fd = n_fd;
+            cnt.n_bp = n_fd;
+        }
+        return;
+    }
+    } else {  // PHASE 2: sections 0-1 ran in post_parallel, section 2 in bp_long
+        n_new = (int)cnt.n_ddc;
+        n_fd = (int)cnt.n_fd;
+        ddc_total = S.ddc_count;
+    }
+    // secondary FFT input: drop the samples chain_sfft has consumed (keep [sf_next, sf_fill))
+    int sf_fill = 0;
+    if (P.sf_n > 0) {
+        const int next = P.sf_reset ? 0 : S.sf_next;
+        const int keep = P.sf_reset ? 0 : S.sf_fill - next;
+        __syncthreads();
+        move_front<float2>(gp(P.sf_buf), next, keep);
+        sf_fill = keep > 0 ? keep : 0;
+        if (tid == 0) {
+            S.sf_fill = sf_fill;
+            S.sf_next = keep > 0 ? 0 : -keep;  // hop > N: the next frame starts past the data
+            if (P.sf_reset) S.sf_row_frame = 0;
+        }
+    }
 
     // ---- 2. Bandpass (inputs + taps staged in LDS when they fit) ------------------------
     const int pend = S.sq_pending;
     const int nbt = P.bp_ntaps;
-    const bool lds_bp = nbt > 0 && (kBpHist + n_fd) <= kBpLds;
+    const bool lds_bp = !P.bp_long && nbt > 0 && (kBpHist + n_fd) <= kBpLds;
     if (lds_bp) {
         for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[j] = fd_buf[j];
         for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
         __syncthreads();
     }
-    for (int j = tid; j < n_fd; j += NT) {
+    for (int j = tid; j < (P.bp_long ? 0 : n_fd); j += NT) {
         const auto x = fd_buf + kBpHist + j;
         float2 y;
         if (lds_bp) {
@@ -247,7 +354,9 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         }
     }
     __syncthreads();
-    {   // keep the last kBpHist bandpass inputs
+    if (P.bp_long) {  // keep the last H bandpass inputs
+        move_front<float2>(fd_buf, n_fd, H);
+    } else {  // keep the last kBpHist bandpass inputs
         const float2 t = fd_buf[n_fd + tid];  // kBpHist == NT
         __syncthreads();
         fd_buf[tid] = t;
@@ -295,7 +404,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
             }
             sh_pass[b] = (uint8_t)pass;
         }
-        counts[blockIdx.x].smeter = ns < P.smeter_cap ? ns : P.smeter_cap;
+        cnt.smeter = ns < P.smeter_cap ? ns : P.smeter_cap;
     }
     __syncthreads();
 
@@ -307,7 +416,7 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
         if (P.sf_n > 0) P.sf_buf[sf_fill + i] = x;  // Selector output -> secondary FFT
         float v;
-        if (P.demod == 0) {
+        if (P.demod == 0 || P.demod == 3) {
             float2 prev = fm_prev0;
             if (i > 0) prev = sh_pass[(i - 1) / L] ? sq_buf[i - 1] : make_float2(0.0f, 0.0f);
             v = limit_step(fm_step(x, prev), 1.0f);
@@ -316,39 +425,144 @@ post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ cou
         } else {
             v = x.x;
         }
-        dem[i] = v;
+        if (P.demod == 3)
+            P.wf_buf[kWfHist + i] = v;  // WFM: FmDemod + Limit at the IF rate
+        else
+            dem[i] = v;
     }
     __syncthreads();
+    int n_audio = nsq;
+    if (P.demod == 3) n_audio = wfm_audio(P, S, nsq);
     {   // move the incomplete squelch block to the front
         const int rem = total - nsq;
         float2 last = S.fm_last;
         if (nsq > 0) last = sh_pass[nb - 1] ? sq_buf[nsq - 1] : make_float2(0.0f, 0.0f);
-        float2 t[kMaxSqLen / NT];
+        if (P.sq_len > kMaxSqLen) {  // WFM: 15625-sample squelch blocks
+            __syncthreads();
+            move_front<float2>(sq_buf, nsq, rem);
+        } else {
+            float2 t[kMaxSqLen / NT];
 #pragma unroll
-        for (int m = 0; m < kMaxSqLen / NT; ++m) {
-            const int i = tid + m * NT;
-            if (i < rem) t[m] = sq_buf[nsq + i];
-        }
-        __syncthreads();
+            for (int m = 0; m < kMaxSqLen / NT; ++m) {
+                const int i = tid + m * NT;
+                if (i < rem) t[m] = sq_buf[nsq + i];
+            }
+            __syncthreads();
 #pragma unroll
-        for (int m = 0; m < kMaxSqLen / NT; ++m) {
-            const int i = tid + m * NT;
-            if (i < rem) sq_buf[i] = t[m];
+            for (int m = 0; m < kMaxSqLen / NT; ++m) {
+                const int i = tid + m * NT;
+                if (i < rem) sq_buf[i] = t[m];
+            }
         }
         if (tid == 0) {
             S.fm_last = last;
             S.sq_pending = rem;
-            S.ddc_count = ddc_total;
-            if (P.frac_enabled) S.fd_next += n_fd;
-            S.fd_count += n_fd;
+            if (PHASE == 0) {
+                S.ddc_count = ddc_total;
+                if (P.frac_enabled) S.fd_next += n_fd;
+                S.fd_count += n_fd;
+            }
             S.sq_blocks += nb;
             if (P.sf_n > 0) S.sf_fill = sf_fill + nsq;
             *P.pstate = S;
-            ChainCounts& c = counts[blockIdx.x];
+            ChainCounts& c = cnt;
             c.n_ddc = n_new;
             c.n_fd = n_fd;
             c.n_bp = n_fd;
-            c.n_sq = nsq;
+            c.n_sq = n_audio;
+            c.n_gate = nsq;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kPostThreads)
+post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts) {
+    post_body<0>(posts[blockIdx.x], counts[blockIdx.x]);
+}
+
+// sections 3-4 of the long-bandpass chains listed in idx (after bp_long)
+__global__ void __launch_bounds__(kPostThreads)
+post_tail(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
+          const int* __restrict__ idx) {
+    const int i = idx[blockIdx.x];
+    post_body<2>(posts[i], counts[i]);
+}
+
+// Bandpass(transition=320/IF, use_fft=True) (csdr/chain/selector.py:115-117) for chains whose
+// FIR is too long for the in-kernel path (WFM: 3125 complex taps at 250 kHz): grid (tiles,
+// chains); each workgroup stages the taps and its input window in LDS and computes kBlTile
+// outputs (two per thread) of y[j] = sum_t g[t] x[j - t] into the squelch input.
+constexpr int kBlTile = 512;
+constexpr int kBlMaxTaps = 4095;
+
+__global__ void __launch_bounds__(kPostThreads)
+bp_long(const ChainPost* __restrict__ posts, const ChainCounts* __restrict__ counts,
+        const int* __restrict__ idx) {
+    const int c = idx[blockIdx.y];
+    const ChainPost& P = posts[c];
+    const int n_fd = (int)counts[c].n_fd;
+    const int j0 = blockIdx.x * kBlTile;
+    if (j0 >= n_fd) return;
+    const int nt = P.bp_ntaps;
+    const int H = P.bp_hist;
+    const int tid = threadIdx.x;
+    const auto fd = gp(P.fd_buf);
+    const int pend = P.pstate->sq_pending;
+    const auto sq = gp(P.sq_buf);
+    if (nt == 0) {  // bandpass switched off (setBandpass(None, None)): pass through
+        for (int jl = tid; jl < kBlTile && j0 + jl < n_fd; jl += kPostThreads) {
+            const int j = j0 + jl;
+            const float2 y = fd[H + j];
+            sq[pend + j] = y;
+            if (P.debug && j < P.dbg_cap) {
+                P.dbg_fd[j] = y;
+                P.dbg_bp[j] = y;
+            }
+        }
+        return;
+    }
+    extern __shared__ __align__(16) float2 bl_sm[];
+    float2* taps = bl_sm;
+    float2* xs = bl_sm + ((nt + 3) & ~3);
+    const int nw = min(kBlTile, n_fd - j0) + nt - 1;
+    for (int t = tid; t < nt; t += kPostThreads) taps[t] = P.bp_taps[t];
+    const int64_t x0 = (int64_t)H + j0 - (nt - 1);  // >= 0: H >= nt - 1
+    for (int m = tid; m < nw; m += kPostThreads) xs[m] = fd[x0 + m];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int jl = tid + h * kPostThreads;
+        if (j0 + jl >= n_fd) break;
+        const float2* x = xs + jl + (nt - 1);
+        float ar = 0.0f, ai = 0.0f, br = 0.0f, bi = 0.0f;
+        int t = 0;
+#pragma unroll 4
+        for (; t + 1 < nt; t += 2) {
+            const float2 g0 = taps[t], g1 = taps[t + 1];
+            const float2 v0 = x[-t], v1 = x[-t - 1];
+            ar = fmaf(g0.x, v0.x, ar);
+            ar = fmaf(-g0.y, v0.y, ar);
+            ai = fmaf(g0.x, v0.y, ai);
+            ai = fmaf(g0.y, v0.x, ai);
+            br = fmaf(g1.x, v1.x, br);
+            br = fmaf(-g1.y, v1.y, br);
+            bi = fmaf(g1.x, v1.y, bi);
+            bi = fmaf(g1.y, v1.x, bi);
+        }
+        if (t < nt) {
+            const float2 g0 = taps[t];
+            const float2 v0 = x[-t];
+            ar = fmaf(g0.x, v0.x, ar);
+            ar = fmaf(-g0.y, v0.y, ar);
+            ai = fmaf(g0.x, v0.y, ai);
+            ai = fmaf(g0.y, v0.x, ai);
+        }
+        const float2 y = make_float2(ar + br, ai + bi);
+        const int j = j0 + jl;
+        sq[pend + j] = y;
+        if (P.debug && j < P.dbg_cap) {
+            P.dbg_fd[j] = x[0];
+            P.dbg_bp[j] = y;
         }
     }
 }
@@ -427,7 +641,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     const float v = cur[j];
                     const float ky = deemph_y, kx = dc_xp, kyy = dc_yp, ke = agc.env;
                     float u;
-                    if (DM == 0) u = deemph_step(v, alpha, beta, deemph_y);
+                    if (DM == 0 || DM == 3) u = deemph_step(v, alpha, beta, deemph_y);
                     else if (DM == 1) u = dcblock_step(v, dc_xp, dc_yp);
                     else u = v;
                     {
@@ -458,6 +672,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             if (it < nchunks) {
                 if (demod == 0) run_dm(std::integral_constant<int, 0>{}, it);
                 else if (demod == 1) run_dm(std::integral_constant<int, 1>{}, it);
+                else if (demod == 3) run_dm(std::integral_constant<int, 3>{}, it);  // WfmDeemphasis
                 else run_dm(std::integral_constant<int, 2>{}, it);
             }
             __syncthreads();
@@ -482,7 +697,9 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                 for (int j = wave - 1; j < kSerChunk; j += kFrontThreads / 64 - 1) {
                     const float2 q = srcu[j][lane];
                     float a;
-                    {
+                    if (demod == 3) {
+                        a = q.x;  // WFm has no Agc (csdr/chain/analog.py:66-71)
+                    } else {
 #pragma clang fp contract(off)
                         float g = (q.y > 0.0f) ? agcp.reference / q.y : agcp.max_gain;
                         if (g > agcp.max_gain) g = agcp.max_gain;
@@ -667,6 +884,26 @@ hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts
                                 hipStream_t st) {
     if (nchains <= 0) return hipSuccess;
     hipLaunchKernelGGL(post_parallel, dim3(nchains), dim3(kPostThreads), 0, st, posts, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const int* idx,
+                            int nlong, int64_t max_fd, int max_taps, hipStream_t st) {
+    if (nlong <= 0) return hipSuccess;
+    if (max_taps > kBlMaxTaps) return hipErrorInvalidValue;
+    const size_t lds = sizeof(float2) * (((max_taps + 3) & ~3) + kBlTile + max_taps);
+    static bool attr = false;
+    if (!attr) {
+        const size_t most = sizeof(float2) * (kBlMaxTaps + 1 + kBlTile + kBlMaxTaps);
+        hipError_t e = hipFuncSetAttribute((const void*)bp_long,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)most);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int tiles = (int)((max_fd + kBlTile - 1) / kBlTile);
+    hipLaunchKernelGGL(bp_long, dim3(std::max(1, tiles), nlong), dim3(kPostThreads), lds, st,
+                       posts, counts, idx);
+    hipLaunchKernelGGL(post_tail, dim3(nlong), dim3(kPostThreads), 0, st, posts, counts, idx);
     return hipGetLastError();
 }
 

@@ -15,7 +15,8 @@ namespace owrx {
 constexpr int kWave = 64;
 constexpr int kFdPoints = 12;     // FractionalDecimator Lagrange points
 constexpr int kFdHist = 16;       // DDC outputs kept for the interpolator window
-constexpr int kBpHist = 256;      // Bandpass history (taps - 1 <= 255)
+constexpr int kBpHist = 256;      // Bandpass history (taps - 1 <= 255) of the in-kernel FIR
+constexpr int kWfHist = 256;      // WFM: IF-rate demod / prefilter history (prefilter <= 255 taps)
 constexpr int kAdpcmSyncPeriod = 1001;  // data bytes per "SYNC" frame (AudioEngine.js:449-491)
 constexpr float kFmK = 0.340447f; // fmdemod_quadri_K
 

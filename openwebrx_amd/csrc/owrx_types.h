@@ -50,6 +50,9 @@ struct ChainStateP {
     int32_t sf_next;
     int32_t sf_row_frame;  // frames already summed into the open row (sf_acc)
     int32_t sf_pad;
+    // WFM audio FractionalDecimator(FLOAT, 250000/hd_rate, prefilter=True) (analog.py:66-71)
+    int64_t wf_count;      // FmDemod+Limit samples produced so far (IF rate)
+    int64_t wf_next;       // next audio output index
 };
 // Owned by post_serial (stream B).
 struct ChainStateS {
@@ -69,11 +72,19 @@ struct ChainPost {
     int32_t output;        // OWRX_OUT_*
     int32_t frac_enabled;
     int32_t bp_ntaps;      // 0 => no bandpass
+    int32_t bp_hist;       // bandpass history kept in fd_buf (>= bp_ntaps - 1, multiple of 256)
+    int32_t bp_long;       // bp_ntaps > kBpHist + 1: the bandpass runs in bp_long (multi-WG)
     double frac_rate;
     const float2* bp_taps;
     int32_t sq_len, sq_dec, sq_hang, sq_flush, sq_report;
     float sq_level;
     float deemph_alpha, deemph_beta;
+    // WFM: prefilter + 12-point Lagrange from the IF-rate FM demod output to the audio rate
+    double wfm_rate;       // 250000 / hd_output_rate
+    const float* pf_taps;  // prefilter lowpass
+    int32_t pf_ntaps;
+    float* wf_buf;         // [kWfHist + cap] FmDemod+Limit output (IF rate)
+    float* pf_buf;         // [kWfHist + cap] prefiltered
     AgcParams agc;
     // buffers
     ChainStateP* pstate;
@@ -124,7 +135,8 @@ struct ChainCounts {
     int64_t out_bytes;
     int32_t smeter;
     int32_t sf_bytes;      // secondary FFT bytes staged this step
-    int64_t n_ddc, n_fd, n_bp, n_sq;  // stage sample counts this step
+    int64_t n_ddc, n_fd, n_bp, n_sq;  // stage sample counts this step (n_sq: demod/audio)
+    int64_t n_gate;        // squelch output samples (IF rate; == n_sq except WFM)
 };
 
 }  // namespace owrx

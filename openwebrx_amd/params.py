@@ -21,9 +21,11 @@ MODE_BANDPASS = {  # owrx/modes.py:124-129
     "lsb": (-3000, -150),
     "usb": (150, 3000),
     "cw": (700, 900),
+    "wfm": (-124000, 124000),  # owrx/modes.py:125
 }
 MODE_DEMOD = {"nfm": _lib.DEMOD_NFM, "am": _lib.DEMOD_AM, "usb": _lib.DEMOD_SSB,
-              "lsb": _lib.DEMOD_SSB, "cw": _lib.DEMOD_SSB}
+              "lsb": _lib.DEMOD_SSB, "cw": _lib.DEMOD_SSB, "wfm": _lib.DEMOD_WFM}
+WFM_IF_RATE = 250000  # WFm.getFixedIfSampleRate (csdr/chain/analog.py:81-82)
 
 
 def f32(x):
@@ -70,8 +72,17 @@ def squelch_level(db):
 
 
 def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=None,
-                 squelch_db=-150, output=_lib.OUT_ADPCM, agc_profile=None):
-    """owrx_chain_params for ClientDemodulatorChain([Selector, demod, ClientAudioChain])."""
+                 squelch_db=-150, output=_lib.OUT_ADPCM, agc_profile=None, hd_output_rate=48000,
+                 wfm_deemphasis_tau=50e-6):
+    """owrx_chain_params for ClientDemodulatorChain([Selector, demod, ClientAudioChain]).
+
+    WFM (FixedIfSampleRateChain + HdAudio): the Selector runs at 250 kHz
+    (ClientDemodulatorChain._getSelectorOutputRate, owrx/dsp.py:150-158) and the audio at
+    hd_output_rate (owrx/dsp.py:494, :160-166)."""
+    wfm = mode == "wfm"
+    audio_rate = hd_output_rate if wfm else output_rate
+    if wfm:
+        output_rate = WFM_IF_RATE
     d, frac, tbw, cutoff = decimation(input_rate, output_rate)
     if bandpass is None:
         bandpass = MODE_BANDPASS.get(mode)
@@ -100,8 +111,11 @@ def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=Non
     p.agc_profile = agc_profile
     p.agc_initial_gain = 200.0 if demod == _lib.DEMOD_AM else -1.0   # Am: setInitialGain(200)
     p.agc_max_gain = 3.0 if demod == _lib.DEMOD_NFM else -1.0        # NFm: setMaxGain(3)
-    p.audio_rate = output_rate
+    p.audio_rate = audio_rate
     p.output = output
+    if wfm:
+        p.if_rate = float(WFM_IF_RATE)
+        p.deemph_tau = f32(wfm_deemphasis_tau)
     return p
 
 

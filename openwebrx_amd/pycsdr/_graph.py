@@ -173,12 +173,21 @@ def plan_segment(head):
     sq = take(M.Squelch)
     selector_last = mods[i - 1]
     fm = take(M.FmDemod)
+    wfm = None
     if fm is not None:
         lim = take(M.Limit)
-        de = take(M.NfmDeemphasis)
-        if lim is None or de is None or lim.max_amplitude != 1.0:
+        if lim is None or lim.max_amplitude != 1.0:
             return None
-        demod, audio_rate = _lib.DEMOD_NFM, de.sample_rate
+        de = take(M.NfmDeemphasis)
+        if de is not None:
+            demod, audio_rate = _lib.DEMOD_NFM, de.sample_rate
+        else:  # WFm: FractionalDecimator(FLOAT, prefilter) -> WfmDeemphasis, no Agc
+            fdf = take(M.FractionalDecimator)
+            wde = take(M.WfmDeemphasis)
+            if fdf is None or wde is None or not fdf.prefilter:
+                return None
+            demod, audio_rate = _lib.DEMOD_WFM, wde.sample_rate
+            wfm = dict(if_rate=fdf.rate * wde.sample_rate, deemph_tau=wde.tau)
     elif take(M.AmDemod) is not None:
         if take(M.DcBlock) is None:
             return None
@@ -187,8 +196,8 @@ def plan_segment(head):
         demod, audio_rate = _lib.DEMOD_SSB, 12000
     else:
         return None
-    agc = take(M.Agc)
-    if agc is None:
+    agc = take(M.Agc) if wfm is None else None
+    if agc is None and wfm is None:
         return None
     output = _lib.OUT_F32
     if take(M.Convert) is not None:
@@ -205,10 +214,12 @@ def plan_segment(head):
              cutoff=fir.cutoff, frac_rate=frac.rate if frac is not None else 1.0,
              bandpass=0, bp_low=0.0, bp_high=0.0, bp_transition=0.0,
              sq_length=750, sq_decimation=5, sq_hang=0, sq_flush=0, sq_report=0, sq_level=0.0,
-             demod=demod, agc_profile=agc.profile.engine_id,
-             agc_initial_gain=-1.0 if agc.initial_gain is None else agc.initial_gain,
-             agc_max_gain=-1.0 if agc.max_gain is None else agc.max_gain,
+             demod=demod, agc_profile=agc.profile.engine_id if agc is not None else 0,
+             agc_initial_gain=-1.0 if agc is None or agc.initial_gain is None else agc.initial_gain,
+             agc_max_gain=-1.0 if agc is None or agc.max_gain is None else agc.max_gain,
              audio_rate=audio_rate, output=output, power_writer=None)
+    if wfm is not None:
+        p.update(wfm)
     if bp is not None and bp.low_cut is not None and bp.high_cut is not None:
         p.update(bandpass=1, bp_low=bp.low_cut, bp_high=bp.high_cut,
                  bp_transition=bp.transition)
@@ -399,5 +410,6 @@ def _compatible(kind, old, new):
     else:
         keys = ("decimation", "transition", "cutoff", "frac_rate", "bp_transition", "sq_length",
                 "sq_decimation", "sq_hang", "sq_flush", "sq_report", "demod", "agc_profile",
-                "agc_initial_gain", "agc_max_gain", "audio_rate", "output")
+                "agc_initial_gain", "agc_max_gain", "audio_rate", "output", "if_rate",
+                "deemph_tau")
     return all(old.get(k) == new.get(k) for k in keys)

@@ -380,15 +380,20 @@ class FirDecimate(_NativeModule):
 
 
 class FractionalDecimator(_NativeModule):
+    """COMPLEX_FLOAT: the Selector's resampler (csdr/chain/selector.py:32-33).  FLOAT with
+    prefilter=True: WFm's IF-to-audio decimator (csdr/chain/analog.py:69).  Both run fused in a
+    chain segment on the engine."""
+
     def __init__(self, format, rate, num_poly_points=12, prefilter=False):
         super().__init__()
-        if format != Format.COMPLEX_FLOAT:
-            raise NotImplementedError("FractionalDecimator: only COMPLEX_FLOAT is on the GPU path")
-        if prefilter:
-            raise NotImplementedError("FractionalDecimator(prefilter=True) (WFM) is not on the "
-                                      "GPU path yet")
+        if format not in (Format.COMPLEX_FLOAT, Format.FLOAT) or num_poly_points != 12:
+            raise NotImplementedError("FractionalDecimator: COMPLEX_FLOAT or FLOAT, 12 points")
+        if prefilter != (format == Format.FLOAT):
+            raise NotImplementedError("FractionalDecimator: the GPU path has COMPLEX_FLOAT "
+                                      "without and FLOAT with prefilter (the reference's uses)")
         self.input_format = self.output_format = format
         self.rate = float(rate)
+        self.prefilter = bool(prefilter)
 
 
 class Bandpass(_NativeModule):
@@ -488,6 +493,23 @@ class Limit(_Unary):
 
     def _params(self):
         return (self.max_amplitude,)
+
+
+class WfmDeemphasis(_Unary):
+    """WfmDeemphasis(sampleRate, tau) (csdr/chain/analog.py:70): one-pole de-emphasis,
+    alpha = dt / (tau + dt)."""
+    input_format = Format.FLOAT
+    output_format = Format.FLOAT
+    _mod = "MOD_DEEMPH"
+
+    def __init__(self, sampleRate, tau=50e-6):
+        super().__init__()
+        self.sample_rate = int(sampleRate)
+        self.tau = float(tau)
+
+    def _params(self):
+        dt = 1.0 / float(self.sample_rate)
+        return (float(np.float32(dt / (float(np.float32(self.tau)) + dt))),)
 
 
 class NfmDeemphasis(_Unary):
@@ -648,6 +670,6 @@ for _name in ("Afc", "AudioResampler", "BaudotDecoder", "Ccir476Decoder", "Ccir4
               "CwDecoder", "DBPskDecoder", "Downmix", "DscDecoder", "ExecModule", "FaxDecoder",
               "Lowpass", "MFRttyDecoder", "NavtexDecoder", "NoiseFilter", "RttyDecoder",
               "SitorBDecoder", "SnrSquelch", "SstvDecoder", "Throttle", "TimingRecovery",
-              "VaricodeDecoder", "WfmDeemphasis"):
+              "VaricodeDecoder"):
     globals()[_name] = _unsupported(_name)
 del _name

@@ -168,6 +168,50 @@ int64_t orc_fractional_decimator(const float* in_cf, int64_t n, double rate, flo
     return k;
 }
 
+/* WFm's FractionalDecimator(FLOAT, 250000/hd_rate, prefilter=True) (csdr/chain/analog.py:69):
+ * causal lowpass prefilter (taps from orc_firdes_lowpass_f(firdes_filter_len(0.03), 0.5/rate),
+ * the build's recalled csdr default, unpinned), then the same 12-point Lagrange positions as
+ * orc_fractional_decimator on the real stream. */
+void orc_fir_real(const float* in, int64_t n, const float* taps, int ntaps, float* out) {
+    for (int64_t i = 0; i < n; i++) {
+        double a = 0.0;
+        int tmax = (i + 1 < ntaps) ? (int)(i + 1) : ntaps;
+        for (int t = 0; t < tmax; t++) a += (double)taps[t] * (double)in[i - t];
+        out[i] = (float)a;
+    }
+}
+
+int64_t orc_fractional_decimator_f(const float* in, int64_t n, double rate, float* out) {
+    int64_t k = 0;
+    for (;; k++) {
+        double w = 6.0 + (double)k * rate;
+        int64_t hi = (int64_t)ceil(w);
+        int64_t lo = hi - FD_POINTS / 2;
+        if (hi + (FD_POINTS / 2 - 1) >= n) break;
+        double u = (w - (double)lo) - 5.5;
+        double a = 0.0;
+        for (int i = 0; i < FD_POINTS; i++) {
+            double L = 1.0;
+            double ni = (double)i - 5.5;
+            for (int j = 0; j < FD_POINTS; j++) {
+                if (j == i) continue;
+                double nj = (double)j - 5.5;
+                L *= (u - nj) / (ni - nj);
+            }
+            a += L * (double)in[lo + i];
+        }
+        out[k] = (float)a;
+    }
+    return k;
+}
+
+/* WfmDeemphasis(rate, tau) (csdr/chain/analog.py:70): csdr deemphasis_wfm_ff,
+ * alpha = dt/(tau+dt), dt = 1/rate; the recurrence is orc_deemphasis. */
+float orc_wfm_deemphasis_alpha(int sample_rate, float tau) {
+    double dt = 1.0 / (double)sample_rate;
+    return (float)(dt / ((double)tau + dt));
+}
+
 /* Bandpass(transition, use_fft=True).setBandpass(lo, hi) (csdr/chain/selector.py:115-117,
  * 159-166).  csdr applies it by FFT overlap-add; the result is the causal convolution
  * y[n] = sum_t g[t] x[n-t] with zero history, which is what is computed here. */

@@ -49,6 +49,9 @@ PROTOS = {
     "orc_fir_decimate": (_L, [_P, _L, _P, _I, _I, _P]),
     "orc_fractional_decimator": (_L, [_P, _L, _D, _P]),
     "orc_fir_complex": (None, [_P, _L, _P, _I, _P]),
+    "orc_fir_real": (None, [_P, _L, _P, _I, _P]),
+    "orc_fractional_decimator_f": (_L, [_P, _L, _D, _P]),
+    "orc_wfm_deemphasis_alpha": (_F, [_I, _F]),
     "orc_squelch": (_L, [_P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P]),
     "orc_fmdemod": (None, [_P, _L, _P]),
     "orc_amdemod": (None, [_P, _L, _P]),
@@ -141,6 +144,30 @@ def fractional_decimator(x, rate):
     y = np.empty(int(x.size / rate) + 4, np.complex64)
     m = lib().orc_fractional_decimator(x.ctypes.data, x.size, rate, y.ctypes.data)
     return y[:m]
+
+
+def fir_real(x, taps):
+    x = _f32(x)
+    taps = _f32(taps)
+    y = np.empty_like(x)
+    lib().orc_fir_real(x.ctypes.data, x.size, taps.ctypes.data, taps.size, y.ctypes.data)
+    return y
+
+
+def fractional_decimator_f(x, rate):
+    x = _f32(x)
+    y = np.empty(int(x.size / rate) + 4, np.float32)
+    m = lib().orc_fractional_decimator_f(x.ctypes.data, x.size, rate, y.ctypes.data)
+    return y[:m]
+
+
+def wfm_audio(sq, if_rate, audio_rate, tau):
+    """WFm (csdr/chain/analog.py:55-116) after the Selector: FmDemod, Limit,
+    FractionalDecimator(FLOAT, if/audio, prefilter=True), WfmDeemphasis(audio, tau)."""
+    r = float(if_rate) / float(audio_rate)
+    pf = lowpass(filter_len(np.float32(0.03)), np.float32(0.5 / r))
+    a = fractional_decimator_f(fir_real(limit(fmdemod(sq)), pf), r)
+    return deemphasis(a, lib().orc_wfm_deemphasis_alpha(int(audio_rate), np.float32(tau or 50e-6)))
 
 
 def fir_complex(x, taps):
@@ -336,6 +363,10 @@ def stages(iq, p):
     bp = fir_complex(fd, c._keep[1]) if p.bandpass else fd
     sq, power = squelch(bp, p.sq_length, p.sq_decimation, p.sq_hang, p.sq_flush, p.sq_report,
                         p.sq_level)
+    if p.demod == 3:  # WFM: no Agc
+        dem = wfm_audio(sq, p.if_rate, p.audio_rate, p.deemph_tau)
+        return dict(ddc=ddc, frac=fd, bandpass=bp, squelch=sq, smeter=power, demod=dem, agc=dem,
+                    s16=convert_s16(dem))
     if p.demod == 0:
         dem = deemphasis(limit(fmdemod(sq)), c.deemph_alpha)
     elif p.demod == 1:

@@ -135,6 +135,22 @@ for sr in (2400000, 10000000, 61440000):
     entry["squelch_m80"] = take()
     res["selector_%d" % sr] = entry
 
+# WFM: Selector(sr, 250000) (FixedIfSampleRateChain, csdr/chain/analog.py:81-82) with the
+# mode's bandpass (owrx/modes.py:125) and WFm(hd_output_rate=48000, tau=50e-6)
+for sr in (2400000, 10000000, 61440000):
+    s = selector.Selector(sr, 250000)
+    entry = {"ctor": [sr, 250000], "calls": take()}
+    s.setFrequencyOffset(-600000 if sr > 2400000 else 300000)
+    entry["offset"] = take()
+    s.setBandpass(-124000, 124000)
+    entry["bandpass_wfm"] = take()
+    s.setSquelchLevel(-150)
+    entry["squelch_m150"] = take()
+    res["selector_wfm_%d" % sr] = entry
+analog.WFm(48000, 50e-6, False)
+res["wfm"] = take()
+clientaudio.ClientAudioChain(Format.FLOAT, 48000, 48000, "adpcm", False, 0)
+res["clientaudio_hd_adpcm"] = take()
 analog.NFm(12000)
 res["nfm"] = take()
 analog.Am()

@@ -46,4 +46,23 @@ def test_chain_params_struct_layout_matches_header():
     from openwebrx_amd import _lib
     # int/float fields are 4 bytes, frac_rate is an 8-byte double at offset 16
     assert _lib.ChainParams.frac_rate.offset == 16
-    assert ctypes.sizeof(_lib.ChainParams) == 88
+    # every field's offset and the size agree with the C compiler's layout of the header
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    names = [n for n, _ in _lib.ChainParams._fields_]
+    prog = ('#include <stdio.h>\n#include <stddef.h>\n#include "owrx_amd.h"\nint main(void){'
+            + "".join('printf("%%zu\\n", offsetof(owrx_chain_params, %s));' % n for n in names)
+            + 'printf("%zu\\n", sizeof(owrx_chain_params)); return 0;}')
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        with open(src, "w") as f:
+            f.write(prog)
+        subprocess.run(["gcc", "-I", inc, src, "-o", exe], check=True)
+        got = [int(v) for v in subprocess.run([exe], capture_output=True, text=True,
+                                              check=True).stdout.split()]
+    want = [getattr(_lib.ChainParams, n).offset for n in names] + [ctypes.sizeof(_lib.ChainParams)]
+    assert got == want

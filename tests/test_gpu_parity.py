@@ -446,3 +446,34 @@ def test_secondary_fft_rows(amd, avg):
     eng.sync()
     assert cf.read_audio() == ca.read_audio()
     eng.close()
+
+
+@pytest.mark.parametrize("fs", [2400000, 10000000])
+def test_wfm_chain(amd, fs):
+    """WFM: Selector at 250 kHz with the 3125-tap bandpass (bp_long kernel),
+    15625-sample squelch blocks, FmDemod + Limit, FractionalDecimator(FLOAT, 250000/48000,
+    prefilter) and WfmDeemphasis (no AGC) to 48 kHz HD audio; stages vs the oracle, next to an
+    NFM chain on the same engine."""
+    from openwebrx_amd import synth
+    n = (1 << 21) + 4321
+    iq, offs = synth.make_iq(fs, n, ["wfm", "nfm"])
+    pw = amd.params.chain_params(fs, offs[0], "wfm", output=amd._lib.OUT_S16)
+    pn = amd.params.chain_params(fs, offs[1], "nfm", output=amd._lib.OUT_S16)
+    assert pw.sq_length == 15625 and pw.audio_rate == 48000
+    eng, (cw, cn) = _run_chains(amd, iq, fs, [pw, pn], 1 << 18)
+    ref = oracle.stages(iq, pw)
+    assert rel_rms(cw.read_debug(0), ref["ddc"]) < 1e-5
+    bp = cw.read_debug(2)
+    assert bp.size == ref["bandpass"].size and rel_rms(bp, ref["bandpass"]) < 1e-5
+    sq = cw.read_debug(3)
+    assert sq.size == ref["squelch"].size and sq.size >= 2 * 15625
+    dem = cw.read_debug(4)
+    assert dem.size == ref["demod"].size and dem.size > 5000, (dem.size, ref["demod"].size)
+    assert rel_rms(dem, ref["demod"]) < 1e-4
+    s16 = np.frombuffer(cw.read_audio(), np.int16)
+    assert s16.size == ref["s16"].size
+    assert np.mean(np.abs(s16.astype(np.int32) - ref["s16"]) <= 1) > 0.999
+    sn = np.frombuffer(cn.read_audio(), np.int16)
+    ref_n = oracle.stages(iq, pn)["s16"]
+    assert sn.size == ref_n.size and np.mean(np.abs(sn.astype(np.int32) - ref_n) <= 1) > 0.999
+    eng.close()

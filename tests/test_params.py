@@ -70,6 +70,8 @@ def test_selector_parameters(gold, sr):
                            ["length", "decimation", "hangLength", "flushLength", "reportInterval"]]))
     assert float(g["offset100k"][0]["args"][0]) == params.shift_rate(100000, sr)
     for mode, (lo, hi) in params.MODE_BANDPASS.items():
+        if mode == "wfm":  # its Selector runs at 250 kHz (test_wfm_chain_params)
+            continue
         a = g["bandpass_" + mode][0]["args"]
         assert [float(v) for v in a] == [lo / 12000, hi / 12000]
     assert float(g["squelch_m150"][0]["args"][0]) == params.squelch_level(-150)
@@ -102,3 +104,33 @@ def test_resampler_params_follow_reference_math():
     assert p.cutoff == 0.5 and p.frac_rate == 1.0 and p.output == _lib.OUT_IQ
     p, if_rate = params.resampler_params(10000000, 14100000, 14074000, 300000)
     assert p.decimation == 33 and abs(if_rate - 10e6 / 33) < 1e-9
+
+
+@pytest.mark.parametrize("sr", [2400000, 10000000, 61440000])
+def test_wfm_chain_params(gold, sr):
+    """WFM: Selector(sr, 250000) with the mode's bandpass and squelch (recorded from
+    csdr/chain/selector.py) and WFm(48000, 50e-6) (csdr/chain/analog.py:55-116)."""
+    from openwebrx_amd import _lib
+    g = gold["selector_wfm_%d" % sr]
+    offset = -600000 if sr > 2400000 else 300000
+    p = params.chain_params(sr, offset, "wfm")
+    fd = _calls(g["calls"], "FirDecimate")[0]["args"]
+    assert fd[0] == p.decimation and np.float32(float(fd[1])) == p.transition
+    assert np.float32(float(fd[2])) == p.cutoff
+    fr = _calls(g["calls"], "FractionalDecimator")
+    assert (float(fr[0]["args"][1]) if fr else 1.0) == p.frac_rate
+    bp = _calls(g["calls"], "Bandpass")[0]["kwargs"]
+    assert np.float32(float(bp["transition"])) == p.bp_transition
+    lo, hi = (float(v) for v in g["bandpass_wfm"][0]["args"])
+    assert (np.float32(lo), np.float32(hi)) == (p.bp_low, p.bp_high)
+    sq = _calls(g["calls"], "Squelch")[0]["kwargs"]
+    assert (sq["length"], sq["hangLength"], sq["flushLength"], sq["reportInterval"]) == \
+        (p.sq_length, p.sq_hang, p.sq_flush, p.sq_report)
+    assert np.float32(float(g["offset"][0]["args"][0])) == p.shift_rate
+    assert p.demod == _lib.DEMOD_WFM and p.if_rate == 250000.0 and p.audio_rate == 48000
+    wfm = {e["module"]: e for e in gold["wfm"] if e["op"] == "new"}
+    assert float(wfm["FractionalDecimator"]["args"][1]) == p.if_rate / p.audio_rate
+    assert wfm["FractionalDecimator"]["kwargs"] == {"prefilter": True}
+    assert wfm["WfmDeemphasis"]["args"][0] == p.audio_rate
+    assert np.float32(float(wfm["WfmDeemphasis"]["args"][1])) == p.deemph_tau
+    assert [e["module"] for e in gold["clientaudio_hd_adpcm"]] == ["Convert", "AdpcmEncoder"]

@@ -210,6 +210,43 @@ def test_planner_secondary_fft_tap():
     _graph.finish(wide)
 
 
+@pytest.mark.parametrize("fs", [2400000, 10000000])
+def test_planner_wfm_chain(fs):
+    """Selector(fs, 250000) + WFm(48000, 50e-6) + ClientAudioChain(FLOAT, 48000, 48000) wired
+    like ClientDemodulatorChain plans to params.chain_params(fs, off, "wfm") exactly."""
+    off = 300000
+    d, frac, tbw, cutoff = params.decimation(fs, 250000)
+    shift = M.Shift(0.0)
+    shift.setRate(params.shift_rate(off, fs))
+    sel = [shift, M.FirDecimate(d, tbw, cutoff)]
+    if frac != 1.0:
+        sel.append(M.FractionalDecimator(Format.COMPLEX_FLOAT, frac))
+    bp = M.Bandpass(transition=320.0 / 250000, use_fft=True)
+    bp.setBandpass(-124000 / 250000, 124000 / 250000)
+    sq = params.squelch_parameters(250000)
+    sel += [bp, M.Squelch(Format.COMPLEX_FLOAT, length=sq["length"], decimation=sq["decimation"],
+                          hangLength=sq["hangLength"], flushLength=sq["flushLength"],
+                          reportInterval=sq["reportInterval"])]
+    dem = [M.FmDemod(), M.Limit(),
+           M.FractionalDecimator(Format.FLOAT, 250000.0 / 48000, prefilter=True),
+           M.WfmDeemphasis(48000, 50e-6)]
+    mods = sel + dem + client_audio()
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    ch = Chain(mods)
+    ch.setWriter(M.Buffer(Format.CHAR))
+    ch.setReader(wide.getReader())
+    kind, p, used = _graph.plan_segment(mods[0])
+    assert kind == "chain" and used == mods
+    got = _graph.chain_params_struct(p)
+    want = params.chain_params(fs, off, "wfm", output=_lib.OUT_ADPCM)
+    for name, _ in _lib.ChainParams._fields_:
+        if name in ("agc_profile", "agc_initial_gain", "agc_max_gain"):
+            continue  # WFm has no Agc
+        g, w = getattr(got, name), getattr(want, name)
+        assert g == pytest.approx(w, rel=1e-6, abs=1e-12), name
+    _graph.finish(wide)
+
+
 def test_unrecognised_graph_is_not_fused():
     wide = M.Buffer(Format.COMPLEX_FLOAT)
     shift = M.Shift(0.1)
