@@ -877,6 +877,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.agc = agc_profile(q.agc_profile);
             if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
             if (q.agc_max_gain >= 0) p.agc.max_gain = q.agc_max_gain;
+            if (q.demod == OWRX_DEMOD_WFM) p.agc.max_gain = std::max(1.0f, p.agc.max_gain);
             p.pstate = c->d_pstate;
             p.sstate = c->d_sstate;
             p.ddc_buf = c->d_ddc;

@@ -652,7 +652,9 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                         const float t = rate * d;
                         agc.env = agc.env + t;
                     }
-                    dst[i + j][lane] = make_float2(u, agc.env);
+                    // WFm has no Agc (csdr/chain/analog.py:66-71): envelope = reference makes
+                    // the gain exactly 1 (correctly rounded x / x; the host keeps max_gain >= 1)
+                    dst[i + j][lane] = make_float2(u, DM == 3 ? agcp.reference : agc.env);
                     if (!FULL && base + i + j >= n) {  // past this lane's end: keep state
                         deemph_y = ky;
                         dc_xp = kx;
@@ -697,9 +699,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                 for (int j = wave - 1; j < kSerChunk; j += kFrontThreads / 64 - 1) {
                     const float2 q = srcu[j][lane];
                     float a;
-                    if (demod == 3) {
-                        a = q.x;  // WFm has no Agc (csdr/chain/analog.py:66-71)
-                    } else {
+                    {
 #pragma clang fp contract(off)
                         float g = (q.y > 0.0f) ? agcp.reference / q.y : agcp.max_gain;
                         if (g > agcp.max_gain) g = agcp.max_gain;
