@@ -133,6 +133,9 @@ typedef struct {
                                 owrx/config/defaults.py:21); 0 => 50e-6 */
     double  if_rate;         /* WFM: the Selector output rate (250000); audio_rate is the HD
                                 output rate (48000, owrx/dsp.py:494) */
+    int32_t nr_enabled;      /* ClientAudioChain NoiseFilter(nr_threshold) before Convert
+                                (csdr/chain/clientaudio.py:12-13; owrx/dsp.py:496-509) */
+    float   nr_threshold;    /* dB, the UI's -20..20 slider (htdocs/index.html:278) */
 } owrx_chain_params;
 
 int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle);
@@ -140,6 +143,10 @@ int owrx_chain_destroy(owrx_engine* e, int handle);
 int owrx_chain_set_shift_rate(owrx_engine* e, int handle, float rate);
 int owrx_chain_set_bandpass(owrx_engine* e, int handle, int enabled, float low, float high);
 int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level);
+/* ClientAudioChain.setNrEnabled / setNrThreshold (csdr/chain/clientaudio.py:80-90): the
+ * reference rebuilds the Converter, i.e. a fresh NoiseFilter; so does this (state reset at the
+ * next block). */
+int owrx_chain_set_noise_filter(owrx_engine* e, int handle, int enabled, float threshold_db);
 /* audio bytes (s16 LE / ADPCM stream / f32) produced so far; Reader.read() of the audio
  * buffer (owrx/dsp.py:846-863) */
 int64_t owrx_chain_read_audio(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes);

@@ -63,6 +63,8 @@ class ChainParams(ctypes.Structure):
         ("output", ctypes.c_int32),
         ("deemph_tau", ctypes.c_float),
         ("if_rate", ctypes.c_double),
+        ("nr_enabled", ctypes.c_int32),
+        ("nr_threshold", ctypes.c_float),
     ]
 
 
@@ -115,6 +117,7 @@ PROTOTYPES = {
     "owrx_chain_set_shift_rate": (_i32, [_vp, _i32, _f32]),
     "owrx_chain_set_bandpass": (_i32, [_vp, _i32, _i32, _f32, _f32]),
     "owrx_chain_set_squelch_level": (_i32, [_vp, _i32, _f32]),
+    "owrx_chain_set_noise_filter": (_i32, [_vp, _i32, _i32, _f32]),
     "owrx_chain_read_audio": (_i64, [_vp, _i32, _vp, _i64]),
     "owrx_chain_read_smeter": (_i64, [_vp, _i32, _vp, _i64]),
     "owrx_chain_origin": (_i64, [_vp, _i32]),

@@ -61,6 +61,8 @@ hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const i
                             int nlong, int64_t max_fd, int max_taps, hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, int output, int debug, hipStream_t st);
+hipError_t launch_chain_nr(const ChainPost* posts, int nposts, ChainCounts* counts,
+                           hipStream_t st);
 hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, ChainCounts* counts,
                              hipStream_t st);
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
@@ -225,6 +227,12 @@ struct Chain {
     float* d_pf = nullptr;
     float* d_pf_taps = nullptr;
     int pf_ntaps = 0;
+    // NoiseFilter (nr_enabled); buffers allocated on first enable, zeroed on (re)start
+    NrState* d_nr_state = nullptr;
+    float* d_nr_in = nullptr;
+    float* d_nr_pow = nullptr;
+    float* d_nr_ola = nullptr;
+    bool nr_reset = false;
     int64_t cap = 0;      // per-step sample capacity of stage buffers
     int64_t out_cap = 0;  // staging bytes per step
     int sm_cap = 0;
@@ -343,6 +351,8 @@ struct owrx_engine {
     int64_t row_tail = 0;  // oldest row slot not yet drained
     std::vector<ChainPost> posts;
     owrx_stats stats;
+    float* d_nr_win = nullptr;    // NoiseFilter window and twiddles (shared by all chains)
+    float2* d_nr_tw = nullptr;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -369,6 +379,10 @@ static void free_chain(Chain* c) {
     dfree(c->d_wf);
     dfree(c->d_pf);
     dfree(c->d_pf_taps);
+    dfree(c->d_nr_state);
+    dfree(c->d_nr_in);
+    dfree(c->d_nr_pow);
+    dfree(c->d_nr_ola);
     dfree(c->d_sf);
     dfree(c->d_sf_acc);
     dfree(c->d_sf_window);
@@ -443,8 +457,8 @@ static int drain_slot(owrx_engine* e, int si) {
                            sizeof(float) * (size_t)std::min<int64_t>(cc.smeter, e->sm_stride));
             if (s.debug && s.h_dbg) {
                 const uint8_t* base = s.h_dbg + (int64_t)k * kDebugStages * e->dbg_stride;
-                const int64_t cnt[kDebugStages] = {cc.n_ddc,  cc.n_fd, cc.n_bp,
-                                                   cc.n_gate, cc.n_sq, cc.n_sq};
+                const int64_t cnt[kDebugStages] = {cc.n_ddc,  cc.n_fd,    cc.n_bp,
+                                                   cc.n_gate, cc.n_front, cc.n_front};
                 const int64_t isz[kDebugStages] = {8, 8, 8, 8, 4, 4};
                 for (int st = 0; st < kDebugStages; ++st) {
                     const int64_t bytes = std::min(cnt[st] * isz[st], e->dbg_stride);
@@ -803,6 +817,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     };
     std::vector<GroupWork> work;
     uint32_t sf_sizes = 0;  // secondary FFT sizes (log2 bit set) present this step
+    bool any_nr = false;    // a chain runs a NoiseFilter this step
     for (auto& gp : e->groups) {  // descriptors first, so the DDC bracket holds only kernels
         ChainGroup* g = gp.get();
         if (g->members.empty()) continue;
@@ -874,6 +889,24 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 p.pf_buf = c->d_pf;
             }
             p.deemph_beta = 1.0f - p.deemph_alpha;
+            if (q.nr_enabled && c->d_nr_state && q.output != OWRX_OUT_IQ) {
+                if (c->nr_reset) {  // a fresh NoiseFilter (ClientAudioChain._updateConverter)
+                    HIPCHK(hipMemsetAsync(c->d_nr_state, 0, sizeof(NrState), e->sB));
+                    HIPCHK(hipMemsetAsync(c->d_nr_in, 0, sizeof(float) * kNrHop, e->sB));
+                    HIPCHK(hipMemsetAsync(c->d_nr_pow, 0, sizeof(float) * 2 * (kNrN / 2 + 1), e->sB));
+                    HIPCHK(hipMemsetAsync(c->d_nr_ola, 0, sizeof(float) * kNrHop, e->sB));
+                    c->nr_reset = false;
+                }
+                p.nr_enabled = 1;
+                p.nr_t = (float)std::pow(10.0, (double)q.nr_threshold / 10.0);
+                p.nr_state = c->d_nr_state;
+                p.nr_in = c->d_nr_in;
+                p.nr_pow = c->d_nr_pow;
+                p.nr_ola = c->d_nr_ola;
+                p.nr_win = e->d_nr_win;
+                p.nr_tw = e->d_nr_tw;
+                any_nr = true;
+            }
             p.agc = agc_profile(q.agc_profile);
             if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
             if (q.agc_max_gain >= 0) p.agc.max_gain = q.agc_max_gain;
@@ -988,6 +1021,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         for (int o = 0; o < 3; ++o)
             HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o], nsel[o], o, dbg,
                                       e->sB));
+        if (any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, e->sB));
         HIPCHK(hipEventRecord(S.evF, e->sB));
         // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host
         HIPCHK(hipStreamWaitEvent(e->sC, S.evF, 0));
@@ -1160,6 +1194,8 @@ int owrx_engine_destroy(owrx_engine* e) {
         if (st) hipStreamSynchronize(st);
     for (auto& kv : e->chains) free_chain(kv.second.get());
     for (auto& kv : e->wfs) free_wf(kv.second.get());
+    dfree(e->d_nr_win);
+    dfree(e->d_nr_tw);
     for (auto& g : e->groups) {
         dfree(g->d_taps);
         dfree(g->d_chains);
@@ -1392,6 +1428,32 @@ int64_t owrx_waterfall_read(owrx_engine* e, int handle, uint8_t* dst, int64_t ma
 
 // ---- chains -----------------------------------------------------------------------------
 
+static int64_t chain_nr_in_cap(const Chain* c) {
+    return kNrHop + c->cap + c->prm.sq_length + 16 + kNrN;
+}
+
+// NoiseFilter buffers (first enable) and the engine's window / twiddle tables
+static int chain_nr_alloc(owrx_engine* e, Chain* c) {
+    if (!e->d_nr_win) {
+        std::vector<float> w(kNrN);
+        for (int i = 0; i < kNrN; ++i)
+            w[i] = (float)std::sqrt(0.5 - 0.5 * std::cos(2.0 * M_PI * (double)i / kNrN));
+        std::vector<float> tw = fft_twiddles(kNrN);
+        HIPCHK(dalloc(&e->d_nr_win, (size_t)kNrN));
+        HIPCHK(dalloc(&e->d_nr_tw, (size_t)kNrN));
+        HIPCHK(hipMemcpy(e->d_nr_win, w.data(), sizeof(float) * kNrN, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->d_nr_tw, tw.data(), sizeof(float) * 2 * kNrN, hipMemcpyHostToDevice));
+    }
+    if (!c->d_nr_state) {
+        HIPCHK(dalloc(&c->d_nr_state, 1));
+        HIPCHK(dalloc(&c->d_nr_in, (size_t)chain_nr_in_cap(c)));
+        HIPCHK(dalloc(&c->d_nr_pow, (size_t)2 * (kNrN / 2 + 1)));
+        HIPCHK(dalloc(&c->d_nr_ola, (size_t)kNrHop));
+    }
+    c->nr_reset = true;
+    return OWRX_OK;
+}
+
 static int chain_validate(const owrx_chain_params* p) {
     if (p && p->output == OWRX_OUT_IQ)  // DDC only: the rest of the struct is unused
         return (p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate != 1.0)
@@ -1531,8 +1593,10 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     HIPCHK(dalloc(&c->d_sq, (size_t)scap));
     // slack: the serial kernels read whole 64-sample chunks / 8-sample prefetches unguarded
     for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_dem[i], (size_t)scap + 160));
-    for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_s16[i], (size_t)scap + 160));
+    // + kNrN: a NoiseFilter emits up to one frame more than its input per step
+    for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_s16[i], (size_t)scap + 160 + kNrN));
     int rc = chain_set_bandpass_taps(e, c.get());
+    if (!rc && p->nr_enabled && p->output != OWRX_OUT_IQ) rc = chain_nr_alloc(e, c.get());
     if (rc) {
         free_chain(c.get());
         return rc;
@@ -1590,6 +1654,17 @@ int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level) {
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     it->second->prm.sq_level = level;
+    return OWRX_OK;
+}
+
+int owrx_chain_set_noise_filter(owrx_engine* e, int handle, int enabled, float threshold_db) {
+    ENGINE_GUARD(e);
+    auto it = e->chains.find(handle);
+    if (it == e->chains.end() || it->second->prm.output == OWRX_OUT_IQ) return OWRX_EINVAL;
+    Chain* c = it->second.get();
+    if (enabled) RC_FAIL(e, chain_nr_alloc(e, c));
+    c->prm.nr_enabled = enabled ? 1 : 0;
+    c->prm.nr_threshold = threshold_db;
     return OWRX_OK;
 }
 

@@ -200,7 +200,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
             c.out_bytes = (int64_t)n_new * 8;
             c.smeter = 0;
             c.n_ddc = n_new;
-            c.n_fd = c.n_bp = c.n_sq = c.n_gate = 0;
+            c.n_fd = c.n_bp = c.n_sq = c.n_gate = c.n_front = 0;
         }
         return;
     }
@@ -470,6 +470,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
             c.n_fd = n_fd;
             c.n_bp = n_fd;
             c.n_sq = n_audio;
+            c.n_front = n_audio;
             c.n_gate = nsq;
         }
     }
@@ -688,7 +689,10 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             if (OUT == 0) counts[c].out_bytes = 2 * (int64_t)n;
         }
     } else {
-        // ---- gain + Convert (waves 1..3 take every third sample), one chunk behind
+        // ---- gain + Convert (waves 1..3 take every third sample), one chunk behind; a chain
+        // with a NoiseFilter stores the AGC output for chain_nr instead (Convert follows it)
+        const bool nr = sl.active && Pp->nr_enabled;
+        const int nr_fill = nr ? kNrHop + Pp->nr_state->pend : 0;
         for (int it = 0; it < nchunks + 1; ++it) {
             const int ch = it - 1;
             if (ch >= 0) {
@@ -707,7 +711,9 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     }
                     const int64_t qi = base + j;
                     const bool valid = sl.active && (full || qi < n);
-                    if (OUT == 2) {
+                    if (nr) {
+                        if (valid) gp(Pp->nr_in)[nr_fill + qi] = a;
+                    } else if (OUT == 2) {
                         if (valid && 4 * qi + 4 <= Pp->out_cap) gp(reinterpret_cast<float*>(Pp->out))[qi] = a;
                     } else if (OUT == 0) {
                         if (valid && 2 * qi + 2 <= Pp->out_cap)

@@ -16,6 +16,8 @@ constexpr int kWave = 64;
 constexpr int kFdPoints = 12;     // FractionalDecimator Lagrange points
 constexpr int kFdHist = 16;       // DDC outputs kept for the interpolator window
 constexpr int kBpHist = 256;      // Bandpass history (taps - 1 <= 255) of the in-kernel FIR
+constexpr int kNrN = 512;         // NoiseFilter frame (42.7 ms at 12 kHz), 50 % overlap
+constexpr int kNrHop = kNrN / 2;
 constexpr int kWfHist = 256;      // WFM: IF-rate demod / prefilter history (prefilter <= 255 taps)
 constexpr int kAdpcmSyncPeriod = 1001;  // data bytes per "SYNC" frame (AudioEngine.js:449-491)
 constexpr float kFmK = 0.340447f; // fmdemod_quadri_K

@@ -64,6 +64,11 @@ struct ChainStateS {
     int32_t has_left;      // ADPCM: one encoded nibble waiting for its pair
     int32_t left_code;
 };
+// NoiseFilter state (stream B; the host zeroes it with the filter's buffers on (re)start)
+struct NrState {
+    int32_t pend;          // input samples after nr_in[0, kNrHop) (the previous hop)
+    int32_t frames;        // frames processed
+};
 
 // Static + per-step description of one chain, shared by post_parallel and post_serial.
 struct ChainPost {
@@ -85,6 +90,15 @@ struct ChainPost {
     int32_t pf_ntaps;
     float* wf_buf;         // [kWfHist + cap] FmDemod+Limit output (IF rate)
     float* pf_buf;         // [kWfHist + cap] prefiltered
+    // NoiseFilter (ClientAudioChain, csdr/chain/clientaudio.py:12-13) between Agc and Convert
+    int32_t nr_enabled;
+    float nr_t;            // 10^(threshold_dB / 10)
+    NrState* nr_state;
+    float* nr_in;          // [kNrHop + cap + kNrN] AGC output not yet filtered
+    float* nr_pow;         // [2 * (kNrN / 2 + 1)] smoothed power, noise floor per bin
+    float* nr_ola;         // [kNrHop] overlap-add tail
+    const float* nr_win;   // [kNrN] sqrt periodic Hann
+    const float2* nr_tw;   // [kNrN] FFT twiddles
     AgcParams agc;
     // buffers
     ChainStateP* pstate;
@@ -137,6 +151,7 @@ struct ChainCounts {
     int32_t sf_bytes;      // secondary FFT bytes staged this step
     int64_t n_ddc, n_fd, n_bp, n_sq;  // stage sample counts this step (n_sq: demod/audio)
     int64_t n_gate;        // squelch output samples (IF rate; == n_sq except WFM)
+    int64_t n_front;       // samples through the demod front / AGC (n_sq before NoiseFilter)
 };
 
 }  // namespace owrx

@@ -73,7 +73,7 @@ def squelch_level(db):
 
 def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=None,
                  squelch_db=-150, output=_lib.OUT_ADPCM, agc_profile=None, hd_output_rate=48000,
-                 wfm_deemphasis_tau=50e-6):
+                 wfm_deemphasis_tau=50e-6, nr_enabled=False, nr_threshold=0):
     """owrx_chain_params for ClientDemodulatorChain([Selector, demod, ClientAudioChain]).
 
     WFM (FixedIfSampleRateChain + HdAudio): the Selector runs at 250 kHz
@@ -113,6 +113,8 @@ def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=Non
     p.agc_max_gain = 3.0 if demod == _lib.DEMOD_NFM else -1.0        # NFm: setMaxGain(3)
     p.audio_rate = audio_rate
     p.output = output
+    p.nr_enabled = 1 if nr_enabled else 0  # ClientAudioChain NoiseFilter (clientaudio.py:12-13)
+    p.nr_threshold = f32(nr_threshold)
     if wfm:
         p.if_rate = float(WFM_IF_RATE)
         p.deemph_tau = f32(wfm_deemphasis_tau)

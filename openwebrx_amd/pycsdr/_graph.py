@@ -199,6 +199,7 @@ def plan_segment(head):
     agc = take(M.Agc) if wfm is None else None
     if agc is None and wfm is None:
         return None
+    nr = take(M.NoiseFilter)
     output = _lib.OUT_F32
     if take(M.Convert) is not None:
         output = _lib.OUT_S16
@@ -220,6 +221,8 @@ def plan_segment(head):
              audio_rate=audio_rate, output=output, power_writer=None)
     if wfm is not None:
         p.update(wfm)
+    p.update(nr_enabled=1 if nr is not None else 0,
+             nr_threshold=nr.threshold if nr is not None else 0.0)
     if bp is not None and bp.low_cut is not None and bp.high_cut is not None:
         p.update(bandpass=1, bp_low=bp.low_cut, bp_high=bp.high_cut,
                  bp_transition=bp.transition)
@@ -411,5 +414,5 @@ def _compatible(kind, old, new):
         keys = ("decimation", "transition", "cutoff", "frac_rate", "bp_transition", "sq_length",
                 "sq_decimation", "sq_hang", "sq_flush", "sq_report", "demod", "agc_profile",
                 "agc_initial_gain", "agc_max_gain", "audio_rate", "output", "if_rate",
-                "deemph_tau")
+                "deemph_tau", "nr_enabled", "nr_threshold")
     return all(old.get(k) == new.get(k) for k in keys)

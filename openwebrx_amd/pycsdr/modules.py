@@ -495,6 +495,17 @@ class Limit(_Unary):
         return (self.max_amplitude,)
 
 
+class NoiseFilter(_NativeModule):
+    """NoiseFilter(threshold) of ClientAudioChain (csdr/chain/clientaudio.py:12-13): FLOAT ->
+    FLOAT spectral subtraction; runs fused in a chain segment (kernels_nr.hip)."""
+    input_format = Format.FLOAT
+    output_format = Format.FLOAT
+
+    def __init__(self, threshold=0):
+        super().__init__()
+        self.threshold = float(threshold)
+
+
 class WfmDeemphasis(_Unary):
     """WfmDeemphasis(sampleRate, tau) (csdr/chain/analog.py:70): one-pole de-emphasis,
     alpha = dt / (tau + dt)."""
@@ -668,7 +679,7 @@ def _unsupported(name):
 
 for _name in ("Afc", "AudioResampler", "BaudotDecoder", "Ccir476Decoder", "Ccir493Decoder",
               "CwDecoder", "DBPskDecoder", "Downmix", "DscDecoder", "ExecModule", "FaxDecoder",
-              "Lowpass", "MFRttyDecoder", "NavtexDecoder", "NoiseFilter", "RttyDecoder",
+              "Lowpass", "MFRttyDecoder", "NavtexDecoder", "RttyDecoder",
               "SitorBDecoder", "SnrSquelch", "SstvDecoder", "Throttle", "TimingRecovery",
               "VaricodeDecoder"):
     globals()[_name] = _unsupported(_name)

@@ -700,3 +700,57 @@ int64_t orc_run_workload(const float* iq, int64_t n, int N, int hop, int avg, fl
     }
     return total;
 }
+
+
+/* NoiseFilter(nr_threshold) (csdr/chain/clientaudio.py:12-13; "spectral subtraction",
+ * CHANGELOG.md:852).  csdr's source is not available: this is the build's documented choice,
+ * mirrored by kernels_nr.hip (parity unpinned against csdr).  Frames of 512 at hop 256,
+ * sqrt(periodic Hann) analysis + synthesis; per bin S = 0.7 S + 0.3 |X|^2 (first frame
+ * S = |X|^2); noise floor Nf = geometric mean of S over the 257 bins (a tone or voice occupies
+ * few bins, so the log-average stays at the noise), smoothed 0.9 / 0.1 across frames; gain
+ * S / (S + t Nf + 1e-30) with t = 10^(threshold/10); overlap-add, one hop of latency (zero
+ * history before sample 0).
+ * Returns the samples emitted: whole hops after the first frame. */
+#define NR_N 512
+#define NR_H 256
+int64_t orc_noise_filter(const float* in, int64_t n, float threshold_db, float* out) {
+    double w[NR_N], S[NR_N / 2 + 1], Nf = 0.0, ola[NR_H];
+    double buf[2 * NR_N], X[2 * NR_N];
+    double t = pow(10.0, (double)threshold_db / 10.0);
+    for (int i = 0; i < NR_N; i++) w[i] = sqrt(0.5 - 0.5 * cos(2.0 * M_PI * i / NR_N));
+    memset(ola, 0, sizeof(ola));
+    int64_t nout = 0;
+    /* frame f covers input [f*H - H, f*H + H) */
+    for (int64_t f = 0; f * NR_H + NR_H <= n; f++) {
+        for (int i = 0; i < NR_N; i++) {
+            int64_t s = f * NR_H - NR_H + i;
+            buf[2 * i] = (s >= 0 ? (double)in[s] : 0.0) * w[i];
+            buf[2 * i + 1] = 0.0;
+        }
+        orc_fft(buf, NR_N, X);
+        double G[NR_N / 2 + 1], lsum = 0.0;
+        for (int k = 0; k <= NR_N / 2; k++) {
+            double p = X[2 * k] * X[2 * k] + X[2 * k + 1] * X[2 * k + 1];
+            S[k] = f == 0 ? p : 0.7 * S[k] + 0.3 * p;
+            lsum += log(S[k] + 1e-30);
+        }
+        double geo = exp(lsum / (NR_N / 2 + 1));
+        Nf = f == 0 ? geo : 0.9 * Nf + 0.1 * geo;
+        for (int k = 0; k <= NR_N / 2; k++) G[k] = S[k] / (S[k] + t * Nf + 1e-30);
+        for (int i = 0; i < NR_N; i++) {
+            double g = G[i <= NR_N / 2 ? i : NR_N - i];
+            buf[2 * i] = g * X[2 * i];
+            buf[2 * i + 1] = -g * X[2 * i + 1];
+        }
+        orc_fft(buf, NR_N, X);
+        for (int i = 0; i < NR_H; i++) {
+            double y0 = X[2 * i] / NR_N * w[i];
+            double y1 = X[2 * (NR_H + i)] / NR_N * w[NR_H + i];
+            double o = ola[i] + y0;
+            ola[i] = y1;
+            if (f > 0) out[nout + i] = (float)o;
+        }
+        if (f > 0) nout += NR_H;
+    }
+    return nout;
+}

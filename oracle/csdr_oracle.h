@@ -114,4 +114,5 @@ int64_t orc_run_workload(const float* iq, int64_t n, int N, int hop, int avg, fl
 void orc_fir_real(const float* in, int64_t n, const float* taps, int ntaps, float* out);
 int64_t orc_fractional_decimator_f(const float* in, int64_t n, double rate, float* out);
 float orc_wfm_deemphasis_alpha(int sample_rate, float tau);
+int64_t orc_noise_filter(const float* in, int64_t n, float threshold_db, float* out);
 #endif

@@ -50,6 +50,7 @@ PROTOS = {
     "orc_fractional_decimator": (_L, [_P, _L, _D, _P]),
     "orc_fir_complex": (None, [_P, _L, _P, _I, _P]),
     "orc_fir_real": (None, [_P, _L, _P, _I, _P]),
+    "orc_noise_filter": (_L, [_P, _L, _F, _P]),
     "orc_fractional_decimator_f": (_L, [_P, _L, _D, _P]),
     "orc_wfm_deemphasis_alpha": (_F, [_I, _F]),
     "orc_squelch": (_L, [_P, _L, _I, _I, _I, _I, _I, _F, _P, _P, _P]),
@@ -158,6 +159,14 @@ def fractional_decimator_f(x, rate):
     x = _f32(x)
     y = np.empty(int(x.size / rate) + 4, np.float32)
     m = lib().orc_fractional_decimator_f(x.ctypes.data, x.size, rate, y.ctypes.data)
+    return y[:m]
+
+
+def noise_filter(x, threshold_db):
+    """NoiseFilter (documented choice, see orc_noise_filter)."""
+    x = _f32(x)
+    y = np.empty(x.size + 512, np.float32)
+    m = lib().orc_noise_filter(x.ctypes.data, x.size, threshold_db, y.ctypes.data)
     return y[:m]
 
 
@@ -374,5 +383,10 @@ def stages(iq, p):
     else:
         dem = realpart(sq)
     ag = agc(dem, c.agc)
-    return dict(ddc=ddc, frac=fd, bandpass=bp, squelch=sq, smeter=power, demod=dem, agc=ag,
-                s16=convert_s16(ag))
+    out = dict(ddc=ddc, frac=fd, bandpass=bp, squelch=sq, smeter=power, demod=dem, agc=ag)
+    if getattr(p, "nr_enabled", 0):
+        out["nr"] = noise_filter(ag, p.nr_threshold)
+        out["s16"] = convert_s16(out["nr"])
+    else:
+        out["s16"] = convert_s16(ag)
+    return out

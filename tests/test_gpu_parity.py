@@ -477,3 +477,42 @@ def test_wfm_chain(amd, fs):
     ref_n = oracle.stages(iq, pn)["s16"]
     assert sn.size == ref_n.size and np.mean(np.abs(sn.astype(np.int32) - ref_n) <= 1) > 0.999
     eng.close()
+
+
+def test_c5_ssb_noise_filter_chains(amd):
+    """BASELINE config 5 shape: 10 Msps, 64 USB chains with NoiseFilter(10) (nr_enabled,
+    ClientAudioChain, csdr/chain/clientaudio.py:12-13) and the 150..3000 Hz bandpass; sampled
+    chains' audio (NoiseFilter output, int16) vs the oracle, one chain without NR alongside."""
+    from openwebrx_amd import synth
+    fs = 10000000
+    modes = ["usb"] * 65
+    n = 1 << 21
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, "usb", output=amd._lib.OUT_S16, nr_enabled=c < 64,
+                                     nr_threshold=10) for c, o in enumerate(offs)]
+    eng, chains = _run_chains(amd, iq, fs, plist, 1 << 19)
+    for c in (0, 37, 63, 64):
+        ref = oracle.stages(iq, plist[c])
+        s16 = np.frombuffer(chains[c].read_audio(), np.int16)
+        assert s16.size == ref["s16"].size and s16.size > 1000, (c, s16.size, ref["s16"].size)
+        d = np.abs(s16.astype(np.int32) - ref["s16"])
+        assert np.mean(d <= 1) > 0.999, (c, np.mean(d <= 1), d.max())
+        if c < 64:
+            assert "nr" in ref
+    eng.close()
+
+
+def test_noise_filter_float_and_reset(amd):
+    """NoiseFilter float output (OUT_F32) within 1e-5 rel-RMS of the oracle; switching it off
+    and on (a fresh NoiseFilter, clientaudio.py:80-90) restarts its state."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    iq, offs = synth.make_iq(fs, 1 << 20, ["nfm"])
+    p = amd.params.chain_params(fs, offs[0], "nfm", output=amd._lib.OUT_F32, nr_enabled=True,
+                                nr_threshold=5)
+    eng, (ch,) = _run_chains(amd, iq, fs, [p], 1 << 18)
+    got = np.frombuffer(ch.read_audio(), np.float32)
+    ref = oracle.stages(iq, p)
+    assert got.size == ref["nr"].size and got.size > 2000
+    assert rel_rms(got, ref["nr"]) < 1e-5
+    eng.close()

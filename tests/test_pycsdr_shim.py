@@ -247,6 +247,34 @@ def test_planner_wfm_chain(fs):
     _graph.finish(wide)
 
 
+def test_planner_noise_filter(tmp_path):
+    """ClientAudioChain(FLOAT, 12000, 12000, "adpcm", True, 10) = [NoiseFilter(10), Convert,
+    AdpcmEncoder] (recorded in tests/golden/chain_params.json "clientaudio_nr") fuses with
+    nr_enabled / nr_threshold (BASELINE config 5)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "chain_params.json")) as f:
+        rec = json.load(f)["clientaudio_nr"]
+    assert [e["module"] for e in rec if e["op"] == "new"] == ["NoiseFilter", "Convert",
+                                                              "AdpcmEncoder"]
+    thr = rec[0]["args"][0]
+    fs, off = 10000000, -250000
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    mods = selector(fs, off, "usb") + demodulator("usb") + [M.NoiseFilter(thr)] + client_audio()
+    ch = Chain(mods)
+    ch.setWriter(M.Buffer(Format.CHAR))
+    ch.setReader(wide.getReader())
+    kind, p, used = _graph.plan_segment(mods[0])
+    assert kind == "chain" and used == mods
+    got = _graph.chain_params_struct(p)
+    want = params.chain_params(fs, off, "usb", output=_lib.OUT_ADPCM, nr_enabled=True,
+                               nr_threshold=thr)
+    for name, _ in _lib.ChainParams._fields_:
+        assert getattr(got, name) == pytest.approx(getattr(want, name), rel=1e-6, abs=1e-12), name
+    assert got.nr_enabled == 1 and got.nr_threshold == 10.0
+    _graph.finish(wide)
+
+
 def test_unrecognised_graph_is_not_fused():
     wide = M.Buffer(Format.COMPLEX_FLOAT)
     shift = M.Shift(0.1)
