@@ -81,6 +81,41 @@ def cpu_baseline(fs, n_fft, hop, avg, plist, seconds_target=15.0):
                       % (n, n / fs, len(plist), threads, dt)}
 
 
+def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block):
+    """SURVEY.md 8d measurement 1: feed the stream at its nominal rate through the host push path
+    (SDR -> host cf32 -> PCIe -> HBM, owrx_push_iq) to a fresh engine with the same waterfall and
+    chains; every block is pushed on its wall-clock deadline, then synced and drained.  Keeps up
+    when no output ring overran and every block finished within its own period."""
+    eng = Engine(fs, max_block=block)
+    wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
+    chains = [eng.chain(p) for p in plist]
+    period = block / fs
+    nblocks = max(1, int(seconds / period))
+    lat = []
+    t0 = time.perf_counter()
+    for i in range(nblocks):
+        wait = t0 + i * period - time.perf_counter()
+        if wait > 0:
+            time.sleep(wait)
+        a = time.perf_counter()
+        eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
+        eng.sync()
+        for ch in chains:
+            ch.read_audio()
+            ch.read_smeter()
+        wf.read()
+        lat.append(time.perf_counter() - a)
+    st = eng.stats()
+    eng.close()
+    return {"seconds": round(nblocks * period, 2), "stream_msps": fs / 1e6, "chains": len(plist),
+            "blocks": nblocks, "block_period_ms": round(1e3 * period, 2),
+            "max_block_latency_ms": round(1e3 * max(lat), 3),
+            "mean_block_latency_ms": round(1e3 * sum(lat) / len(lat), 3),
+            "overruns": int(st["overruns"]),
+            "keeps_up": bool(st["overruns"] == 0 and max(lat) < period),
+            "path": "host cf32 -> owrx_push_iq (PCIe) -> engine, sync + drain per block"}
+
+
 def pmc_traffic(prefix):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc passes
@@ -105,6 +140,8 @@ def main():
     ap.add_argument("--chains", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-waterfall", action="store_true")
+    ap.add_argument("--realtime-seconds", type=float, default=3.0,
+                    help="paced real-time check at 10 Msps through the host push path (0: skip)")
     ap.add_argument("--no-timing", action="store_true",
                     help="skip the per-kernel HIP-event brackets (roofline fields become null)")
     args = ap.parse_args()
@@ -240,6 +277,11 @@ def main():
     wf_launches = s1["waterfall_launches"] - s0["waterfall_launches"]
 
     traffic, traffic_src = pmc_traffic("ddc_lds<")
+    rt = None
+    if rank == 0 and world == 1 and args.realtime_seconds > 0:
+        host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
+                            args.realtime_seconds, 1 << 20)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -289,6 +331,7 @@ def main():
                 "post": round(post_ms / args.steps, 3),
                 "waterfall_hbm_GBps": round(8.0 * samples / (wf_ms / 1e3) / 1e9, 1) if wf_ms > 0 else None,
             },
+            "realtime": rt,
             "cpu_baseline": cpu,
             "output_bytes": out_bytes,
         }
