@@ -309,6 +309,13 @@ ddc_lds(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end,
 }
 
 constexpr int kLdsR = 32;
+#ifndef OWRX_DDC_LDS_WPE
+#define OWRX_DDC_LDS_WPE 4
+#endif
+// waves-per-EU target of ddc_lds: 4 caps it at 128 VGPRs (132 at 2, i.e. 3 waves per SIMD);
+// the compiler then spills 8 VGPRs, all outside the chunk loop (prologue and the final wave
+// reduction).  Same-box A/B on MI355X: +4 % DDC TFLOP/s at 32 chains, +6 % at 256.
+constexpr int kLdsWpe = OWRX_DDC_LDS_WPE;
 
 
 
@@ -329,7 +336,7 @@ inline size_t ddc_lds_bytes(int P, int tpw, int R = kLdsR) {
     return win > red ? win : red;
 }
 
-template <int P, int WPE = 2, int R = kLdsR>
+template <int P, int WPE = kLdsWpe, int R = kLdsR>
 hipError_t launch_ddc_lds_p(const float2* blk, int64_t blk_start, int64_t blk_end,
                                    const float* taps_poly, const DdcChain* chains, int nchains,
                                    int D, int64_t k_begin, int nk, int nseg, float2* partial,
@@ -376,7 +383,7 @@ int ddc_occ(bool flat, int tpw) {
         ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
               &nb, reinterpret_cast<const void*>(&ddc_polyphase<P, 32, 2, 16>), 64 * kDdcWaves, 0)
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &nb, reinterpret_cast<const void*>(&ddc_lds<P, kLdsR, 2>), 64 * kDdcWaves,
+              &nb, reinterpret_cast<const void*>(&ddc_lds<P, kLdsR, kLdsWpe>), 64 * kDdcWaves,
               ddc_lds_bytes(P, tpw));
     if (e != hipSuccess) return 2;
     return nb > 0 ? nb : 1;
@@ -389,7 +396,7 @@ int ddc_occ(bool flat, int tpw) {
      int, float2*, hipStream_t)
 #define OWRX_DDC_INSTANTIATE(EXT, P)                                                         \
     EXT template hipError_t launch_ddc_p<P, 32, 2, 16> OWRX_DDC_SIG;                         \
-    EXT template hipError_t launch_ddc_lds_p<P, 2, kLdsR> OWRX_DDC_SIG;                      \
+    EXT template hipError_t launch_ddc_lds_p<P, kLdsWpe, kLdsR> OWRX_DDC_SIG;                      \
     EXT template int ddc_occ<P>(bool, int);
 #define OWRX_DDC_DEPTHS(X, EXT) X(EXT, 8) X(EXT, 16) X(EXT, 27) X(EXT, 28) X(EXT, 32) X(EXT, 48) X(EXT, 64)
 

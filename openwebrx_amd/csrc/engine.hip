@@ -60,7 +60,7 @@ hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts
 hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const int* idx,
                             int nlong, int64_t max_fd, int max_taps, hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
-                              int nsel, int output, int debug, hipStream_t st);
+                              int nsel, int output, int debug, int nr, hipStream_t st);
 hipError_t launch_chain_nr(const ChainPost* posts, int nposts, ChainCounts* counts,
                            hipStream_t st);
 hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, ChainCounts* counts,
@@ -72,6 +72,7 @@ constexpr int kWfFramesPerGroup = 1;  // the four-step FFT (N > kWfLdsMaxN) reli
 constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
 constexpr int kWfMaxN = 65536;
 constexpr int kBlMaxTaps = 4095;       // longest bandpass of the bp_long path (kernels_post.hip)
+constexpr int kSelPad = 64 * 4 * 6;    // serial lane lists: 64-lane padding per (output, NR, demod)
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
 constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
@@ -603,8 +604,8 @@ static int ensure_post_capacity(owrx_engine* e) {
         HIPCHK(dalloc(&s.d_posts, cap));
         HIPCHK(halloc(&s.h_posts, cap));
         // serial lane lists (+ demodulator-run padding), then the long-bandpass post list
-        HIPCHK(dalloc(&s.d_sel, (size_t)2 * cap + 64 * 4 * 4));
-        HIPCHK(halloc(&s.h_sel, (size_t)2 * cap + 64 * 4 * 4));
+        HIPCHK(dalloc(&s.d_sel, (size_t)2 * cap + kSelPad));
+        HIPCHK(halloc(&s.h_sel, (size_t)2 * cap + kSelPad));
         HIPCHK(dalloc(&s.d_counts, cap));
         HIPCHK(dalloc(&s.d_out, (size_t)e->out_total));
         HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
@@ -973,7 +974,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         // long-bandpass chains (indices after the serial lane lists in the sel buffer)
         int nlong = 0, long_taps = 0;
         int64_t long_fd = 0;
-        S.long_off = e->post_cap + 64 * 4 * 4;
+        S.long_off = e->post_cap + kSelPad;
         for (int i = 0; i < np; ++i)
             if (e->posts[i].bp_long && e->posts[i].output != OWRX_OUT_IQ) {
                 S.h_sel[S.long_off + nlong++] = i;
@@ -997,35 +998,41 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         // one post_serial_front launch per output format present (S16 / ADPCM / F32); within
         // a format the chains are ordered by demodulator and every demodulator's run is padded
         // to whole 64-lane workgroups (-1 = idle lane), so each wave has a uniform demodulator
-        int nsel[3] = {0, 0, 0}, off[3] = {0, 0, 0};
+        // lists per (output, NoiseFilter): a NoiseFilter chain's front stores for chain_nr
+        // instead of converting; the two ADPCM lists are adjacent (one chain_adpcm launch)
+        int nsel[3][2] = {}, off[3][2] = {};
         int nfill = 0;
-        for (int o = 0; o < 3; ++o) {
-            off[o] = nfill;
-            for (int dm = 0; dm < 4; ++dm) {
-                int run = 0;
-                for (int i = 0; i < np; ++i)
-                    if (e->posts[i].output == o && e->posts[i].demod == dm) {
-                        S.h_sel[nfill++] = i;
+        for (int o = 0; o < 3; ++o)
+            for (int nr = 0; nr < 2; ++nr) {
+                off[o][nr] = nfill;
+                for (int dm = 0; dm < 4; ++dm) {
+                    int run = 0;
+                    for (int i = 0; i < np; ++i)
+                        if (e->posts[i].output == o && e->posts[i].demod == dm &&
+                            (e->posts[i].nr_enabled != 0) == (nr != 0)) {
+                            S.h_sel[nfill++] = i;
+                            run++;
+                        }
+                    while (run % 64) {
+                        S.h_sel[nfill++] = -1;
                         run++;
                     }
-                while (run % 64) {
-                    S.h_sel[nfill++] = -1;
-                    run++;
                 }
+                nsel[o][nr] = nfill - off[o][nr];
             }
-            nsel[o] = nfill - off[o];
-        }
         HIPCHK(hipMemcpyAsync(S.d_sel, S.h_sel, sizeof(int) * nfill, hipMemcpyHostToDevice,
                               e->sB));
         const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
         for (int o = 0; o < 3; ++o)
-            HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o], nsel[o], o, dbg,
-                                      e->sB));
+            for (int nr = 0; nr < 2; ++nr)
+                HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o][nr],
+                                          nsel[o][nr], o, dbg, nr, e->sB));
         if (any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, e->sB));
         HIPCHK(hipEventRecord(S.evF, e->sB));
         // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host
         HIPCHK(hipStreamWaitEvent(e->sC, S.evF, 0));
-        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + off[1], nsel[1], e->sC));
+        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + off[1][0],
+                                  nsel[1][0] + nsel[1][1], e->sC));
         if (timed) HIPCHK(hipEventRecord(S.b1, e->sC));
         // the copies to host go on stream R (behind this block's encoder), so stream C runs
         // encoders back to back: its kernel is the pipeline's longest serial stage

@@ -595,7 +595,7 @@ OWRX_DEV SerLane ser_lane(const int* __restrict__ sel, int nsel) {
     return SerLane{cs >= 0 ? cs : c0, cs >= 0};
 }
 
-template <int OUT, bool DEBUG>
+template <int OUT, bool DEBUG, bool NR>
 __global__ void __launch_bounds__(kFrontThreads)
 post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
                   const int* __restrict__ sel, int nsel) {
@@ -691,7 +691,9 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     } else {
         // ---- gain + Convert (waves 1..3 take every third sample), one chunk behind; a chain
         // with a NoiseFilter stores the AGC output for chain_nr instead (Convert follows it)
-        const bool nr = sl.active && Pp->nr_enabled;
+        // NR: this launch's chains all run a NoiseFilter (the host groups them), so the
+        // per-sample store below is not a divergent branch
+        const bool nr = NR && sl.active;
         const int nr_fill = nr ? kNrHop + Pp->nr_state->pend : 0;
         for (int it = 0; it < nchunks + 1; ++it) {
             const int ch = it - 1;
@@ -711,7 +713,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     }
                     const int64_t qi = base + j;
                     const bool valid = sl.active && (full || qi < n);
-                    if (nr) {
+                    if (NR) {
                         if (valid) gp(Pp->nr_in)[nr_fill + qi] = a;
                     } else if (OUT == 2) {
                         if (valid && 4 * qi + 4 <= Pp->out_cap) gp(reinterpret_cast<float*>(Pp->out))[qi] = a;
@@ -914,19 +916,22 @@ hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const i
 }
 
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
-                              int nsel, int output, int debug, hipStream_t st) {
+                              int nsel, int output, int debug, int nr, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
     const dim3 g((nsel + 63) / 64), b(kFrontThreads);
-    switch (output * 2 + (debug ? 1 : 0)) {
-        case 0: hipLaunchKernelGGL((post_serial_front<0, false>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 1: hipLaunchKernelGGL((post_serial_front<0, true>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 2: hipLaunchKernelGGL((post_serial_front<1, false>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 3: hipLaunchKernelGGL((post_serial_front<1, true>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 4: hipLaunchKernelGGL((post_serial_front<2, false>), g, b, 0, st, posts, counts, sel, nsel); break;
-        case 5: hipLaunchKernelGGL((post_serial_front<2, true>), g, b, 0, st, posts, counts, sel, nsel); break;
-        default: return hipErrorInvalidValue;
+#define OWRX_FRONT(O, D, N)                                                                  \
+    if (output == O && (debug != 0) == D && (nr != 0) == N) {                                \
+        hipLaunchKernelGGL((post_serial_front<O, D, N>), g, b, 0, st, posts, counts, sel, nsel); \
+        return hipGetLastError();                                                            \
     }
-    return hipGetLastError();
+#define OWRX_FRONT_O(O) \
+    OWRX_FRONT(O, false, false) OWRX_FRONT(O, true, false) OWRX_FRONT(O, false, true) OWRX_FRONT(O, true, true)
+    OWRX_FRONT_O(0)
+    OWRX_FRONT_O(1)
+    OWRX_FRONT_O(2)
+#undef OWRX_FRONT_O
+#undef OWRX_FRONT
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,

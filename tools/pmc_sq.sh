@@ -10,6 +10,6 @@ i=0
 for grp in "$@"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc_${R}_$i -o pmc \
-    -- python -u bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-timing > gpurun_out/${R}_pmc_$i.log 2>&1
+    -- python -u bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-timing --realtime-seconds 0 > gpurun_out/${R}_pmc_$i.log 2>&1
   rc=$?; echo "pmc [$grp] rc=$rc" >> gpurun_out/${R}_pmc_$i.log; [ $rc -eq 0 ] || exit $rc
 done
