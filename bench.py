@@ -5,6 +5,9 @@ Workload (N=1): BASELINE config 2 -- 10 Msps synthetic cf32 IQ -> 16384-bin wate
 (FftChain: fps 9, v-overlap 0.3 -> avg 97, hop 11454, ADPCM rows) + 32 client chains
 (16 NFM + 16 AM ClientDemodulatorChain: Shift -> FirDecimate(833, 22223 taps) ->
 FractionalDecimator -> Bandpass -> Squelch -> demod -> Agc -> Convert -> AdpcmEncoder(sync)).
+`--config c3|c4|c5` runs the other BASELINE shapes per GPU (256 NFM/USB/CW chains; 61.44 Msps
+with a 65536-bin waterfall and 128 chains; 64 USB chains with NoiseFilter) for reference; the
+metric line is config 2.
 A step is one block of `--block` IQ samples pushed through all of it, inputs resident in HBM,
 outputs (waterfall rows, ADPCM audio, s-meter) copied back to host rings and drained.
 
@@ -25,6 +28,19 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "IQ Msamples/s ingested + concurrent demod chains @ real-time, 1/2/4/8 GPU"
+# BASELINE.json configs (per GPU): sample rate, waterfall bins, chains, chain modes, NoiseFilter
+CONFIGS = {
+    "c2": dict(fs=10000000, n_fft=16384, chains=32, modes=("nfm", "am"), nr=False,
+               label="C2: 10 Msps cf32 IQ -> 16384-bin waterfall + %d NFM/AM chains per GPU"),
+    "c3": dict(fs=10000000, n_fft=16384, chains=256, modes=("nfm", "usb", "cw"), nr=False,
+               label="C3: 10 Msps cf32 IQ -> 16384-bin waterfall + %d NFM/USB/CW chains per GPU"),
+    "c4": dict(fs=61440000, n_fft=65536, chains=128, modes=("nfm", "am", "usb", "cw"), nr=False,
+               label="C4 (per GPU of 8): 61.44 Msps cf32 IQ -> 65536-bin waterfall + %d mixed "
+                     "chains per GPU"),
+    "c5": dict(fs=10000000, n_fft=16384, chains=64, modes=("usb",), nr=True,
+               label="C5: 10 Msps cf32 IQ -> 16384-bin waterfall + %d USB chains with "
+                     "NoiseFilter(10) per GPU"),
+}
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector
 HBM_PEAK_GBS = 8000.0
 
@@ -44,6 +60,9 @@ def gen_stream_torch(torch, dev, fs, n, modes, offsets, seed=20251114, chunk=1 <
             if mode == "nfm":
                 ph = 2 * np.pi * f * t + 2.5 * torch.sin(2 * np.pi * 1000.0 * t)
                 x += (0.05 * torch.exp(1j * ph)).to(torch.complex64)
+            elif mode in ("usb", "cw"):
+                tone = 1000.0 if mode == "usb" else 800.0
+                x += (0.05 * torch.exp(2j * np.pi * (f + tone) * t)).to(torch.complex64)
             else:  # am
                 env = 0.05 * (1.0 + 0.3 * torch.sin(2 * np.pi * 1000.0 * t))
                 x += (env * torch.exp(2j * np.pi * f * t)).to(torch.complex64)
@@ -137,7 +156,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--block", type=int, default=1 << 22)
-    ap.add_argument("--chains", type=int, default=32)
+    ap.add_argument("--chains", type=int, default=None,
+                    help="chains per GPU (default: the config's)")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
+                    help="BASELINE.json config shape (c2 is the metric's; the others are "
+                         "reported for reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-waterfall", action="store_true")
     ap.add_argument("--realtime-seconds", type=float, default=3.0,
@@ -164,11 +187,12 @@ def main():
     torch.cuda.set_device(dev)
 
     from openwebrx_amd import Engine, params
-    fs = 10000000
-    n_fft = 16384
+    cfg = CONFIGS[args.config]
+    fs = cfg["fs"]
+    n_fft = cfg["n_fft"]
     avg, hop = params.fft_parameters(fs, n_fft, 9, 0.3)
-    C = args.chains
-    modes = ["nfm" if c % 2 == 0 else "am" for c in range(C)]
+    C = args.chains if args.chains is not None else cfg["chains"]
+    modes = [cfg["modes"][c % len(cfg["modes"])] for c in range(C)]
     from openwebrx_amd.synth import carrier_offsets
     offs = carrier_offsets(fs, C)
     # the job's chains: C per GPU (weak scaling), copy r listening 37 Hz * r off the carriers
@@ -176,7 +200,8 @@ def main():
     from openwebrx_amd.multi import IqBroadcast, shard_chains
     everything = [(o + 37 * r, m) for r in range(world) for o, m in zip(offs, modes)]
     mine = shard_chains(everything, world, rank, key=lambda it: it[1])
-    plist = [params.chain_params(fs, o, m) for o, m in mine]
+    plist = [params.chain_params(fs, o, m, nr_enabled=cfg["nr"], nr_threshold=10)
+             for o, m in mine]
 
     block = args.block
     eng = Engine(fs, max_block=block, device=local)
@@ -284,7 +309,7 @@ def main():
                             args.realtime_seconds, 1 << 20)
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             cpu = cpu_baseline(fs, n_fft, hop, avg, plist)
         res = {
             "metric": METRIC,
@@ -300,16 +325,16 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": "C2: 10 Msps cf32 IQ -> 16384-bin waterfall (avg %d, hop %d, ADPCM) "
-                            "+ %d NFM/AM chains per GPU (D=%d, %d taps, frac %.6f, bandpass, "
-                            "squelch, AGC, ADPCM audio)" % (avg, hop, C, D, T, frac),
+                "workload": (cfg["label"] % C) + " (waterfall avg %d, hop %d, ADPCM rows; chains "
+                            "D=%d, %d taps, frac %.6f, bandpass, squelch, AGC, ADPCM audio)"
+                            % (avg, hop, D, T, frac),
                 "samp_rate": fs, "fft_size": n_fft, "chains_per_gpu": C,
                 "block_samples": block,
                 "parallelism": "1 GPU" if world == 1 else
                 "IQ broadcast over RCCL from rank 0, %d chains per rank" % C,
             },
             "iq_msps_stream": round(samples / dt / 1e6, 2),
-            "realtime_factor_10msps": round(samples / dt / fs, 1),
+            "realtime_factor": round(samples / dt / fs, 1),
             "chains_total": C * world,
             "roofline": {
                 "bound": "valu",
