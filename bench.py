@@ -346,7 +346,10 @@ def main():
                 "traffic": traffic,
                 "note": "algorithmic flops per launch = chains*outputs*(4*taps+6*D); average launch "
                         "time from HIP events on the engine stream; FP32 vector peak (the DDC is a "
-                        "1-D stencil on VALU, SURVEY.md 8d; no MFMA by design). traffic = HBM "
+                        "1-D stencil on VALU, SURVEY.md 8d; no MFMA by design). The event bracket "
+                        "also holds the dispatch gaps around the launch, so it runs ~10 % above "
+                        "the rocprofv3 kernel average (profiles/r01_bench_kernel_stats_v50.csv: "
+                        "219 us vs 247 us): achieved is conservative. traffic = HBM "
                         "bytes per launch from separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
                         "and WRITE_SIZE passes, " + traffic_src,
             },
