@@ -244,7 +244,12 @@ def main():
             host_s["process"] += time.perf_counter() - t0
         else:  # the one exchange step: rank 0's block to every rank over RCCL
             t, off = bcast.step(i)
-            torch.cuda.synchronize(dev)
+            # wait for this broadcast only (an event behind it on torch's stream), not for the
+            # device: the engine's own streams keep blocks i-1 .. i-3 in flight meanwhile, and
+            # the next broadcast overlaps block i (its window was released by this call)
+            arrived = torch.cuda.Event()
+            arrived.record()
+            arrived.synchronize()
             eng.process_device(t.data_ptr() + 8 * off, block)
         return drain()
 
