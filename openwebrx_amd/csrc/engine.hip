@@ -1179,9 +1179,14 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
             hipEventCreateWithFlags(&s.evF, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.evB, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&s.evC, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreate(&s.a0) != hipSuccess || hipEventCreate(&s.a1) != hipSuccess ||
-            hipEventCreate(&s.a2) != hipSuccess || hipEventCreate(&s.a3) != hipSuccess ||
-            hipEventCreate(&s.b0) != hipSuccess || hipEventCreate(&s.b1) != hipSuccess)
+            // timing-only events: no system-scope fence, so the markers bracketing a kernel
+            // do not add cache write-backs to the interval they measure
+            hipEventCreateWithFlags(&s.a0, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.a1, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.a2, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.a3, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.b0, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.b1, hipEventDisableSystemFence) != hipSuccess)
             return fail("event");
     }
     for (int i = 0; i < 2; ++i)
