@@ -600,6 +600,9 @@ __global__ void __launch_bounds__(kFrontThreads)
 post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
                   const int* __restrict__ sel, int nsel) {
     __shared__ float2 ue[2][kSerChunk][64];  // wave 0 -> waves 1, 2: (u, envelope)
+    __shared__ float as_[2][kSerChunk][65];  // waves 1-3: AGC output, [sample][chain], padded
+    __shared__ int64_t s_lim[64];            // per chain: samples to store (0: inactive lane)
+    __shared__ void* s_ptr[64];              // per chain: destination of sample 0
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const SerLane sl = ser_lane(sel, nsel);
@@ -671,7 +674,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             if (ch < nfull) run(dm, std::true_type{}, ch);
             else run(dm, std::false_type{}, ch);
         };
-        for (int it = 0; it < nchunks + 1; ++it) {
+        for (int it = 0; it < nchunks + 2; ++it) {
             if (it < nchunks) {
                 if (demod == 0) run_dm(std::integral_constant<int, 0>{}, it);
                 else if (demod == 1) run_dm(std::integral_constant<int, 1>{}, it);
@@ -690,14 +693,36 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
         }
     } else {
         // ---- gain + Convert (waves 1..3 take every third sample), one chunk behind; a chain
-        // with a NoiseFilter stores the AGC output for chain_nr instead (Convert follows it)
-        // NR: this launch's chains all run a NoiseFilter (the host groups them), so the
-        // per-sample store below is not a divergent branch
-        const bool nr = NR && sl.active;
-        const int nr_fill = nr ? kNrHop + Pp->nr_state->pend : 0;
-        for (int it = 0; it < nchunks + 1; ++it) {
+        // with a NoiseFilter stores the AGC output for chain_nr instead (Convert follows it).
+        // The results go through LDS (as_) and are written out one more chunk behind,
+        // transposed: lane = sample, so each chain's chunk is one contiguous store per wave
+        // instead of 64 lanes touching 64 chains' cache lines per sample.
+        if (wave == 1) {
+            const bool nr = NR && sl.active;
+            const int64_t nr_fill = nr ? kNrHop + Pp->nr_state->pend : 0;
+            int64_t lim = 0;
+            void* dptr = nullptr;
+            if (sl.active) {
+                if (NR) {
+                    lim = n;
+                    dptr = Pp->nr_in + nr_fill;
+                } else if (OUT == 2) {
+                    lim = min((int64_t)n, Pp->out_cap / 4);
+                    dptr = Pp->out;
+                } else if (OUT == 0) {
+                    lim = min((int64_t)n, Pp->out_cap / 2);
+                    dptr = Pp->out;
+                } else {
+                    lim = INT64_MAX;  // the ADPCM scratch's slack covers the ragged chunk
+                    dptr = Pp->s16;
+                }
+            }
+            s_lim[lane] = lim;
+            s_ptr[lane] = dptr;
+        }
+        for (int it = 0; it < nchunks + 2; ++it) {
             const int ch = it - 1;
-            if (ch >= 0) {
+            if (ch >= 0 && ch < nchunks) {
                 const int base = ch * kSerChunk;
                 const float2(*srcu)[64] = ue[ch & 1];
                 const bool full = ch < nfull;
@@ -711,21 +736,27 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                         if (g > agcp.max_gain) g = agcp.max_gain;
                         a = g * q.x;
                     }
-                    const int64_t qi = base + j;
-                    const bool valid = sl.active && (full || qi < n);
-                    if (NR) {
-                        if (valid) gp(Pp->nr_in)[nr_fill + qi] = a;
-                    } else if (OUT == 2) {
-                        if (valid && 4 * qi + 4 <= Pp->out_cap) gp(reinterpret_cast<float*>(Pp->out))[qi] = a;
-                    } else if (OUT == 0) {
-                        if (valid && 2 * qi + 2 <= Pp->out_cap)
-                            gp(reinterpret_cast<int16_t*>(Pp->out))[qi] = convert_s16(a);
-                    } else if (sl.active) {
-                        gp(Pp->s16)[qi] = convert_s16(a);  // slack covers the ragged chunk
+                    as_[ch & 1][j][lane] = a;
+                    if (DEBUG) {
+                        const int64_t qi = base + j;
+                        const bool valid = sl.active && (full || qi < n);
+                        if (valid && qi < Pp->dbg_cap) {
+                            gp(Pp->dbg_dem)[qi] = q.x;
+                            gp(Pp->dbg_agc)[qi] = a;
+                        }
                     }
-                    if (DEBUG && valid && qi < Pp->dbg_cap) {
-                        gp(Pp->dbg_dem)[qi] = q.x;
-                        gp(Pp->dbg_agc)[qi] = a;
+                }
+            }
+            const int w = it - 2;  // chunk written out this iteration (as_ complete since the
+            if (w >= 0) {          // previous barrier)
+                const float(*src)[65] = as_[w & 1];
+                const int64_t qi = (int64_t)w * kSerChunk + lane;
+                for (int cc = wave - 1; cc < 64; cc += kFrontThreads / 64 - 1) {
+                    const int64_t lim = s_lim[cc];
+                    if (qi < lim) {
+                        const float a = src[lane][cc];
+                        if (NR || OUT == 2) gp(reinterpret_cast<float*>(s_ptr[cc]))[qi] = a;
+                        else gp(reinterpret_cast<int16_t*>(s_ptr[cc]))[qi] = convert_s16(a);
                     }
                 }
             }
