@@ -45,28 +45,18 @@ FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector
 HBM_PEAK_GBS = 8000.0
 
 
-def gen_stream_torch(torch, dev, fs, n, modes, offsets, seed=20251114, chunk=1 << 22):
-    """Same signal model as openwebrx_amd.synth (AWGN 0.01 + one carrier per chain), generated
-    on the GPU in float64 phase / float32 samples (bench data only)."""
+def gen_stream_torch(torch, dev, fs, n, modes, offsets, seed=20251114):
+    """Same signal model as openwebrx_amd.synth (AWGN 0.01 + one carrier per chain), generated on
+    the GPU by the library's synthetic source (owrx_synth_iq: one kernel per 2^24 samples; bench
+    data only)."""
+    from openwebrx_amd import _lib
     out = torch.empty(n, dtype=torch.complex64, device=dev)
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    for s in range(0, n, chunk):
-        m = min(chunk, n - s)
-        x = torch.complex(torch.randn(m, generator=g, device=dev) * 0.01,
-                          torch.randn(m, generator=g, device=dev) * 0.01)
-        t = (torch.arange(m, dtype=torch.float64, device=dev) + s) / fs
-        for mode, f in zip(modes, offsets):
-            if mode == "nfm":
-                ph = 2 * np.pi * f * t + 2.5 * torch.sin(2 * np.pi * 1000.0 * t)
-                x += (0.05 * torch.exp(1j * ph)).to(torch.complex64)
-            elif mode in ("usb", "cw"):
-                tone = 1000.0 if mode == "usb" else 800.0
-                x += (0.05 * torch.exp(2j * np.pi * (f + tone) * t)).to(torch.complex64)
-            else:  # am
-                env = 0.05 * (1.0 + 0.3 * torch.sin(2 * np.pi * 1000.0 * t))
-                x += (env * torch.exp(2j * np.pi * f * t)).to(torch.complex64)
-        out[s:s + m] = x
+    code = {"nfm": 0, "am": 1, "usb": 2, "cw": 3, "lsb": 4}
+    offs = np.asarray(offsets, np.float64)
+    mds = np.asarray([code[m] for m in modes], np.int32)
+    _lib.check(_lib.lib.owrx_synth_iq(dev.index or 0, out.data_ptr(), n, 0, float(fs), len(mds),
+                                      offs.ctypes.data, mds.ctypes.data, seed, 0.01, 0.05),
+               "owrx_synth_iq")
     return out
 
 
@@ -119,9 +109,7 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
         a = time.perf_counter()
         eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
         eng.sync()
-        for ch in chains:
-            ch.read_audio()
-            ch.read_smeter()
+        eng.read_chains(chains)
         wf.read()
         lat.append(time.perf_counter() - a)
     st = eng.stats()
@@ -135,14 +123,14 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             "path": "host cf32 -> owrx_push_iq (PCIe) -> engine, sync + drain per block"}
 
 
-def pmc_traffic(prefix):
-    """HBM bytes per launch of a kernel from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from rocprofv3 --pmc passes
-    of this same bench command); (None, reason) when absent."""
+def pmc_traffic(prefix, config):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary OF THIS CONFIG
+    (profiles/*_pmc_traffic_<config>.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
+    passes of this same bench command); (None, reason) when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_%s.json" % config)))
     if not files:
-        return None, "no PMC summary committed"
+        return None, "no PMC summary committed for config %s" % config
     d = json.load(open(files[-1]))
     for k, v in d["kernels"].items():
         if k.startswith(prefix):
@@ -158,9 +146,9 @@ def main():
     ap.add_argument("--block", type=int, default=1 << 22)
     ap.add_argument("--chains", type=int, default=None,
                     help="chains per GPU (default: the config's)")
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS),
-                    help="BASELINE.json config shape (c2 is the metric's; the others are "
-                         "reported for reference)")
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="BASELINE.json config shape (c3, the largest single-GPU config, is the "
+                         "metric's; the others are reported for reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-waterfall", action="store_true")
     ap.add_argument("--realtime-seconds", type=float, default=3.0,
@@ -226,10 +214,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     def drain():
-        nbytes = 0
-        for ch in chains:
-            nbytes += len(ch.read_audio())
-            ch.read_smeter()
+        # every chain's audio and s-meter values in two native calls (a one-thread server pump)
+        audio, _, _, _ = eng.read_chains(chains)
+        nbytes = int(audio.size)
         if wf is not None:
             nbytes += len(wf.read())
         return nbytes
@@ -296,22 +283,30 @@ def main():
     samples = args.steps * block
     value = world * samples / dt / 1e6
     ms_step = dt * 1e3 / args.steps
-    # DDC roofline (dominant kernel): algorithmic flops per launch = C * nk * (4T + 6D)
+    # DDC work: the fast-convolution GEMM (fc_mac) is the dominant kernel of the chain path;
+    # achieved = its algorithmic flop per launch / its average launch time (HIP events on the
+    # engine's stream A, around that kernel only)
     D, frac, tbw, cutoff = params.decimation(fs, 12000)
     T = int(4.0 / float(np.float32(tbw)))
     T += 1 - (T % 2)
-    launches = s1["ddc_launches"] - s0["ddc_launches"]
-    ddc_ms = s1["gpu_ms_ddc"] - s0["gpu_ms_ddc"]
-    nk_total = (s1["ddc_outputs"] - s0["ddc_outputs"]) / max(1, C)
-    flops = C * nk_total * (4.0 * T + 6.0 * D)
-    avg_launch_s = ddc_ms / 1e3 / max(1, launches)
-    achieved_tf = (flops / max(1, launches) / avg_launch_s / 1e12
-                   if launches and avg_launch_s > 0 else 0.0)
-    wf_ms = s1["gpu_ms_waterfall"] - s0["gpu_ms_waterfall"]
-    post_ms = s1["gpu_ms_post"] - s0["gpu_ms_post"]
-    wf_launches = s1["waterfall_launches"] - s0["waterfall_launches"]
+    d = {k: s1[k] - s0[k] for k in s1}
+    launches = d["ddc_launches"]
+    ddc_ms = d["gpu_ms_ddc"]
+    nk_total = d["ddc_outputs"] / max(1, C)
+    direct_flops = C * nk_total * (4.0 * T + 6.0 * D)   # the direct form's count
+    mac_ms = d["gpu_ms_ddc_mac"]
+    fast = d["ddc_fast_launches"] == launches and launches > 0
+    if fast and mac_ms > 0:
+        achieved_tf = d["ddc_mac_flop"] / (mac_ms / 1e3) / 1e12
+        mac_gbs = d["ddc_mac_bytes"] / (mac_ms / 1e3) / 1e9
+    else:
+        achieved_tf = direct_flops / (ddc_ms / 1e3) / 1e12 if ddc_ms > 0 else 0.0
+        mac_gbs = None
+    wf_ms = d["gpu_ms_waterfall"]
+    post_ms = d["gpu_ms_post"]
+    wf_launches = d["waterfall_launches"]
 
-    traffic, traffic_src = pmc_traffic("ddc_lds<")
+    traffic, traffic_src = pmc_traffic("fc_mac<" if fast else "ddc_lds<", args.config)
     rt = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
@@ -319,7 +314,7 @@ def main():
                             args.realtime_seconds, 1 << 20)
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1 and args.config == "c2":
+        if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(fs, n_fft, hop, avg, plist)
         res = {
             "metric": METRIC,
@@ -348,28 +343,48 @@ def main():
             "realtime_factor": round(samples / dt / fs, 1),
             "chains_total": C * world,
             "roofline": {
-                "bound": "valu",
-                "kernel": "ddc_lds (fused Shift + FirDecimate, all chains of the group)",
+                "bound": "mfma" if fast else "valu",
+                "kernel": ("fc_mac: the fast-convolution DDC's per-bin complex GEMM (frames x "
+                           "chains x branches) on v_mfma_f32_16x16x4_f32" if fast else
+                           "ddc_lds (direct polyphase Shift + FirDecimate)"),
                 "achieved": round(achieved_tf, 3),
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "note": "algorithmic flops per launch = chains*outputs*(4*taps+6*D); average launch "
-                        "time from HIP events on the engine stream; FP32 vector peak (the DDC is a "
-                        "1-D stencil on VALU, SURVEY.md 8d; no MFMA by design). The event bracket "
-                        "also holds the dispatch gaps around the launch, so it runs ~10 % above "
-                        "the rocprofv3 kernel average (profiles/r01_bench_kernel_stats_v50.csv: "
-                        "219 us vs 247 us): achieved is conservative. traffic = HBM "
-                        "bytes per launch from separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) "
-                        "and WRITE_SIZE passes, " + traffic_src,
+                "algorithmic_bytes_per_launch": (round(d["ddc_mac_bytes"] / max(1, launches))
+                                                 if fast else None),
+                "achieved_hbm_GBps": round(mac_gbs, 1) if mac_gbs else None,
+                "hbm_frac": round(mac_gbs / HBM_PEAK_GBS, 4) if mac_gbs else None,
+                "note": "achieved = algorithmic flop per launch (8 per complex MAC over the frames "
+                        "that carry outputs: 8 M Dp C F) / average launch time from HIP events "
+                        "around the kernel on the engine stream; peak = f32 MFMA = f32 vector "
+                        "(MI355X_MICROARCH.md).  Its operands stream once per launch (filter "
+                        "spectra W, branch spectra U, products Y: algorithmic_bytes_per_launch), "
+                        "so the HBM fraction is given beside it.  traffic = HBM bytes per launch "
+                        "from separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE "
+                        "passes of this config: " + traffic_src,
+            },
+            "ddc": {
+                "form": "fast convolution" if fast else "direct",
+                "gpu_ms_per_step": round(ddc_ms / args.steps, 4),
+                "direct_form_equivalent_TFLOPs": round(direct_flops / (ddc_ms / 1e3) / 1e12, 2)
+                if ddc_ms > 0 else None,
+                "note": "the whole DDC (branch DFTs + GEMM + inverse DFTs and rotators) against the "
+                        "flop count of the direct form it replaces (C outputs (4T + 6D), SURVEY "
+                        "8d): what the same outputs would need at that rate",
             },
             "kernels_ms_per_step": {
                 "ddc": round(ddc_ms / args.steps, 3),
+                "ddc_mac": round(mac_ms / args.steps, 3),
                 "waterfall": round(wf_ms / args.steps, 3),
-                "post": round(post_ms / args.steps, 3),
+                "post_stream_a": round(post_ms / args.steps, 3),
+                "post_to_encoder_end": round(d["gpu_ms_serial"] / args.steps, 3),
                 "waterfall_hbm_GBps": round(8.0 * samples / (wf_ms / 1e3) / 1e9, 1) if wf_ms > 0 else None,
             },
+            "host_ms_per_step": {k[8:]: round(d[k] / args.steps, 3) for k in
+                                 ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots",
+                                  "host_ms_wait_rows")},
             "realtime": rt,
             "cpu_baseline": cpu,
             "output_bytes": out_bytes,

@@ -152,6 +152,14 @@ int owrx_chain_set_noise_filter(owrx_engine* e, int handle, int enabled, float t
 int64_t owrx_chain_read_audio(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes);
 /* Squelch power writer values (owrx/connection.py:483-489) */
 int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t max_values);
+/* Batched forms for a server pump that serves many clients from one thread (the reference runs
+ * one pump thread per output, owrx/dsp.py:846-863): chain handles[i]'s available bytes / values
+ * are appended to dst in order until max_bytes / max_values; lens[i] / counts[i] receive each
+ * chain's share.  Returns the total. */
+int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
+                               int64_t max_bytes, int64_t* lens);
+int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float* dst,
+                                int64_t max_values, int64_t* counts);
 /* Secondary FFT of the chain's Selector output: ClientDemodulatorChain._createSecondaryFftChain
  * (owrx/dsp.py:220-225) = FftChain(selectorOutputRate, digimodes_fft_size, 0.3, 9, "adpcm")
  * reading selectorBuffer, i.e. Fft(size, every_n_samples) -> LogAveragePower(add_db, size,
@@ -187,13 +195,31 @@ typedef struct {
     int64_t overruns;          /* host output ring drops */
     double  gpu_ms_ddc;        /* HIP-event time of the DDC kernels (when timing enabled) */
     double  gpu_ms_waterfall;
-    double  gpu_ms_post;
+    double  gpu_ms_post;       /* stream A's post kernels (post_parallel, bp_long, chain_sfft) */
     int64_t ddc_launches;
     int64_t waterfall_launches;
+    int64_t ddc_fast_launches; /* of ddc_launches: fast-convolution form (OWRX_DDC_FAST) */
+    double  gpu_ms_ddc_mac;    /* HIP-event time of the fast form's GEMM (fc_mac), timed blocks */
+    double  ddc_mac_flop;      /* its algorithmic flop (8 per complex MAC, frames with outputs) */
+    double  ddc_mac_bytes;     /* its algorithmic bytes: filter spectra W + branch spectra U + Y */
+    double  gpu_ms_serial;     /* post_parallel start -> encoder end (streams A, B, C) */
+    double  host_ms_process;   /* host time inside block processing, of which waiting for: */
+    double  host_ms_wait_input;/*   the previous block's stream-A work (input / descriptors) */
+    double  host_ms_wait_slots;/*   block k - 4's chain outputs (the pipeline depth) */
+    double  host_ms_wait_rows; /*   the oldest waterfall row slot */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* 1 => record HIP events around each kernel group on the engine's streams */
 int owrx_set_timing(owrx_engine* e, int enable);
+/* Form of the fused Shift + FirDecimate (csdr/chain/selector.py:11-35, :95, :132-140) every
+ * chain group runs from the next block on.  Both compute y[k] = sum_t h[t] x[kD+t] e^{j phase}
+ * exactly (fp32 rounding apart):
+ *   OWRX_DDC_FAST   polyphase branches convolved through M-point DFTs, the per-chain filter
+ *                   spectra applied as one f32-MFMA complex GEMM per bin (default)
+ *   OWRX_DDC_DIRECT the direct polyphase FIR (4T + 6D flop per output and chain) */
+#define OWRX_DDC_FAST 0
+#define OWRX_DDC_DIRECT 1
+int owrx_set_ddc_mode(owrx_engine* e, int mode);
 
 /* ---- single-module runners (pycsdr module granularity, stateful, host buffers) -----------
  * Used by pycsdr.modules classes that run outside a fused chain and by the per-module parity
@@ -218,6 +244,15 @@ int owrx_module_destroy(owrx_module* m);
 /* in: n input items (cf32 for demods, f32, s16 for ADPCM); out: capacity in bytes */
 int64_t owrx_module_process(owrx_module* m, const void* in, int64_t n, void* out,
                             int64_t out_cap_bytes);
+
+/* ---- synthetic test source (benchmarks / tests; SURVEY.md 8d signal model) ---------------
+ * Writes n cf32 samples of the stream starting at absolute sample `start` into device memory:
+ * complex AWGN (sigma `noise`) + one carrier per entry of offsets_hz with modes[c] 0 NFM (1 kHz,
+ * 2.5 kHz deviation), 1 AM (30 %, 1 kHz), 2 USB (+1 kHz tone), 3 CW (+800 Hz), 4 LSB (-1 kHz),
+ * amplitude `amp`.  Synchronous.  Stands in for the SDR source (owrx/source/__init__.py:307-330). */
+int owrx_synth_iq(int device, float* dst_dev, int64_t n, int64_t start, double samp_rate,
+                  int ncarriers, const double* offsets_hz, const int* modes, uint64_t seed,
+                  float noise, float amp);
 
 #ifdef __cplusplus
 }

@@ -81,6 +81,15 @@ class Stats(ctypes.Structure):
         ("gpu_ms_post", ctypes.c_double),
         ("ddc_launches", ctypes.c_int64),
         ("waterfall_launches", ctypes.c_int64),
+        ("ddc_fast_launches", ctypes.c_int64),
+        ("gpu_ms_ddc_mac", ctypes.c_double),
+        ("ddc_mac_flop", ctypes.c_double),
+        ("ddc_mac_bytes", ctypes.c_double),
+        ("gpu_ms_serial", ctypes.c_double),
+        ("host_ms_process", ctypes.c_double),
+        ("host_ms_wait_input", ctypes.c_double),
+        ("host_ms_wait_slots", ctypes.c_double),
+        ("host_ms_wait_rows", ctypes.c_double),
     ]
 
 
@@ -128,6 +137,10 @@ PROTOTYPES = {
     "owrx_chain_read_debug": (_i64, [_vp, _i32, _i32, _vp, _i64]),
     "owrx_get_stats": (_i32, [_vp, ctypes.POINTER(Stats)]),
     "owrx_set_timing": (_i32, [_vp, _i32]),
+    "owrx_set_ddc_mode": (_i32, [_vp, _i32]),
+    "owrx_synth_iq": (_i32, [_i32, _vp, _i64, _i64, _f64, _i32, _vp, _vp, ctypes.c_uint64, _f32, _f32]),
+    "owrx_chains_read_audio": (_i64, [_vp, _i32, _pi32, _vp, _i64, _pi64]),
+    "owrx_chains_read_smeter": (_i64, [_vp, _i32, _pi32, _vp, _i64, _pi64]),
     "owrx_module_create": (_i32, [_i32, _i32, _f64, _f64, _f64, ctypes.POINTER(_vp)]),
     "owrx_module_destroy": (_i32, [_vp]),
     "owrx_module_process": (_i64, [_vp, _vp, _i64, _vp, _i64]),

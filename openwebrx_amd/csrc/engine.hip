@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -55,6 +56,13 @@ hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_e
 int ddc_padded_p(int p);
 int ddc_segments(int D, int nseg, int P, int nchains);
 int ddc_blocks_per_cu(int P, int nchains);
+hipError_t launch_fc_make_w(int logm, const float* h, int T, int D, int Dp, int P,
+                            uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st);
+hipError_t launch_fc_ddc(int logm, const float2* blk, int64_t blk_start, int64_t blk_end,
+                         const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
+                         int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
+                         const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
+                         hipEvent_t mac0, hipEvent_t mac1);
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
                                 hipStream_t st);
 hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const int* idx,
@@ -197,6 +205,22 @@ struct ChainGroup {
     int nseg = 1;
     DdcChain* h_chains[2] = {};  // pinned copy sources, per block parity
     int h_cap = 0;
+    // fast-convolution form (kernels_fcddc.hip); fc_logm == 0: direct form only
+    int fc_logm = 0;
+    int fc_P = 0;                 // ceil(T / D), unpadded
+    int fc_V = 0;                 // valid outputs per frame, M - P + 1
+    int fc_Dp = 0;                // branches padded to a multiple of 96
+    int fc_Fs = 0;                // frame stride of U / Y (>= frames of the largest block)
+    float* d_h = nullptr;         // linear taps (T)
+    float2* d_fc_tw = nullptr;    // M-point twiddles e^{-j 2 pi m / M}
+    float2* d_fc_u = nullptr;     // U[M][Fs][Dp] (stream A only)
+    float2* d_fc_y = nullptr;     // Y[chains][Fs][M] (stream A only)
+    size_t fc_y_elems = 0;
+    // filter spectra of every member, W[kappa][slot][Dp] (slot = index in `members`; a
+    // destroyed member's slot is refilled by the last member's)
+    float2* d_fc_w = nullptr;
+    int fc_w_cap = 0;             // slots
+    int64_t fc_w_ks() const { return (int64_t)fc_w_cap * fc_Dp; }
 };
 
 struct Chain {
@@ -278,6 +302,8 @@ struct Slot {  // one block's outputs in flight on streams B / C
     // timing brackets: A: [a0 waterfall + descriptors a1 DDC kernels a2 .. a3];
     // B/C: [b0 post_parallel, post_serial_front .. chain_adpcm b1]
     hipEvent_t a0 = nullptr, a1 = nullptr, a2 = nullptr, a3 = nullptr;
+    hipEvent_t m0 = nullptr, m1 = nullptr;  // around the fast-convolution DDC's GEMM (fc_mac)
+    bool timed_mac = false;
     hipEvent_t b0 = nullptr, b1 = nullptr;
     bool timed = false;
     bool timed_wf = false;
@@ -311,6 +337,67 @@ ingest_cs16(const int16_t* __restrict__ in, int64_t nsamples, float gain, float*
     }
 }
 
+// Per-block host <-> device transfers run as kernels on the stream that owns them, reading or
+// writing the pinned (GPU-mapped) host buffers directly.  hipMemcpyAsync of the same buffers
+// shares the copy engines between streams: a 115 KB descriptor upload on stream A measured
+// ~1.1 ms behind the other streams' output downloads (C3, 256 chains); as kernels they take a
+// few microseconds and stay in their stream's order.
+template <typename V>
+__global__ void __launch_bounds__(256)
+copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n) {
+    constexpr int W = sizeof(V);
+    const int64_t nv = n / W;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nv;
+         i += (int64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<V*>(dst)[i] = reinterpret_cast<const V*>(src)[i];
+    const int64_t t = nv * W + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && t < n) dst[t] = src[t];
+}
+
+static hipError_t kcopy(void* dst, const void* src, size_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const bool v16 = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+    const bool v4 = (((uintptr_t)dst | (uintptr_t)src) & 3) == 0;
+    const int64_t nv = (int64_t)(n / (v16 ? 16 : v4 ? 4 : 1));
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(256, (nv + 255) / 256));
+    if (v16)
+        hipLaunchKernelGGL(copy_bytes<uint4>, dim3(blocks), dim3(256), 0, st, (uint8_t*)dst,
+                           (const uint8_t*)src, (int64_t)n);
+    else if (v4)
+        hipLaunchKernelGGL(copy_bytes<uint32_t>, dim3(blocks), dim3(256), 0, st, (uint8_t*)dst,
+                           (const uint8_t*)src, (int64_t)n);
+    else
+        hipLaunchKernelGGL(copy_bytes<uint8_t>, dim3(blocks), dim3(256), 0, st, (uint8_t*)dst,
+                           (const uint8_t*)src, (int64_t)n);
+    return hipGetLastError();
+}
+
+// One block's chain outputs to the pinned host staging, only what each chain produced: its
+// counts record, its audio bytes, its secondary FFT bytes and its s-meter values (the staging
+// regions are sized for the worst case: copying them whole moved ~10x the produced bytes).
+__global__ void __launch_bounds__(256)
+gather_outputs(const ChainPost* __restrict__ posts, const ChainCounts* __restrict__ counts,
+               const uint8_t* __restrict__ d_out, uint8_t* __restrict__ h_out,
+               const float* __restrict__ d_sm, float* __restrict__ h_sm, int sm_stride,
+               ChainCounts* __restrict__ h_counts) {
+    const int k = blockIdx.x;
+    const ChainPost& p = posts[k];
+    const ChainCounts c = counts[k];
+    if (threadIdx.x == 0) h_counts[k] = c;
+    auto move = [&](const uint8_t* src, int64_t n) {
+        uint8_t* dst = h_out + (src - d_out);
+        const int64_t nv = n >> 4;  // regions start 256-B aligned
+        for (int64_t i = threadIdx.x; i < nv; i += blockDim.x)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+        for (int64_t i = (nv << 4) + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    };
+    move(p.out, c.out_bytes < p.out_cap ? c.out_bytes : p.out_cap);
+    if (p.sf_out && c.sf_bytes > 0) move(p.sf_out, c.sf_bytes < p.sf_out_cap ? c.sf_bytes : p.sf_out_cap);
+    const int ns = c.smeter < sm_stride ? c.smeter : sm_stride;
+    for (int i = threadIdx.x; i < ns; i += blockDim.x)
+        h_sm[(int64_t)k * sm_stride + i] = d_sm[(int64_t)k * sm_stride + i];
+}
+
 }  // namespace owrx
 
 using namespace owrx;
@@ -331,6 +418,7 @@ struct owrx_engine {
     bool failed = false;
     bool debug = false;
     bool timing = false;
+    int ddc_mode = OWRX_DDC_FAST;
     std::recursive_mutex mu;
     // push-path window (ping-pong): [history | block]
     float2* d_win[2] = {nullptr, nullptr};
@@ -435,9 +523,14 @@ static int drain_slot(owrx_engine* e, int si) {
         if (s.timed) {
             float ms = 0;
             if (hipEventElapsedTime(&ms, s.a1, s.a2) == hipSuccess) e->stats.gpu_ms_ddc += ms;
-            if (hipEventElapsedTime(&ms, s.b0, s.b1) == hipSuccess) e->stats.gpu_ms_post += ms;
+            // stream A's post kernels, and separately the span from post_parallel's start to the
+            // end of the encoder (streams A -> B -> C)
             if (hipEventElapsedTime(&ms, s.a2, s.a3) == hipSuccess) e->stats.gpu_ms_post += ms;
+            if (hipEventElapsedTime(&ms, s.b0, s.b1) == hipSuccess) e->stats.gpu_ms_serial += ms;
+            if (s.timed_mac && hipEventElapsedTime(&ms, s.m0, s.m1) == hipSuccess)
+                e->stats.gpu_ms_ddc_mac += ms;
             s.timed = false;
+            s.timed_mac = false;
         }
         for (size_t k = 0; k < s.post_ids.size(); ++k) {
             auto it = e->chains.find(s.post_ids[k]);
@@ -471,7 +564,10 @@ static int drain_slot(owrx_engine* e, int si) {
         float ms = 0;
         HIPCHK(hipEventSynchronize(s.a3));
         if (hipEventElapsedTime(&ms, s.a1, s.a2) == hipSuccess) e->stats.gpu_ms_ddc += ms;
+        if (s.timed_mac && hipEventElapsedTime(&ms, s.m0, s.m1) == hipSuccess)
+            e->stats.gpu_ms_ddc_mac += ms;
         s.timed = false;
+        s.timed_mac = false;
     }
     if (s.timed_wf) {
         float ms = 0;
@@ -665,6 +761,72 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         g->partial_elems = need;
     }
     g->nseg = nseg;
+    if (g->fc_logm) {  // fast-convolution product rows Y[chains][Fs][M]
+        const size_t ny = (size_t)std::max(1, n) * g->fc_Fs * ((size_t)1 << g->fc_logm);
+        if (ny > g->fc_y_elems) {
+            RCCHK(drain_all(e));
+            dfree(g->d_fc_y);
+            HIPCHK(dalloc(&g->d_fc_y, ny));
+            g->fc_y_elems = ny;
+        }
+    }
+    return OWRX_OK;
+}
+
+// Frame length M = 2^logm of the fast-convolution DDC for a group: the M (64, 128, 256) with
+// the least modelled time per block and chain, max(f32 MFMA time of the padded frame tiles, HBM
+// time of the W reads), ties to the longer frame (fewer frames: less U / Y traffic).  0 when
+// the branch filters are too long for these frames (the group then runs the direct form).
+static int fc_choose_logm(int D, int P, int64_t nk_max) {
+    const int Dp = (D + 95) / 96 * 96;
+    int best = 0;
+    double best_t = 0;
+    for (int logm = 8; logm >= 6; --logm) {
+        const int M = 1 << logm;
+        const int V = M - P + 1;
+        if (V < M / 2) continue;
+        const int64_t F = (nk_max + V - 1) / V;
+        const int64_t ft = F > 16 ? 32 : 16;
+        const int64_t Fp = (F + ft - 1) / ft * ft;
+        const double flop = 8.0 * M * Dp * Fp;
+        const double wbytes = 8.0 * M * Dp * (Fp / ft);
+        const double t = std::max(flop / 150e12, wbytes / 5e12);
+        if (!best || t < best_t * 0.999) {
+            best = logm;
+            best_t = t;
+        }
+    }
+    return best;
+}
+
+// (Re)builds the W[kappa][r] of the chain in `slot` for its current shift rate on stream A,
+// ordered before the next block's DDC (and after every earlier block's, which still read the
+// old spectra).
+static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
+    ChainGroup* g = c->group;
+    if (!g->fc_logm) return OWRX_OK;
+    HIPCHK(launch_fc_make_w(g->fc_logm, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P, c->rate_fx,
+                            g->d_fc_w + (int64_t)slot * g->fc_Dp, g->fc_w_ks(), e->sA));
+    return OWRX_OK;
+}
+
+// Room for `slots` members' spectra (the engine is drained): grows W[kappa][slot][Dp] by
+// doubling, moving the existing rows with one strided copy.
+static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
+    if (!g->fc_logm || slots <= g->fc_w_cap) return OWRX_OK;
+    const int M = 1 << g->fc_logm;
+    const int cap = std::max(std::max(32, 2 * g->fc_w_cap), slots);
+    float2* nw = nullptr;
+    HIPCHK(dalloc(&nw, (size_t)M * cap * g->fc_Dp));
+    if (g->d_fc_w && g->fc_w_cap > 0) {
+        const size_t row = sizeof(float2) * (size_t)g->fc_w_cap * g->fc_Dp;
+        HIPCHK(hipMemcpy2DAsync(nw, sizeof(float2) * (size_t)cap * g->fc_Dp, g->d_fc_w, row, row,
+                                (size_t)M, hipMemcpyDeviceToDevice, e->sA));
+        HIPCHK(hipStreamSynchronize(e->sA));
+    }
+    dfree(g->d_fc_w);
+    g->d_fc_w = nw;
+    g->fc_w_cap = cap;
     return OWRX_OK;
 }
 
@@ -732,10 +894,8 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     const int bp = (int)(e->block_index & 1);
     memcpy(w->h_groups[bp], w->groups.data(), sizeof(WfGroup) * w->groups.size());
     memcpy(w->h_rows[bp], w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size());
-    HIPCHK(hipMemcpyAsync(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(),
-                          hipMemcpyHostToDevice, e->sA));
-    HIPCHK(hipMemcpyAsync(w->d_rows, w->h_rows[bp], sizeof(WfRow) * w->rowdesc.size(),
-                          hipMemcpyHostToDevice, e->sA));
+    HIPCHK(kcopy(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(), e->sA));
+    HIPCHK(kcopy(w->d_rows, w->h_rows[bp], sizeof(WfRow) * w->rowdesc.size(), e->sA));
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(),
                          w->d_window, w->d_tw, w->d_partial, w->d_y4, e->sA));
     const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
@@ -754,11 +914,18 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     return OWRX_OK;
 }
 
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
+    const double t_enter = now_ms();
     // the previous block's stream-A work must be done before its input / descriptors are
     // reused; waiting here (not at the end of that block) lets the caller's host work overlap it
     if (e->in_pending) {
         HIPCHK(hipEventSynchronize(e->evIn));
+        e->stats.host_ms_wait_input += now_ms() - t_enter;
         e->in_pending = false;
     }
     const int bp = (int)(e->block_index & 1);
@@ -767,14 +934,20 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const int si = (int)(e->block_index % kSlots);
     Slot& S = e->slots[si];
     // the slot's previous block (k - kSlots) must be drained before its buffers are reused
-    RCCHK(drain_slots(e, true, kSlots - 1));
+    {
+        const double t = now_ms();
+        RCCHK(drain_slots(e, true, kSlots - 1));
+        e->stats.host_ms_wait_slots += now_ms() - t;
+    }
     const bool timed = e->timing;
     if (timed) HIPCHK(hipEventRecord(S.a0, e->sA));
 
     // ---- waterfalls (stream A); row encoding + copy on the row slot's own stream
     bool any_rows = false;
     if (!e->wfs.empty()) {
+        const double t = now_ms();
         RCCHK(drain_rows(e, true, kRowSlots - 1));  // frees the slot about to be reused
+        e->stats.host_ms_wait_rows += now_ms() - t;
         const int ri = (int)(e->row_head % kRowSlots);
         RowSlot& R = e->rslots[ri];
         for (auto& kv : e->wfs) {
@@ -794,11 +967,9 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 if (w->pend_adpcm[ri]) {
                     HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
                                            R.stream));
-                    HIPCHK(hipMemcpyAsync(w->h_bytes[ri], w->d_bytes[ri], rb * nr,
-                                          hipMemcpyDeviceToHost, R.stream));
+                    HIPCHK(kcopy(w->h_bytes[ri], w->d_bytes[ri], rb * nr, R.stream));
                 } else {
-                    HIPCHK(hipMemcpyAsync(w->h_bytes[ri], w->d_f32[ri], rb * nr,
-                                          hipMemcpyDeviceToHost, R.stream));
+                    HIPCHK(kcopy(w->h_bytes[ri], w->d_f32[ri], rb * nr, R.stream));
                 }
             }
             HIPCHK(hipEventRecord(R.evC, R.stream));
@@ -815,6 +986,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         ChainGroup* g;
         int64_t k_end;
         int nk;
+        bool fast;
     };
     std::vector<GroupWork> work;
     uint32_t sf_sizes = 0;  // secondary FFT sizes (log2 bit set) present this step
@@ -835,6 +1007,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 c->rate = c->new_rate;
                 c->rate_fx = rate_to_fx(c->rate);
                 c->rate_pending = false;
+                RCCHK(fc_build_w(e, c, (int)i));
             }
             DdcChain& d = g->h_chains[bp][i];
             d.rate_fx = c->rate_fx;
@@ -842,9 +1015,9 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             d.n0 = c->n0;
             d.P0 = c->P0;
         }
-        HIPCHK(hipMemcpyAsync(g->d_chains, g->h_chains[bp], sizeof(DdcChain) * g->members.size(),
-                              hipMemcpyHostToDevice, e->sA));
-        work.push_back(GroupWork{g, k_end, (int)nk64});
+        HIPCHK(kcopy(g->d_chains, g->h_chains[bp], sizeof(DdcChain) * g->members.size(), e->sA));
+        work.push_back(GroupWork{g, k_end, (int)nk64,
+                                 g->fc_logm != 0 && e->ddc_mode == OWRX_DDC_FAST});
     }
     if (timed) {
         HIPCHK(hipEventRecord(S.a1, e->sA));
@@ -854,10 +1027,30 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         ChainGroup* g = gw.g;
         const int64_t k_end = gw.k_end;
         const int nk = gw.nk;
-        HIPCHK(launch_ddc(g->P, blk, blk_start, blk_end, g->d_taps, g->d_chains,
-                          (int)g->members.size(), g->D, g->k_next, nk, g->nseg, g->d_partial[si],
-                          e->sA));
+        if (gw.fast) {
+            // the first fast group's GEMM is timed (one group in the benchmark configurations)
+            const bool tm = timed && !S.timed_mac;
+            HIPCHK(launch_fc_ddc(g->fc_logm, blk, blk_start, blk_end, g->d_chains, g->d_fc_w,
+                                 g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
+                                 g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
+                                 g->d_fc_y, g->d_partial[si], e->sA, tm ? S.m0 : nullptr,
+                                 tm ? S.m1 : nullptr));
+            if (tm) {
+                // algorithmic work of that GEMM: 8 flop per complex MAC over the frames that
+                // carry outputs; bytes = W (every member's spectra) + U + Y, each moved once
+                const double M = (double)(1 << g->fc_logm);
+                const double F = (double)((nk + g->fc_V - 1) / g->fc_V);
+                const double C = (double)g->members.size();
+                e->stats.ddc_mac_flop += 8.0 * M * g->fc_Dp * C * F;
+                e->stats.ddc_mac_bytes += 8.0 * M * g->fc_Dp * (C + F) + 8.0 * C * F * M;
+                S.timed_mac = true;
+            }
+        } else
+            HIPCHK(launch_ddc(g->P, blk, blk_start, blk_end, g->d_taps, g->d_chains,
+                              (int)g->members.size(), g->D, g->k_next, nk, g->nseg,
+                              g->d_partial[si], e->sA));
         e->stats.ddc_launches++;
+        if (gw.fast) e->stats.ddc_fast_launches++;
         for (size_t i = 0; i < g->members.size(); ++i) {
             Chain* c = e->chains[g->members[i]].get();
             ChainPost p;
@@ -920,7 +1113,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.dem = c->d_dem[si];
             p.s16 = c->d_s16[si];
             p.partial = g->d_partial[si];
-            p.nseg = g->nseg;
+            p.nseg = gw.fast ? 1 : g->nseg;
             p.group_chains = (int)g->members.size();
             p.chain_in_group = (int)i;
             p.nk = nk;
@@ -981,13 +1174,11 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 long_taps = std::max(long_taps, e->posts[i].bp_ntaps);
                 long_fd = std::max<int64_t>(long_fd, e->chains[S.post_ids[i]]->cap);
             }
-        HIPCHK(hipMemcpyAsync(S.d_posts, S.h_posts, sizeof(ChainPost) * np,
-                              hipMemcpyHostToDevice, e->sA));
+        HIPCHK(kcopy(S.d_posts, S.h_posts, sizeof(ChainPost) * np, e->sA));
         if (timed) HIPCHK(hipEventRecord(S.b0, e->sA));
         HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
         if (nlong > 0) {  // long bandpass chains: bp_long + post_tail (after post_parallel)
-            HIPCHK(hipMemcpyAsync(S.d_sel + S.long_off, S.h_sel + S.long_off, sizeof(int) * nlong,
-                                  hipMemcpyHostToDevice, e->sA));
+            HIPCHK(kcopy(S.d_sel + S.long_off, S.h_sel + S.long_off, sizeof(int) * nlong, e->sA));
             HIPCHK(launch_post_long(S.d_posts, S.d_counts, S.d_sel + S.long_off, nlong, long_fd,
                                     long_taps, e->sA));
         }
@@ -1020,8 +1211,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 }
                 nsel[o][nr] = nfill - off[o][nr];
             }
-        HIPCHK(hipMemcpyAsync(S.d_sel, S.h_sel, sizeof(int) * nfill, hipMemcpyHostToDevice,
-                              e->sB));
+        HIPCHK(kcopy(S.d_sel, S.h_sel, sizeof(int) * nfill, e->sB));
         const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
         for (int o = 0; o < 3; ++o)
             for (int nr = 0; nr < 2; ++nr)
@@ -1038,12 +1228,9 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         // encoders back to back: its kernel is the pipeline's longest serial stage
         HIPCHK(hipEventRecord(S.evC, e->sC));
         HIPCHK(hipStreamWaitEvent(e->sR, S.evC, 0));
-        HIPCHK(hipMemcpyAsync(S.h_counts, S.d_counts, sizeof(ChainCounts) * np,
-                              hipMemcpyDeviceToHost, e->sR));
-        HIPCHK(hipMemcpyAsync(S.h_out, S.d_out, (size_t)out_off,
-                              hipMemcpyDeviceToHost, e->sR));
-        HIPCHK(hipMemcpyAsync(S.h_sm, S.d_sm, sizeof(float) * np * e->sm_stride,
-                              hipMemcpyDeviceToHost, e->sR));
+        hipLaunchKernelGGL(gather_outputs, dim3(np), dim3(256), 0, e->sR, S.d_posts, S.d_counts,
+                           S.d_out, S.h_out, S.d_sm, S.h_sm, (int)e->sm_stride, S.h_counts);
+        HIPCHK(hipGetLastError());
         S.debug = e->debug && S.d_dbg;
         if (S.debug)
             HIPCHK(hipMemcpyAsync(S.h_dbg, S.d_dbg, (size_t)np * kDebugStages * e->dbg_stride,
@@ -1059,6 +1246,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     e->in_pending = true;
     e->pos = blk_end;
     e->stats.samples_in += n;
+    e->stats.host_ms_process += now_ms() - t_enter;
     e->stats.blocks++;
     e->block_index++;
     // collect whatever earlier blocks have finished (B / C / R work overlaps later blocks)
@@ -1186,7 +1374,9 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
             hipEventCreateWithFlags(&s.a2, hipEventDisableSystemFence) != hipSuccess ||
             hipEventCreateWithFlags(&s.a3, hipEventDisableSystemFence) != hipSuccess ||
             hipEventCreateWithFlags(&s.b0, hipEventDisableSystemFence) != hipSuccess ||
-            hipEventCreateWithFlags(&s.b1, hipEventDisableSystemFence) != hipSuccess)
+            hipEventCreateWithFlags(&s.b1, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.m0, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.m1, hipEventDisableSystemFence) != hipSuccess)
             return fail("event");
     }
     for (int i = 0; i < 2; ++i)
@@ -1210,6 +1400,11 @@ int owrx_engine_destroy(owrx_engine* e) {
     dfree(e->d_nr_tw);
     for (auto& g : e->groups) {
         dfree(g->d_taps);
+        dfree(g->d_h);
+        dfree(g->d_fc_tw);
+        dfree(g->d_fc_u);
+        dfree(g->d_fc_y);
+        dfree(g->d_fc_w);
         dfree(g->d_chains);
         for (int i = 0; i < kSlots; ++i) dfree(g->d_partial[i]);
         hfree(g->h_chains[0]);
@@ -1222,7 +1417,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     if (e->evIn) hipEventDestroy(e->evIn);
     for (auto& s : e->slots) {
         free_slot_staging(s);
-        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1})
+        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1, s.m0, s.m1})
             if (ev) hipEventDestroy(ev);
     }
     for (auto& r : e->rslots) {
@@ -1542,6 +1737,25 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         HIPCHK(dalloc(&ng->d_taps, poly.size()));
         HIPCHK(hipMemcpy(ng->d_taps, poly.data(), sizeof(float) * poly.size(),
                          hipMemcpyHostToDevice));
+        // fast-convolution form: frame length, branch padding, U and twiddles
+        ng->fc_P = (T + D - 1) / D;
+        const int64_t nk_max = e->max_block / D + 4;
+        ng->fc_logm = ng->fc_P <= 64 ? fc_choose_logm(D, ng->fc_P, nk_max) : 0;
+        if (ng->fc_logm) {
+            const int M = 1 << ng->fc_logm;
+            ng->fc_V = M - ng->fc_P + 1;
+            ng->fc_Dp = (D + 95) / 96 * 96;  // kFcDpAlign (kernels_fcddc.hip)
+            ng->fc_Fs = (int)((nk_max + ng->fc_V - 1) / ng->fc_V + 15) & ~15;
+            HIPCHK(dalloc(&ng->d_h, (size_t)T));
+            HIPCHK(hipMemcpy(ng->d_h, h.data(), sizeof(float) * T, hipMemcpyHostToDevice));
+            std::vector<float> tw = fft_twiddles(M);
+            HIPCHK(dalloc(&ng->d_fc_tw, (size_t)M));
+            HIPCHK(hipMemcpy(ng->d_fc_tw, tw.data(), sizeof(float) * 2 * M, hipMemcpyHostToDevice));
+            HIPCHK(dalloc(&ng->d_fc_u, (size_t)M * ng->fc_Fs * ng->fc_Dp));
+            if (getenv("OWRX_VERBOSE"))
+                fprintf(stderr, "owrx: DDC group D=%d T=%d: fast convolution M=%d V=%d Fs=%d\n",
+                        D, T, M, ng->fc_V, ng->fc_Fs);
+        }
         ng->k_next = aligned / D;
         e->groups.push_back(std::move(ng));
         g = e->groups.back().get();
@@ -1613,6 +1827,14 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         free_chain(c.get());
         return rc;
     }
+    if (g->fc_logm) {
+        int wrc = fc_reserve(e, g, (int)g->members.size() + 1);
+        if (!wrc) wrc = fc_build_w(e, c.get(), (int)g->members.size());
+        if (wrc) {
+            free_chain(c.get());
+            return wrc;
+        }
+    }
     const int h = e->next_handle++;
     g->members.push_back(h);
     e->chains[h] = std::move(c);
@@ -1630,7 +1852,19 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     HIPCHK(hipStreamSynchronize(e->sB));
     HIPCHK(hipStreamSynchronize(e->sC));
     ChainGroup* g = it->second->group;
-    g->members.erase(std::remove(g->members.begin(), g->members.end(), handle), g->members.end());
+    // swap-remove: the last member takes the slot (and its filter spectra move with it)
+    const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
+    const int last = (int)g->members.size() - 1;
+    if (slot != last && g->fc_logm) {
+        const int M = 1 << g->fc_logm;
+        const size_t pitch = sizeof(float2) * (size_t)g->fc_w_ks();
+        HIPCHK(hipMemcpy2DAsync(g->d_fc_w + (int64_t)slot * g->fc_Dp, pitch,
+                                g->d_fc_w + (int64_t)last * g->fc_Dp, pitch,
+                                sizeof(float2) * (size_t)g->fc_Dp, (size_t)M,
+                                hipMemcpyDeviceToDevice, e->sA));
+    }
+    g->members[slot] = g->members[last];
+    g->members.pop_back();
     free_chain(it->second.get());
     e->chains.erase(it);
     if (!g->members.empty()) RC_FAIL(e, group_refresh_device(e, g));
@@ -1693,6 +1927,36 @@ int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t m
     if (it == e->chains.end() || !dst || max_values < 0) return OWRX_EINVAL;
     return (int64_t)it->second->smeter.pop((uint8_t*)dst, sizeof(float) * (size_t)max_values) /
            (int64_t)sizeof(float);
+}
+
+int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
+                               int64_t max_bytes, int64_t* lens) {
+    ENGINE_GUARD(e);
+    if (n < 0 || (n > 0 && (!handles || !dst || !lens)) || max_bytes < 0) return OWRX_EINVAL;
+    int64_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        auto it = e->chains.find(handles[i]);
+        if (it == e->chains.end()) return OWRX_EINVAL;
+        lens[i] = (int64_t)it->second->audio.pop(dst + off, (size_t)(max_bytes - off));
+        off += lens[i];
+    }
+    return off;
+}
+
+int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float* dst,
+                                int64_t max_values, int64_t* counts) {
+    ENGINE_GUARD(e);
+    if (n < 0 || (n > 0 && (!handles || !dst || !counts)) || max_values < 0) return OWRX_EINVAL;
+    int64_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        auto it = e->chains.find(handles[i]);
+        if (it == e->chains.end()) return OWRX_EINVAL;
+        counts[i] = (int64_t)(it->second->smeter.pop((uint8_t*)(dst + off),
+                                                     sizeof(float) * (size_t)(max_values - off)) /
+                              sizeof(float));
+        off += counts[i];
+    }
+    return off;
 }
 
 int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int every_n_samples,
@@ -1802,6 +2066,13 @@ int owrx_get_stats(owrx_engine* e, owrx_stats* s) {
     for (auto& kv : e->chains) dropped += kv.second->audio.dropped;
     for (auto& kv : e->wfs) dropped += kv.second->ring.dropped;
     s->overruns += dropped;
+    return OWRX_OK;
+}
+
+int owrx_set_ddc_mode(owrx_engine* e, int mode) {
+    ENGINE_GUARD(e);
+    if (mode != OWRX_DDC_FAST && mode != OWRX_DDC_DIRECT) return OWRX_EINVAL;
+    e->ddc_mode = mode;
     return OWRX_OK;
 }
 

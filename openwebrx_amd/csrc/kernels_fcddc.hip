@@ -1,0 +1,371 @@
+// kernels_fcddc.hip -- exact fast-convolution form of the fused Selector front end:
+// Shift(rate_c) (csdr/chain/selector.py:95,132-140) followed by FirDecimate(D, transition,
+// cutoff) (selector.py:11-35), for every chain of one (D, taps) group.
+//
+//   y_c[k] = sum_{t<T} h[t] x[kD + t] exp(j 2 pi phase_c(kD + t))
+//          = rot_c(k) * sum_{r<D} sum_{p<P} u_r[k + p] g_{c,r}[p]
+// with rot_c(k) = exp(j 2 pi phase_c(kD)) (64-bit fixed-point phase, as ddc_lds seeds it),
+// u_r[i] = x[iD + r] (polyphase branch r of the wideband input, shared by all chains) and
+// g_{c,r}[p] = h[pD + r] exp(j 2 pi rate_c (pD + r)) (the chain's modulated branch taps).
+//
+// Each branch correlation runs on frames of M branch samples through M-point DFTs
+// (overlap-save: V = M - P + 1 valid outputs per frame).  For frame f, k0 = k_begin + f V:
+//   U[kappa][f][r]  = sum_{i<M} u_r[k0 + i] e^{-j 2 pi i kappa / M}            (fc_fwd)
+//   Y_c[f][kappa]   = sum_r U[kappa][f][r] W_c[kappa][r]                       (fc_mac: per kappa
+//                                                         one complex GEMM frames x chains x D)
+//   y_c[k0 + m]     = rot_c(k0 + m) IDFT_M(Y_c[f])[m],   m < V                 (fc_out)
+// with W_c[kappa][r] = sum_p g_{c,r}[p] e^{+j 2 pi p kappa / M} built once per chain and
+// rebuilt on retune (fc_make_w, fp64).  Exact up to fp32 rounding: a numpy float32 model of
+// these steps is 1.8e-7 rel-RMS from the float64 oracle at D = 833 (tests/test_gpu_parity.py
+// holds the GPU to <= 1e-5).
+//
+// Work per output and chain: 8 M Dp / V flop (7.5k at D = 833, M = 256) against 4T + 6D =
+// 94k for the direct form (ddc_lds) -- and it is a real matrix product, so it runs on the
+// f32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 products and sums; the complex product is the
+// real GEMM [Ur Ui] x [[Wr Wi] [-Wi Wr]]).  Its operands stream once per block: W (C M Dp 8 B,
+// unique per chain) from HBM, U from L2, so fc_mac sits between the HBM and the f32 MFMA roof.
+#include "owrx_types.h"
+#include "fft_lds.h"
+
+namespace owrx {
+
+typedef float fc_f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const fc_f4 gf4;  // global (not flat) loads
+
+#define HIPCHK_RET(expr)                 \
+    do {                                 \
+        hipError_t _e = (expr);          \
+        if (_e != hipSuccess) return _e; \
+    } while (0)
+
+constexpr int kFcRT = 16;   // branches (r) per fc_fwd / fc_make_w workgroup
+constexpr int kFcDpAlign = 96;  // Dp: a multiple of kFcRT and of 4 (K split) x 3 K-blocks of 8
+
+// ---- W_c[kappa][r], fp64, one chain per launch --------------------------------------------
+// grid: Dp / kFcRT workgroups; block 256.  h: the group's linear taps (T floats); the chain's
+// row kappa is written at W + kappa * w_ks.
+template <int LOGM>
+__global__ void __launch_bounds__(256)
+fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rate_fx,
+          float2* __restrict__ W, int64_t w_ks) {
+    constexpr int M = 1 << LOGM;
+    __shared__ double2 g[kFcRT][64];   // P <= 64
+    __shared__ double2 tw[M];          // e^{+j 2 pi m / M}
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * kFcRT;
+    for (int m = tid; m < M; m += 256) {
+        double s, c;
+        sincospi(2.0 * (double)m / (double)M, &s, &c);
+        tw[m] = make_double2(c, s);
+    }
+    for (int e = tid; e < kFcRT * P; e += 256) {
+        const int j = e / P, p = e % P;
+        const int r = r0 + j;
+        const int64_t t = (int64_t)p * D + r;
+        double2 v = make_double2(0.0, 0.0);
+        if (r < D && t < T) {
+            // phase of tap t in 2^-64 turns, exact; signed turns in [-0.5, 0.5)
+            const int64_t ph = (int64_t)((uint64_t)t * rate_fx);
+            const double turns = (double)ph * 5.421010862427522e-20;  // 2^-64
+            double s, c;
+            sincospi(2.0 * turns, &s, &c);
+            const double hv = (double)h[t];
+            v = make_double2(hv * c, hv * s);
+        }
+        g[j][p] = v;
+    }
+    __syncthreads();
+    const int j = tid % kFcRT;
+    for (int kap = tid / kFcRT; kap < M; kap += 256 / kFcRT) {
+        double re = 0.0, im = 0.0;
+        for (int p = 0; p < P; ++p) {
+            const double2 a = g[j][p];
+            const double2 b = tw[(p * kap) & (M - 1)];
+            re += a.x * b.x - a.y * b.y;
+            im += a.x * b.y + a.y * b.x;
+        }
+        W[(int64_t)kap * w_ks + r0 + j] = make_float2((float)re, (float)im);  // zero for r >= D
+    }
+}
+
+// ---- U[kappa][f][r]: M-point DFT of every branch frame --------------------------------------
+// grid: (Dp / kFcRT, F); block 256.  tw: M-point table e^{-j 2 pi m / M}.
+template <int LOGM>
+__global__ void __launch_bounds__(256)
+fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64_t k_begin,
+       int V, int D, int Dp, int Fs, const float2* __restrict__ tw, float2* __restrict__ U) {
+    constexpr int M = 1 << LOGM;
+    constexpr int RS = M + 1;          // LDS row stride (float2): column writes hit distinct banks
+    __shared__ float2 sm[kFcRT * RS];
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * kFcRT;
+    const int f = blockIdx.y;
+    const int64_t k0 = k_begin + (int64_t)f * V;
+    const int j = tid % kFcRT;
+    const int r = r0 + j;
+    // rows i of the frame: 16 consecutive branches = one 128-B run per row
+#pragma unroll 4
+    for (int i = tid / kFcRT; i < M; i += 256 / kFcRT) {
+        const int64_t n = (k0 + i) * (int64_t)D + r;
+        float2 x = make_float2(0.0f, 0.0f);
+        if (r < D && n < blk_end) x = blk[n - blk_start];
+        sm[j * RS + i] = x;
+    }
+    __syncthreads();
+    lds_fft_rows<LOGM, kFcRT, 256>(sm, RS, tw, 1);
+    float2* out = U + (int64_t)f * Dp + r0 + j;
+#pragma unroll 4
+    for (int kap = tid / kFcRT; kap < M; kap += 256 / kFcRT)
+        out[(int64_t)kap * Fs * Dp] = sm[j * RS + kap];
+}
+
+// ---- Y_c[f][kappa] = sum_r U[kappa][f][r] W_c[kappa][r] on the f32 MFMA ---------------------
+// One workgroup: one kappa, FTT tiles of 16 frames x CTT tiles of 8 chains; its four waves
+// split the branch range four ways (K split) and are summed through LDS in a fixed order.
+// v_mfma_f32_16x16x4_f32 lane layout: A[i][k] and B[k][j] at lane i|j + 16 k, D[4 (l/16) + v][l%16].
+// Rows = frames, columns = (chain, re|im), K = (r, re|im).  The K order inside a block of 8
+// branches is permuted (lane group g takes branches 2g, 2g+1 of the block, MFMA s takes
+// component s of that float4), the same permutation on both operands.  W of chain slot c at
+// W + c * w_cs + kappa * w_ks.
+constexpr int kFcKSplit = 4;
+template <int FTT, int CTT, bool NT>
+__global__ void __launch_bounds__(64 * kFcKSplit)
+fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs, int64_t w_ks,
+       int nchains, int Fs, int F, int Dp, int M, int ncg, float2* __restrict__ Y) {
+    // XCD-aware decode: consecutive workgroup ids land on different XCDs (round robin), so the
+    // ids one XCD receives are mapped to one contiguous kappa range; the 8-B Y stores of
+    // neighbouring kappas (one Y line) then meet in that XCD's L2
+    const int w = blockIdx.x;
+    const int xcd = w & 7;
+    const int q = w >> 3;
+    const int mper = M >> 3;
+    const int kap = xcd * mper + q % mper;
+    const int rest = q / mper;
+    const int cg = rest % ncg;
+    const int fg = rest / ncg;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    const int col = lane & 15;
+    const int cc = col >> 1;
+    const bool bim = col & 1;
+    // this wave's K range: a quarter of the K-blocks of 8 branches (Dp is a multiple of 96,
+    // so a multiple of 3 blocks each)
+    const int nkb = (Dp >> 3) / kFcKSplit;
+    const int kb0 = wave * nkb;
+
+    // rows of frames >= F and columns of chains >= nchains read frame 0 / chain 0 instead:
+    // an MFMA row (column) of D depends only on its A row (B column), and those outputs are
+    // never stored, so the loads need no guard (and the loop no branches)
+    const gf4* up[FTT];
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft) {
+        const int f = fg * 16 * FTT + ft * 16 + col;
+        up[ft] = (const gf4*)(U + ((int64_t)kap * Fs + (f < F ? f : 0)) * Dp + 8 * kb0 + 2 * g);
+    }
+    const gf4* wp[CTT];
+#pragma unroll
+    for (int t = 0; t < CTT; ++t) {
+        const int c = cg * 8 * CTT + t * 8 + cc;
+        wp[t] = (const gf4*)(W + (c < nchains ? c : 0) * w_cs + (int64_t)kap * w_ks + 8 * kb0 + 2 * g);
+    }
+    fc_f4 acc[FTT][CTT];
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) acc[ft][t] = fc_f4{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // operands of K-blocks kb (ready), kb + 1 and kb + 2 (in flight) in three register sets
+    // with fixed roles (a 3-way unrolled loop): two blocks of MFMA work cover the load latency
+    fc_f4 ua0[FTT], ua1[FTT], ua2[FTT], wa0[CTT], wa1[CTT], wa2[CTT];
+    auto load = [&](fc_f4* ua, fc_f4* wa, int kb) {
+        const int o = (kb < nkb ? kb : nkb - 1) * 4;
+#pragma unroll
+        for (int ft = 0; ft < FTT; ++ft) ua[ft] = up[ft][o];
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) {
+            if constexpr (NT) wa[t] = __builtin_nontemporal_load(wp[t] + o);
+            else wa[t] = wp[t][o];
+        }
+    };
+    auto block = [&](const fc_f4* ua, const fc_f4* wa) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            float bsel[CTT];
+#pragma unroll
+            for (int t = 0; t < CTT; ++t) {
+                // B[(r, a)][(c, b)]: a = 0 -> (Wr | Wi), a = 1 -> (-Wi | Wr)
+                const float wr = (s < 2) ? wa[t].x : wa[t].z;
+                const float wi = (s < 2) ? wa[t].y : wa[t].w;
+                bsel[t] = (s & 1) ? (bim ? wr : -wi) : (bim ? wi : wr);
+            }
+#pragma unroll
+            for (int ft = 0; ft < FTT; ++ft) {
+                const float a = ua[ft][s];
+#pragma unroll
+                for (int t = 0; t < CTT; ++t)
+                    acc[ft][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bsel[t], acc[ft][t], 0, 0, 0);
+            }
+        }
+    };
+    load(ua0, wa0, 0);
+    load(ua1, wa1, 1);
+    for (int kb = 0; kb < nkb; kb += 3) {
+        load(ua2, wa2, kb + 2);
+        __builtin_amdgcn_sched_barrier(0);  // issue the loads before this block's MFMAs
+        block(ua0, wa0);
+        load(ua0, wa0, kb + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        block(ua1, wa1);
+        load(ua1, wa1, kb + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        block(ua2, wa2);
+    }
+    // K-split sum, fixed order ((w0 + w1) + (w2 + w3))
+    __shared__ fc_f4 red[kFcKSplit - 1][FTT * CTT][64];
+    if (wave > 0) {
+#pragma unroll
+        for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+            for (int t = 0; t < CTT; ++t) red[wave - 1][ft * CTT + t][lane] = acc[ft][t];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) {
+            const int i = ft * CTT + t;
+            acc[ft][t] = (acc[ft][t] + red[0][i][lane]) + (red[1][i][lane] + red[2][i][lane]);
+        }
+    // lanes col = 2cc (re) and 2cc + 1 (im) hold one chain's 4 frames: swap halves, each lane
+    // stores two complex outputs
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) {
+            const fc_f4 o = acc[ft][t];
+            fc_f4 p;
+            p.x = __shfl_xor(o.x, 1);
+            p.y = __shfl_xor(o.y, 1);
+            p.z = __shfl_xor(o.z, 1);
+            p.w = __shfl_xor(o.w, 1);
+            const int c = cg * 8 * CTT + t * 8 + cc;
+            if (c >= nchains) continue;
+            const int fb = fg * 16 * FTT + ft * 16 + 4 * g + (bim ? 2 : 0);
+            const float2 y0 = bim ? make_float2(p.z, o.z) : make_float2(o.x, p.x);
+            const float2 y1 = bim ? make_float2(p.w, o.w) : make_float2(o.y, p.y);
+            float2* yc = Y + ((int64_t)c * Fs) * M + kap;
+            if (fb < F) yc[(int64_t)fb * M] = y0;
+            if (fb + 1 < F) yc[(int64_t)(fb + 1) * M] = y1;
+        }
+}
+
+// ---- y_c[k0 + m] = rot_c(k0 + m) IDFT_M(Y_c[f])[m] into the group's output rows ------------
+// grid: ceil(nchains F / RW) workgroups of RW = 1024 / M rows; block 256.
+OWRX_DEV float2 fc_rotator(const DdcChain& ch, int64_t n) {
+    const uint64_t ph = ch.P0 + (uint64_t)(n - ch.n0 + 1) * ch.rate_fx;
+    const int32_t hi = (int32_t)(uint32_t)(ph >> 32);
+    const float t = (float)hi * 2.3283064365386963e-10f;  // 2^-32
+    float s, c;
+    sincospif(2.0f * t, &s, &c);
+    return make_float2(c, s);
+}
+
+template <int LOGM>
+__global__ void __launch_bounds__(256)
+fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nchains, int Fs,
+       int F, int V, int D, int64_t k_begin, int nk, const float2* __restrict__ tw,
+       float2* __restrict__ out) {
+    constexpr int M = 1 << LOGM;
+    constexpr int RW = 1024 / M;
+    constexpr int RS = M + 4;
+    __shared__ float2 sm[RW * RS];
+    const int tid = threadIdx.x;
+    const int row0 = blockIdx.x * RW;
+    const int nrows = nchains * F;
+    // conj(Y) in, forward DFT, conj out = M * IDFT(Y)
+    for (int e = tid; e < RW * M; e += 256) {
+        const int rr = e / M, kap = e % M;
+        const int row = row0 + rr;
+        float2 v = make_float2(0.0f, 0.0f);
+        if (row < nrows) {
+            const int c = row / F, f = row % F;
+            v = Y[((int64_t)c * Fs + f) * M + kap];
+        }
+        sm[rr * RS + kap] = make_float2(v.x, -v.y);
+    }
+    __syncthreads();
+    lds_fft_rows<LOGM, RW, 256>(sm, RS, tw, 1);
+    const float inv = 1.0f / (float)M;
+    for (int e = tid; e < RW * M; e += 256) {
+        const int rr = e / M, m = e % M;
+        const int row = row0 + rr;
+        if (row >= nrows || m >= V) continue;
+        const int c = row / F, f = row % F;
+        const int kk = f * V + m;
+        if (kk >= nk) continue;
+        const float2 z = sm[rr * RS + m];
+        const float2 y = make_float2(z.x * inv, -z.y * inv);
+        const float2 rot = fc_rotator(chains[c], (k_begin + kk) * (int64_t)D);
+        out[(int64_t)c * nk + kk] = cmul(y, rot);
+    }
+}
+
+// ---- host launchers ----------------------------------------------------------------------
+
+hipError_t launch_fc_make_w(int logm, const float* h, int T, int D, int Dp, int P,
+                            uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st) {
+    const dim3 grid(Dp / kFcRT);
+    switch (logm) {
+        case 6: hipLaunchKernelGGL(fc_make_w<6>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks); break;
+        case 7: hipLaunchKernelGGL(fc_make_w<7>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks); break;
+        case 8: hipLaunchKernelGGL(fc_make_w<8>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// frames per block F = ceil(nk / V); U: [M][Fs][Dp], Y: [nchains][Fs][M], out: [nchains][nk]
+hipError_t launch_fc_ddc(int logm, const float2* blk, int64_t blk_start, int64_t blk_end,
+                         const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
+                         int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
+                         const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
+                         hipEvent_t mac0, hipEvent_t mac1) {
+    const int M = 1 << logm;
+    const int F = (nk + V - 1) / V;
+    if (F > Fs || nk <= 0 || nchains <= 0) return hipErrorInvalidValue;
+    const dim3 gf(Dp / kFcRT, F);
+    switch (logm) {
+        case 6: hipLaunchKernelGGL(fc_fwd<6>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U); break;
+        case 7: hipLaunchKernelGGL(fc_fwd<7>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U); break;
+        case 8: hipLaunchKernelGGL(fc_fwd<8>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U); break;
+        default: return hipErrorInvalidValue;
+    }
+    HIPCHK_RET(hipGetLastError());
+    // wave tiles: 32 frames x 32 chains, or 16 frames x 64 chains when a block has <= 16 frames
+    const bool wide = F > 16;
+    const int ctt = wide ? 4 : 8;
+    const int ftt = wide ? 2 : 1;
+    const int ncg = (nchains + 8 * ctt - 1) / (8 * ctt);
+    const int nfg = (F + 16 * ftt - 1) / (16 * ftt);
+    const dim3 gm(M * ncg * nfg);
+    if (Dp % kFcDpAlign) return hipErrorInvalidValue;
+    if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
+    if (wide)
+        hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, Y);
+    else
+        hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, Y);
+    HIPCHK_RET(hipGetLastError());
+    if (mac1) HIPCHK_RET(hipEventRecord(mac1, st));
+    const int rw = 1024 / M;
+    const dim3 go((nchains * F + rw - 1) / rw);
+    switch (logm) {
+        case 6: hipLaunchKernelGGL(fc_out<6>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out); break;
+        case 7: hipLaunchKernelGGL(fc_out<7>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out); break;
+        case 8: hipLaunchKernelGGL(fc_out<8>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace owrx

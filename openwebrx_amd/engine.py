@@ -100,6 +100,10 @@ class Engine:
     def set_debug(self, on=True):
         check(lib.owrx_set_debug(self._h, 1 if on else 0), "owrx_set_debug")
 
+    def set_ddc_mode(self, mode):
+        """DDC form: "fast" (fast-convolution filter bank, default) or "direct" (polyphase FIR)."""
+        check(lib.owrx_set_ddc_mode(self._h, {"fast": 0, "direct": 1}[mode]), "owrx_set_ddc_mode")
+
     def set_timing(self, on=True):
         check(lib.owrx_set_timing(self._h, 1 if on else 0), "owrx_set_timing")
 
@@ -107,6 +111,25 @@ class Engine:
         s = _lib.Stats()
         check(lib.owrx_get_stats(self._h, ctypes.byref(s)), "owrx_get_stats")
         return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
+
+    def read_chains(self, chains, max_bytes=64 << 20, max_values=1 << 16):
+        """Drains the audio and s-meter rings of many chains with two native calls
+        (owrx_chains_read_audio / owrx_chains_read_smeter) -- the one-thread pump for a server with
+        hundreds of clients.  Returns (audio, alens, smeter, scounts): the concatenated bytes and
+        float values as numpy arrays plus each chain's share, in the order of `chains`."""
+        n = len(chains)
+        handles = np.fromiter((c.id for c in chains), dtype=np.int32, count=n)
+        alens = np.zeros(n, np.int64)
+        scounts = np.zeros(n, np.int64)
+        abuf = _scratch(max_bytes)
+        na = check(lib.owrx_chains_read_audio(self._h, n, handles.ctypes.data_as(_lib._pi32),
+                                              abuf.ctypes.data, max_bytes,
+                                              alens.ctypes.data_as(_lib._pi64)), "read_chains")
+        sbuf = np.empty(max_values, np.float32)
+        ns = check(lib.owrx_chains_read_smeter(self._h, n, handles.ctypes.data_as(_lib._pi32),
+                                               sbuf.ctypes.data, max_values,
+                                               scounts.ctypes.data_as(_lib._pi64)), "read_chains")
+        return abuf[:na], alens, sbuf[:ns], scounts
 
     def waterfall(self, fft_size, every_n_samples, avg_number, add_db=-70.0, adpcm=True):
         return Waterfall(self, fft_size, every_n_samples, avg_number, add_db, adpcm)

@@ -3,10 +3,10 @@
 (tools/gpu_round.sh ... pmc): FETCH_SIZE and WRITE_SIZE (KB per dispatch), averaged over
 dispatches.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half of
 the bytes of wide coalesced streaming reads, so fetched bytes = 2 x FETCH_SIZE; WRITE_SIZE is
-taken as is.  Writes profiles/<tag>_pmc_traffic.json, which bench.py reports as
+taken as is.  Writes profiles/<tag>_pmc_traffic_<config>.json, which bench.py reports as
 roofline.traffic for the dominant kernel.
 
-usage: tools/pmc_traffic.py TAG FETCH_DIR WRITE_DIR"""
+usage: tools/pmc_traffic.py TAG CONFIG FETCH_DIR WRITE_DIR"""
 import collections
 import csv
 import glob
@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-tag, fdir, wdir = sys.argv[1:4]
+tag, config, fdir, wdir = sys.argv[1:5]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in (fdir, wdir):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -25,7 +25,8 @@ for d in (fdir, wdir):
             short = name.split("(")[0].replace("void ", "").replace("owrx::", "")
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
-                 "'python bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-timing'",
+                 "'python bench.py --config %s --steps 5 --warmup 3 --no-cpu-baseline --no-timing'" % config,
+       "config": config,
        "correction": "fetch_bytes = 2 x FETCH_SIZE (gfx950), write_bytes = WRITE_SIZE",
        "kernels": {}}
 for k, cs in sorted(vals.items()):
@@ -34,7 +35,7 @@ for k, cs in sorted(vals.items()):
     out["kernels"][k] = {"fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1),
                          "hbm_bytes_per_launch": int(round((2 * f + w) * 1024))}
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                    "%s_pmc_traffic.json" % tag)
+                    "%s_pmc_traffic_%s.json" % (tag, config))
 json.dump(out, open(path, "w"), indent=1)
 print(path)
 for k, v in out["kernels"].items():
