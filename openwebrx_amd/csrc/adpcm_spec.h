@@ -26,49 +26,71 @@ OWRX_DEV AdpcmTab unpack_state(uint32_t v) {
     return AdpcmTab{adpcm_tab_rec((int)(v >> 16)), (int)(int16_t)(v & 0xffffu)};
 }
 
+// Segment-transposed LDS layout: sample t of the window lives at (t % seg) * S + t / seg, so
+// when every lane walks its own segment the 64 lanes of a wave touch 64 consecutive elements
+// (a row-major layout put every lane's segment 2 * seg bytes apart: one LDS bank for the whole
+// wave, a 64-way conflict on every access).  S = nseg rounded up to odd.
+struct SpecGeom {
+    int seg, nseg, S;
+};
+OWRX_DEV SpecGeom spec_geom(int n, int min_seg) {
+    const int seg = max(min_seg, (((n + kSpecThreads - 1) / kSpecThreads) + 1) & ~1);
+    const int nseg = (n + seg - 1) / seg;
+    return SpecGeom{seg, nseg, nseg | 1};
+}
+OWRX_DEV int spec_at(const SpecGeom& g, int t) { return (t % g.seg) * g.S + t / g.seg; }
+
+// capacity for a window of WIN samples in the transposed layout: seg * S <= n + 2 seg, and
+// seg <= max(64, WIN / 256 + 2)
 template <int WIN>
 struct SpecLds {
+    static constexpr int kCap = WIN + 2 * ((WIN / kSpecThreads + 2) > 64 ? (WIN / kSpecThreads + 2) : 64) + 2;
     uint32_t NS[kAdpcmTabEntries];  // adpcm_encode_tab successor table (16-B aligned rows)
-    int16_t x[WIN];
-    uint8_t code[WIN];
-    uint32_t traj[WIN];
+    int16_t x[kCap];
+    uint8_t code[kCap];
+    uint32_t traj[kCap];
     uint32_t seg_start[kSpecThreads], seg_final[kSpecThreads];
     int16_t T[96];
     int any;
 };
 
-// Encodes L.x[0, n) from `start` (block-uniform).  Returns with L.code / L.traj filled.
+// Encodes the window x[spec_at(g, t)], t < n, from `start` (block-uniform); g = spec_geom(n,
+// min_seg) as the caller laid x out.  Returns with code / traj filled (same layout).
 // Segments start from (index = `guess_index`, predictor = previous sample), or with
 // guess_index < 0 from the step index matching the local slope.
 template <int WIN>
-OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int guess_index,
-                                int min_seg) {
+OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, const SpecGeom& g, uint32_t start,
+                                int guess_index) {
     const int tid = threadIdx.x;
-    const int seg = max(min_seg, (((n + kSpecThreads - 1) / kSpecThreads) + 1) & ~1);
-    const int nseg = (n + seg - 1) / seg;
+    const int seg = g.seg, nseg = g.nseg, S = g.S;
     const int b0 = min(tid * seg, n), b1 = min(b0 + seg, n);
+    const int len = b1 - b0;
     const int16_t* T = L.T;
     // pass 1
     if (tid < nseg) {
         AdpcmTab st;
         if (tid == 0) {
             st = unpack_state(start);
-        } else if (guess_index >= 0) {
-            st = AdpcmTab{adpcm_tab_rec(guess_index), (int)L.x[b0 - 1]};
         } else {
-            // predictor = previous sample, step index from the local slope
-            const int d = abs((int)L.x[b0 - 1] - (int)L.x[b0 - 2]);
-            int lo = 0, hi = 88;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (T[mid] < d) lo = mid + 1; else hi = mid;
+            // the previous segment's last samples: x[b0 - 1], x[b0 - 2] at the tail of lane tid-1
+            const int prev1 = (int)L.x[(seg - 1) * S + tid - 1];
+            if (guess_index >= 0) {
+                st = AdpcmTab{adpcm_tab_rec(guess_index), prev1};
+            } else {
+                // predictor = previous sample, step index from the local slope
+                const int d = abs(prev1 - (int)L.x[(seg - 2) * S + tid - 1]);
+                int lo = 0, hi = 88;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (T[mid] < d) lo = mid + 1; else hi = mid;
+                }
+                st = AdpcmTab{adpcm_tab_rec(lo), prev1};
             }
-            st = AdpcmTab{adpcm_tab_rec(lo), (int)L.x[b0 - 1]};
         }
         L.seg_start[tid] = pack_state(st);
-        for (int t = b0; t < b1; ++t) {
-            L.code[t] = (uint8_t)adpcm_encode_tab(st, L.x[t], L.NS);
-            L.traj[t] = pack_state(st);
+        for (int j = 0, a = tid; j < len; ++j, a += S) {
+            L.code[a] = (uint8_t)adpcm_encode_tab(st, L.x[a], L.NS);
+            L.traj[a] = pack_state(st);
         }
         L.seg_final[tid] = pack_state(st);
     }
@@ -87,14 +109,14 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, uint32_t start, int gues
         if (rerun) {
             AdpcmTab r = unpack_state(want);
             bool merged = false;
-            for (int t = b0; t < b1; ++t) {
-                L.code[t] = (uint8_t)adpcm_encode_tab(r, L.x[t], L.NS);
+            for (int j = 0, a = tid; j < len; ++j, a += S) {
+                L.code[a] = (uint8_t)adpcm_encode_tab(r, L.x[a], L.NS);
                 const uint32_t ps = pack_state(r);
-                if (ps == L.traj[t]) {
+                if (ps == L.traj[a]) {
                     merged = true;
                     break;
                 }
-                L.traj[t] = ps;
+                L.traj[a] = ps;
             }
             if (!merged) fin = pack_state(r);
             L.seg_start[tid] = want;

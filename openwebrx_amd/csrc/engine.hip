@@ -76,7 +76,7 @@ hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, Chain
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st);
 
-constexpr int kWfFramesPerGroup = 1;  // the four-step FFT (N > kWfLdsMaxN) relies on it
+constexpr int kWfMaxFramesPerGroup = 16;  // frames one FFT workgroup sums (N <= kWfLdsMaxN)
 constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
 constexpr int kWfMaxN = 65536;
 constexpr int kBlMaxTaps = 4095;       // longest bandpass of the bp_long path (kernels_post.hip)
@@ -635,7 +635,7 @@ static int drain_all(owrx_engine* e) {
 
 static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
     // capacities derived from the current hop/avg; re-run when they change
-    const int64_t frames = e->max_block / std::max(1, w->hop) + 2 * kWfFramesPerGroup + 2;
+    const int64_t frames = e->max_block / std::max(1, w->hop) + 2 * kWfMaxFramesPerGroup + 2;
     const int groups = (int)(frames + 2);  // a group may hold a single frame at row ends
     const int rows = (int)(frames / std::max(1, w->avg) + 3);
     if (groups > w->partial_groups || rows > w->rows_cap) RCCHK(drain_all(e));
@@ -836,6 +836,20 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
 
 // Schedules and launches one FftChain's work for the block on stream A; completed rows are
 // staged in slot `si` (their ADPCM / copy is enqueued by the caller on stream C).
+// Frames summed by one FFT workgroup: enough that a full block's frames occupy stream A's CUs
+// about once (the partial |X|^2 rows written per block shrink by the same factor).  Depends
+// only on the engine geometry and hop, and groups start at fixed frame offsets of a row, so
+// the summation order -- hence every row, bit for bit -- does not depend on how the stream is
+// cut into blocks.  The four-step FFT (N > kWfLdsMaxN) takes one frame per group.
+static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
+    if (w->N > kWfLdsMaxN) return 1;
+    const int64_t hop = std::max(1, w->hop);
+    const int64_t per_block = e->max_block / hop;
+    int64_t fpg = (per_block + std::max(1, e->cus_a) - 1) / std::max(1, e->cus_a);
+    fpg = std::min<int64_t>(fpg, (e->history - w->N) / hop);
+    return (int)std::max<int64_t>(1, std::min<int64_t>(fpg, kWfMaxFramesPerGroup));
+}
+
 static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, int64_t blk_start,
                              int64_t blk_end, int ri, int* completed) {
     *completed = 0;
@@ -846,7 +860,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     const int adpcm_now = w->adpcm;
     const int avg_now = w->avg;
     while (true) {
-        const int gf = std::min(kWfFramesPerGroup, w->avg - w->row_frame);
+        const int gf = std::min(wf_frames_per_group(e, w), w->avg - w->row_frame);
         const int64_t last = w->next_start + (int64_t)(gf - 1) * w->hop;
         if (last + w->N > blk_end) break;
         if ((int)w->groups.size() >= w->partial_groups) break;
@@ -1551,7 +1565,7 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
                        "every_n_samples > 0");
         return OWRX_EINVAL;
     }
-    if ((int64_t)kWfFramesPerGroup * every_n_samples + fft_size > e->history) {
+    if ((int64_t)every_n_samples + fft_size > e->history) {
         set_last_error("owrx_waterfall_create: hop too large for engine history");
         return OWRX_EINVAL;
     }
@@ -1589,7 +1603,7 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
     auto it = e->wfs.find(handle);
     if (it == e->wfs.end() || every_n_samples <= 0 || avg_number < 0) return OWRX_EINVAL;
     Waterfall* w = it->second.get();
-    if ((int64_t)kWfFramesPerGroup * every_n_samples + w->N > e->history) return OWRX_EINVAL;
+    if ((int64_t)every_n_samples + w->N > e->history) return OWRX_EINVAL;
     RC_FAIL(e, drain_all(e));
     w->new_hop = every_n_samples;
     w->new_avg = std::max(1, avg_number);

@@ -55,6 +55,7 @@ chain_sfft(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts
 #pragma unroll
     for (int m = 0; m < PPT; ++m) acc[m] = rf > 0 ? P.sf_acc[tid + m * kSfThreads] : 0.0f;
     const int64_t rb = adpcm ? (N + 10) / 2 : 4 * (int64_t)N;
+    const SpecGeom gm = spec_geom(N + 10, 64);  // the FftAdpcm window's transposed layout
     int rows = 0;
     while (next + N <= fill) {
 #pragma unroll
@@ -87,10 +88,10 @@ chain_sfft(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts
             const int o = (i + N / 2) & (N - 1);
             if (adpcm) {
                 const int16_t q = db_to_s16(db);
-                S.enc.x[10 + o] = q;
+                S.enc.x[spec_at(gm, 10 + o)] = q;
                 if (o == 0) {
 #pragma unroll
-                    for (int k = 0; k < 10; ++k) S.enc.x[k] = q;  // COMPRESS_FFT_PAD_N copies
+                    for (int k = 0; k < 10; ++k) S.enc.x[spec_at(gm, k)] = q;  // COMPRESS_FFT_PAD_N copies
                 }
             } else if (room) {
                 reinterpret_cast<float*>(row)[o] = db;
@@ -99,11 +100,12 @@ chain_sfft(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts
         }
         if (adpcm) {
             __syncthreads();
-            adpcm_spec_window(S.enc, N + 10, 0u, 30, 64);  // FftAdpcm: fresh state per row
+            adpcm_spec_window(S.enc, N + 10, gm, 0u, 30);  // FftAdpcm: fresh state per row
             __syncthreads();
             if (room)
                 for (int i = tid; i < (N + 10) / 2; i += kSfThreads)
-                    row[i] = (uint8_t)((S.enc.code[2 * i] & 15) | (S.enc.code[2 * i + 1] << 4));
+                    row[i] = (uint8_t)((S.enc.code[spec_at(gm, 2 * i)] & 15) |
+                                       (S.enc.code[spec_at(gm, 2 * i + 1)] << 4));
             __syncthreads();
         }
         rf = 0;

@@ -13,6 +13,9 @@
 //   (rows span blocks), 10*log10 + add_db correction, fftshift, quantise (short)(dB*100).
 // wf_adpcm_rows_spec: FftAdpcm (IMA-ADPCM of each padded row), one workgroup per row,
 //   segment-parallel and exact (adpcm_spec.h).
+#include <stdlib.h>
+#include <string.h>
+
 #include "adpcm_spec.h"
 #include "fft_lds.h"
 #include "owrx_types.h"
@@ -131,6 +134,223 @@ wf_fft_power(const float2* __restrict__ blk, int64_t blk_start,
     }
 }
 
+// ---- wf_fft_r16: the same product with radix-16 passes in registers (N = 1024 .. 16384) ----
+// N/16 threads, 16 points each.  Stockham passes of radix 16 (and one final radix 2/4/8 pass
+// for log2 N not a multiple of 4): pass 1 takes its 16 points straight from HBM (coalesced, times
+// the window), every pass but the last writes LDS, the last one squares its outputs into
+// per-thread |X|^2 accumulators -- the bins a thread finishes are the same in every frame, so a
+// group of frames is summed in registers and written once.  Three LDS round trips per frame at
+// N = 16384 (seven for the radix-4 kernel), twiddles W^k from the N-point table once per pass
+// and their powers by complex products; the LDS image is padded one element in 16 so that the
+// stride-16 stores of the first pass spread over the banks.
+OWRX_DEV int wf_pad(int i) { return i + (i >> 4); }
+
+
+
+// Complex arithmetic on packed FP32 pairs: a complex add is one v_pk_add_f32, a complex product
+// two packed instructions, so a radix-4 butterfly is 8 instructions instead of 16 (the FFT is
+// VALU-bound per CU at these sizes: ~1.5k scalar instructions per thread and 16384-point frame).
+typedef float c2 __attribute__((ext_vector_type(2)));
+OWRX_DEV c2 c2_of(float2 v) { return c2{v.x, v.y}; }
+OWRX_DEV float2 f2_of(c2 v) { return make_float2(v.x, v.y); }
+OWRX_DEV c2 pk_mul(c2 a, c2 w) {  // complex a * w
+    c2 t, s;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(s) : "v"(a), "v"(w), "v"(t));
+    return s;
+}
+OWRX_DEV c2 pk_add_mi(c2 t, c2 d) {  // t + (-i) d
+    c2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(t), "v"(d));
+    return r;
+}
+OWRX_DEV c2 pk_sub_mi(c2 t, c2 d) {  // t - (-i) d
+    c2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(t), "v"(d));
+    return r;
+}
+
+// W_L^k = exp(-2 pi i k / L), L a power of two
+OWRX_DEV c2 wf_twiddle(int k, int L) {
+    float s, c;
+    sincospif(-2.0f * (float)k / (float)L, &s, &c);
+    return c2{c, s};
+}
+
+// in-register DFT of size R (forward), natural order in and out
+OWRX_DEV void dft4(c2& a0, c2& a1, c2& a2, c2& a3) {
+    const c2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3;
+    a0 = t0 + t2;
+    a2 = t0 - t2;
+    a1 = pk_add_mi(t1, d);
+    a3 = pk_sub_mi(t1, d);
+}
+
+template <int R>
+OWRX_DEV void dft_r(c2* a) {
+    if constexpr (R == 2) {
+        const c2 t = a[1];
+        a[1] = a[0] - t;
+        a[0] = a[0] + t;
+    } else if constexpr (R == 4) {
+        dft4(a[0], a[1], a[2], a[3]);
+    } else if constexpr (R == 8) {
+        // n = 2 n1 + n2 (n1 < 4, n2 < 2), k = k1 + 4 k2
+        c2 b0[4] = {a[0], a[2], a[4], a[6]}, b1[4] = {a[1], a[3], a[5], a[7]};
+        dft4(b0[0], b0[1], b0[2], b0[3]);
+        dft4(b1[0], b1[1], b1[2], b1[3]);
+        const float h = 0.70710678118654752f;
+        const c2 w[4] = {c2{1.f, 0.f}, c2{h, -h}, c2{0.f, -1.f}, c2{-h, -h}};  // W8^k1
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1) {
+            const c2 t = k1 ? pk_mul(b1[k1], w[k1]) : b1[k1];
+            a[k1] = b0[k1] + t;
+            a[k1 + 4] = b0[k1] - t;
+        }
+    } else {
+        static_assert(R == 16, "radix");
+        // n = 4 n1 + n2, k = k1 + 4 k2: DFT4 over n1, twiddle W16^(n2 k1), DFT4 over n2
+#pragma unroll
+        for (int n2 = 0; n2 < 4; ++n2) dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
+        const float c1 = 0.92387953251128676f, s1 = 0.38268343236508977f, h = 0.70710678118654752f;
+        // B[n2][k1] sits at a[4 k1 + n2]; multiply by W16^(n2 k1)
+        a[4 * 1 + 1] = pk_mul(a[4 * 1 + 1], c2{c1, -s1});   // W^1
+        a[4 * 2 + 1] = pk_mul(a[4 * 2 + 1], c2{h, -h});     // W^2
+        a[4 * 3 + 1] = pk_mul(a[4 * 3 + 1], c2{s1, -c1});   // W^3
+        a[4 * 1 + 2] = pk_mul(a[4 * 1 + 2], c2{h, -h});     // W^2
+        a[4 * 2 + 2] = c2{a[4 * 2 + 2].y, -a[4 * 2 + 2].x}; // W^4 = -i
+        a[4 * 3 + 2] = pk_mul(a[4 * 3 + 2], c2{-h, -h});    // W^6
+        a[4 * 1 + 3] = pk_mul(a[4 * 1 + 3], c2{s1, -c1});   // W^3
+        a[4 * 2 + 3] = pk_mul(a[4 * 2 + 3], c2{-h, -h});    // W^6
+        a[4 * 3 + 3] = pk_mul(a[4 * 3 + 3], c2{-c1, s1});   // W^9
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1) dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
+        // X[k1 + 4 k2] is at a[4 k1 + k2]: transpose the 4 x 4 register block
+        c2 t[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i] = a[i];
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) a[k1 + 4 * k2] = t[4 * k1 + k2];
+    }
+}
+
+// a[r] *= W^(r k) for r < R given w1 = W^k (successive powers: two live twiddles; the
+// rounding of 15 products stays ~1e-6 relative)
+template <int R>
+OWRX_DEV void twiddle_r(c2* a, c2 w1) {
+    c2 w = w1;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+        a[r] = pk_mul(a[r], w);
+        if (r + 1 < R) w = pk_mul(w, w1);
+    }
+}
+
+template <int LOGN>
+struct WfR16 {
+    static constexpr int N = 1 << LOGN;
+    static constexpr int NT = N / 16;
+    static constexpr int P16 = LOGN / 4;                          // radix-16 passes
+    static constexpr int RL = 1 << (LOGN - 4 * P16);              // last radix (1: none)
+    static constexpr int BL = RL > 1 ? N / RL / NT : 1;           // butterflies / thread, last
+    static constexpr int NACC = RL > 1 ? BL * RL : 16;            // bins per thread
+    static constexpr size_t kLds = sizeof(float2) * (N + N / 16);
+};
+
+template <int LOGN>
+__global__ void __launch_bounds__(WfR16<LOGN>::NT)
+wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
+           const WfGroup* __restrict__ groups, const float* __restrict__ window,
+           const float2* __restrict__ tw, float* __restrict__ partial) {
+    using K = WfR16<LOGN>;
+    constexpr int N = K::N, NT = K::NT, P16 = K::P16, RL = K::RL, BL = K::BL;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int tid0 = threadIdx.x;
+    const WfGroup g = groups[blockIdx.x];
+    c2 acc[K::NACC];  // (sum re^2, sum im^2) per bin, added at the end
+#pragma unroll
+    for (int m = 0; m < K::NACC; ++m) acc[m] = c2{0.0f, 0.0f};
+    // the next frame's samples are loaded while this frame's LDS passes run
+    c2 nx[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) nx[r] = c2_of(blk[g.start - blk_start + tid0 + r * NT]);
+#pragma unroll 1
+    for (int f = 0; f < g.nframes; ++f) {
+        // opaque copy of the thread id: keeps every pass's address arithmetic inside the frame
+        // loop (hoisted, the addresses of all passes stay live and spill)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        c2 a[16];
+        // pass 1 (Ns = 1, no twiddles): j = tid, inputs j + r N/16
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float wr = window[tid + r * NT];
+            a[r] = nx[r] * wr;
+        }
+        int ns = 1;
+#pragma unroll
+        for (int pass = 0; pass < P16; ++pass) {
+            if (pass > 0) {
+                __syncthreads();  // the previous pass's stores
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a[r] = c2_of(sm[wf_pad(tid + r * NT)]);
+                const int k = tid & (ns - 1);
+                if (k) twiddle_r<16>(a, c2_of(tw[k * (N / (ns * 16))]));  // W_(16 Ns)^k
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dft_r<16>(a);
+            __builtin_amdgcn_sched_barrier(0);
+            const bool last = (pass == P16 - 1) && RL == 1;
+            if (last) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = __builtin_elementwise_fma(a[r], a[r], acc[r]);
+            } else {
+                if (pass > 0) __syncthreads();  // every load of this pass before any store
+                const int k = tid & (ns - 1);
+                const int d = ((tid / ns) * ns * 16) + k;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sm[wf_pad(d + r * ns)] = f2_of(a[r]);
+                if (pass == 0 && f + 1 < g.nframes) {
+                    const float2* xn = blk + (g.start + (int64_t)(f + 1) * g.hop - blk_start);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) nx[r] = c2_of(xn[tid + r * NT]);
+                }
+            }
+            ns *= 16;
+        }
+        if constexpr (RL > 1) {
+            // last pass: radix RL, Ns = N / RL, butterflies j = tid + b NT, outputs j + r N/RL
+            __syncthreads();
+#pragma unroll
+            for (int b = 0; b < BL; ++b) {
+                const int j = tid + b * NT;
+                c2 c[RL];
+#pragma unroll
+                for (int r = 0; r < RL; ++r) c[r] = c2_of(sm[wf_pad(j + r * (N / RL))]);
+                if (j) twiddle_r<RL>(c, c2_of(tw[j]));  // W_N^(r j)
+                dft_r<RL>(c);
+#pragma unroll
+                for (int r = 0; r < RL; ++r) acc[b * RL + r] = __builtin_elementwise_fma(c[r], c[r], acc[b * RL + r]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();  // LDS reused by the next frame
+    }
+    float* out = partial + (int64_t)blockIdx.x * N;
+    if constexpr (RL > 1) {
+#pragma unroll
+        for (int b = 0; b < BL; ++b)
+#pragma unroll
+            for (int r = 0; r < RL; ++r) out[tid0 + b * NT + r * (N / RL)] = acc[b * RL + r].x + acc[b * RL + r].y;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = acc[r].x + acc[r].y;
+    }
+}
+
 // ---- FFT sizes above one CU's LDS (32768, 65536): four-step, two launches ------------------
 // N = N1 * N2, n = N2*n1 + n2, k = k1 + N1*k2:
 //   X[k1 + N1 k2] = sum_n2 W_N2^(n2 k2) * W_N^(n2 k1) * sum_n1 x[N2 n1 + n2] W_N1^(n1 k1).
@@ -203,7 +423,17 @@ wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
     if (i >= N) return;
     const WfRow r = rows[blockIdx.y];
     float s = r.use_carry ? carry_in[i] : 0.0f;
-    for (int gi = 0; gi < r.ngroups; ++gi) s += partial[(int64_t)(r.first_group + gi) * N + i];
+    // the groups' partials in order (the row's summation order); loads batched 8 deep
+    const float* pp = partial + (int64_t)r.first_group * N + i;
+    int gi = 0;
+    for (; gi + 8 <= r.ngroups; gi += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = pp[(int64_t)(gi + u) * N];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; gi < r.ngroups; ++gi) s += pp[(int64_t)gi * N];
     if (!r.complete) {
         carry_out[i] = s;
         return;
@@ -243,21 +473,49 @@ wf_adpcm_rows_spec(const int16_t* __restrict__ s16, int N, int nrows, uint8_t* _
     uint32_t state = 0;  // FftAdpcm restarts every row at (index 0, predictor 0)
     for (int w0 = 0; w0 < M; w0 += kRowWin) {
         const int nw = min(kRowWin, M - w0);
+        const SpecGeom gm = spec_geom(nw, 64);
         __syncthreads();
         for (int i = tid; i < nw; i += kSpecThreads) {
             const int t = w0 + i;
-            L.x[i] = t < 10 ? x[0] : x[t - 10];
+            L.x[spec_at(gm, i)] = t < 10 ? x[0] : x[t - 10];
         }
         __syncthreads();
-        adpcm_spec_window(L, nw, state, 30, 64);
+        adpcm_spec_window(L, nw, gm, state, 30);
         __syncthreads();
         for (int i = tid; i < nw / 2; i += kSpecThreads)
-            o[w0 / 2 + i] = (uint8_t)((L.code[2 * i] & 15) | (L.code[2 * i + 1] << 4));
-        state = L.traj[nw - 1];
+            o[w0 / 2 + i] = (uint8_t)((L.code[spec_at(gm, 2 * i)] & 15) |
+                                      (L.code[spec_at(gm, 2 * i + 1)] << 4));
+        state = L.traj[spec_at(gm, nw - 1)];
     }
 }
 
 // host launch helpers -------------------------------------------------------------------
+template <int LOGN>
+static hipError_t launch_fft_r16(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                 int ngroups, const float* window, const float2* tw,
+                                 float* partial, hipStream_t st) {
+    using K = WfR16<LOGN>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_r16<LOGN>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)K::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(wf_fft_r16<LOGN>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start,
+                       groups, window, tw, partial);
+    return hipGetLastError();
+}
+
+static bool wf_radix4_only() {  // OWRX_WF_KERNEL=radix4: the radix-4 LDS kernel (A/B)
+    static const bool v = [] {
+        const char* s = getenv("OWRX_WF_KERNEL");
+        return s && strcmp(s, "radix4") == 0;
+    }();
+    return v;
+}
+
 template <int LOGN>
 static hipError_t launch_fft_t(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                int ngroups, const float* window, const float2* tw,
@@ -309,11 +567,26 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
     switch (logn) {
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 10: return launch_fft_t<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 11: return launch_fft_t<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 12: return launch_fft_t<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 13: return launch_fft_t<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 14: return launch_fft_t<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 10:
+            if (!wf_radix4_only())
+                return launch_fft_r16<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+            return launch_fft_t<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 11:
+            if (!wf_radix4_only())
+                return launch_fft_r16<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+            return launch_fft_t<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 12:
+            if (!wf_radix4_only())
+                return launch_fft_r16<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+            return launch_fft_t<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 13:
+            if (!wf_radix4_only())
+                return launch_fft_r16<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+            return launch_fft_t<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 14:
+            if (!wf_radix4_only())
+                return launch_fft_r16<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+            return launch_fft_t<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 15: return launch_fft4_t<7, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
                                             scratch, st);
         case 16: return launch_fft4_t<8, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
