@@ -175,6 +175,15 @@ int64_t owrx_chain_secondary_fft_row_bytes(owrx_engine* e, int handle);
  * owrx/connection.py:500-501) */
 int64_t owrx_chain_read_secondary_fft(owrx_engine* e, int handle, uint8_t* dst,
                                       int64_t max_bytes);
+/* Taps for secondary readers of the chain's buffers (ClientDemodulatorChain, owrx/dsp.py:185-206):
+ * selector != 0 publishes the Selector output (squelch-gated cf32 at the Selector rate, what
+ * selectorBuffer carries to a SecondarySelector or a COMPLEX_FLOAT secondary demodulator);
+ * audio != 0 the demodulator chain's f32 output before ClientAudioChain (what audioBuffer
+ * carries to a FLOAT secondary demodulator).  The chain itself is unchanged. */
+int owrx_chain_set_taps(owrx_engine* e, int handle, int selector, int audio);
+/* which: 0 selector (cf32 items), 1 audio (f32 items); whole items only */
+int64_t owrx_chain_read_tap(owrx_engine* e, int handle, int which, uint8_t* dst,
+                            int64_t max_bytes);
 /* absolute stream sample index of the chain's sample 0 (aligned to the decimation grid) */
 int64_t owrx_chain_origin(owrx_engine* e, int handle);
 
@@ -237,10 +246,16 @@ int owrx_set_ddc_mode(owrx_engine* e, int mode);
 #define OWRX_MOD_FFTADPCM 11      /* p0 = fft size; input f32 rows (already swapped) */
 #define OWRX_MOD_CONVERT_CS16_CF32 12  /* Convert(COMPLEX_SHORT, COMPLEX_FLOAT); n = samples */
 #define OWRX_MOD_GAIN 13          /* Gain(format, p0); p1 = 1 complex (n samples), 0 float */
+#define OWRX_MOD_SHIFT 14         /* Shift(p0 = rate), cf32; phase continuous across calls */
+#define OWRX_MOD_BANDPASS 15      /* Bandpass(p0 = low, p1 = high, p2 = transition), cf32 */
+#define OWRX_MOD_AUDIO_RESAMPLER 16 /* AudioResampler(p0 = input rate, p1 = output rate), f32:
+                                       rational L/M polyphase lowpass (the build's choice) */
 typedef struct owrx_module owrx_module;
 int owrx_module_create(int device, int type, double p0, double p1, double p2,
                        owrx_module** out);
 int owrx_module_destroy(owrx_module* m);
+/* Shift.setRate(p0) (phase continuous) / Bandpass.setBandpass(p0, p1) with transition p2 */
+int owrx_module_set(owrx_module* m, double p0, double p1, double p2);
 /* in: n input items (cf32 for demods, f32, s16 for ADPCM); out: capacity in bytes */
 int64_t owrx_module_process(owrx_module* m, const void* in, int64_t n, void* out,
                             int64_t out_cap_bytes);

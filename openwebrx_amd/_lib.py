@@ -36,6 +36,9 @@ MOD_FFTSWAP = 10
 MOD_FFTADPCM = 11
 MOD_CONVERT_CS16_CF32 = 12
 MOD_GAIN = 13
+MOD_SHIFT = 14
+MOD_BANDPASS = 15
+MOD_AUDIO_RESAMPLER = 16
 
 
 class ChainParams(ctypes.Structure):
@@ -138,6 +141,9 @@ PROTOTYPES = {
     "owrx_get_stats": (_i32, [_vp, ctypes.POINTER(Stats)]),
     "owrx_set_timing": (_i32, [_vp, _i32]),
     "owrx_set_ddc_mode": (_i32, [_vp, _i32]),
+    "owrx_module_set": (_i32, [_vp, _f64, _f64, _f64]),
+    "owrx_chain_set_taps": (_i32, [_vp, _i32, _i32, _i32]),
+    "owrx_chain_read_tap": (_i64, [_vp, _i32, _i32, _vp, _i64]),
     "owrx_synth_iq": (_i32, [_i32, _vp, _i64, _i64, _f64, _i32, _vp, _vp, ctypes.c_uint64, _f32, _f32]),
     "owrx_chains_read_audio": (_i64, [_vp, _i32, _pi32, _vp, _i64, _pi64]),
     "owrx_chains_read_smeter": (_i64, [_vp, _i32, _pi32, _vp, _i64, _pi64]),

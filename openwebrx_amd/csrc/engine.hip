@@ -223,6 +223,9 @@ struct ChainGroup {
     int64_t fc_w_ks() const { return (int64_t)fc_w_cap * fc_Dp; }
 };
 
+// staging regions start 256-B aligned
+static int64_t out_region(int64_t cap) { return (cap + 255) & ~(int64_t)255; }
+
 struct Chain {
     owrx_chain_params prm;
     ChainGroup* group = nullptr;
@@ -274,6 +277,11 @@ struct Chain {
     float2* d_sf_tw = nullptr;
     int64_t sf_out_cap = 0;      // staging bytes per step
     ByteRing sfft;
+    // taps for secondary readers (owrx/dsp.py:185-206): selectorBuffer (cf32 after Squelch)
+    // and audioBuffer (f32 demodulator-chain output); staging bytes per step, 0 = off
+    int64_t tap_sq_cap = 0, tap_agc_cap = 0;
+    ByteRing tap_sel, tap_audio;
+    int64_t tap_bytes() const { return out_region(tap_sq_cap) + out_region(tap_agc_cap); }
     int64_t sf_row_bytes() const { return sf_adpcm ? (sf_n + 10) / 2 : 4 * (int64_t)sf_n; }
 };
 
@@ -393,6 +401,9 @@ gather_outputs(const ChainPost* __restrict__ posts, const ChainCounts* __restric
     };
     move(p.out, c.out_bytes < p.out_cap ? c.out_bytes : p.out_cap);
     if (p.sf_out && c.sf_bytes > 0) move(p.sf_out, c.sf_bytes < p.sf_out_cap ? c.sf_bytes : p.sf_out_cap);
+    if (p.tap_sq) move((const uint8_t*)p.tap_sq, 8 * (c.n_gate < p.tap_sq_cap ? c.n_gate : p.tap_sq_cap));
+    if (p.tap_agc)
+        move((const uint8_t*)p.tap_agc, 4 * (c.n_front < p.tap_agc_cap ? c.n_front : p.tap_agc_cap));
     const int ns = c.smeter < sm_stride ? c.smeter : sm_stride;
     for (int i = threadIdx.x; i < ns; i += blockDim.x)
         h_sm[(int64_t)k * sm_stride + i] = d_sm[(int64_t)k * sm_stride + i];
@@ -447,8 +458,6 @@ struct owrx_engine {
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
-
-static int64_t out_region(int64_t cap) { return (cap + 255) & ~(int64_t)255; }
 
 static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
     int64_t nk = e->max_block / D + 4;
@@ -544,6 +553,20 @@ static int drain_slot(owrx_engine* e, int si) {
                 const int64_t sb = std::min<int64_t>(cc.sf_bytes, c->sf_out_cap);
                 if (cc.sf_bytes > c->sf_out_cap) e->stats.overruns++;
                 c->sfft.push(s.h_out + s.out_off[k] + out_region(c->out_cap), (size_t)sb);
+            }
+            if (c->tap_bytes() > 0) {
+                const uint8_t* tb = s.h_out + s.out_off[k] + out_region(c->out_cap) +
+                                    out_region(c->sf_out_cap);
+                if (c->tap_sq_cap > 0) {
+                    const int64_t b = std::min<int64_t>(8 * cc.n_gate, c->tap_sq_cap);
+                    if (8 * cc.n_gate > c->tap_sq_cap) e->stats.overruns++;
+                    c->tap_sel.push(tb, (size_t)b);
+                }
+                if (c->tap_agc_cap > 0) {
+                    const int64_t b = std::min<int64_t>(4 * cc.n_front, c->tap_agc_cap);
+                    if (4 * cc.n_front > c->tap_agc_cap) e->stats.overruns++;
+                    c->tap_audio.push(tb + out_region(c->tap_sq_cap), (size_t)b);
+                }
             }
             e->stats.audio_bytes += nb;
             e->stats.ddc_outputs += cc.n_ddc;
@@ -680,7 +703,8 @@ static int ensure_post_capacity(owrx_engine* e) {
     // is ~2.6 KB per C2 block, a service resampler's cf32 IF up to 8 B per decimated sample)
     int64_t need_out = 256, need_sm = 4, need_dbg = 64;
     for (auto& kv : e->chains) {
-        need_out += out_region(kv.second->out_cap) + out_region(kv.second->sf_out_cap);
+        need_out += out_region(kv.second->out_cap) + out_region(kv.second->sf_out_cap) +
+                    kv.second->tap_bytes();
         need_sm = std::max<int64_t>(need_sm, kv.second->sm_cap);
         // squelch / demod taps hold up to cap + sq_length samples per step
         need_dbg = std::max<int64_t>(need_dbg, (kv.second->cap + kv.second->prm.sq_length + 16) * 8 + 64);
@@ -1155,6 +1179,15 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 sf_sizes |= 1u << c->sf_logn;
             }
             out_off += out_region(c->sf_out_cap);
+            if (c->tap_sq_cap > 0 && q.output != OWRX_OUT_IQ) {
+                p.tap_sq = (float2*)(S.d_out + out_off);
+                p.tap_sq_cap = c->tap_sq_cap / 8;
+            }
+            if (c->tap_agc_cap > 0 && q.output != OWRX_OUT_IQ) {
+                p.tap_agc = (float*)(S.d_out + out_off + out_region(c->tap_sq_cap));
+                p.tap_agc_cap = c->tap_agc_cap / 4;
+            }
+            out_off += c->tap_bytes();
             p.smeter = S.d_sm + (int64_t)slot * e->sm_stride;
             p.smeter_cap = (int)e->sm_stride;
             p.debug = (e->debug && S.d_dbg) ? 1 : 0;
@@ -1971,6 +2004,37 @@ int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float
         off += counts[i];
     }
     return off;
+}
+
+int owrx_chain_set_taps(owrx_engine* e, int handle, int selector, int audio) {
+    ENGINE_GUARD(e);
+    auto it = e->chains.find(handle);
+    if (it == e->chains.end()) return OWRX_EINVAL;
+    Chain* c = it->second.get();
+    if (c->prm.output == OWRX_OUT_IQ && (selector || audio)) {
+        set_last_error("owrx_chain_set_taps: the chain has no Selector output / audio");
+        return OWRX_EINVAL;
+    }
+    RC_FAIL(e, drain_all(e));
+    const int64_t scap = c->cap + c->prm.sq_length + 16;  // samples per step, as the staging
+    c->tap_sq_cap = selector ? 8 * scap : 0;
+    c->tap_agc_cap = audio ? 4 * scap : 0;
+    if (!selector) c->tap_sel.clear();
+    if (!audio) c->tap_audio.clear();
+    RC_FAIL(e, ensure_post_capacity(e));
+    return OWRX_OK;
+}
+
+int64_t owrx_chain_read_tap(owrx_engine* e, int handle, int which, uint8_t* dst,
+                            int64_t max_bytes) {
+    ENGINE_GUARD(e);
+    auto it = e->chains.find(handle);
+    if (it == e->chains.end() || !dst || max_bytes < 0 || which < 0 || which > 1)
+        return OWRX_EINVAL;
+    ByteRing& r = which == 0 ? it->second->tap_sel : it->second->tap_audio;
+    const size_t item = which == 0 ? 8 : 4;
+    const size_t n = std::min<size_t>((size_t)max_bytes, r.avail()) / item * item;
+    return (int64_t)r.pop(dst, n);
 }
 
 int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int every_n_samples,

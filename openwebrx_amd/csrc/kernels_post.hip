@@ -414,6 +414,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
     for (int i = tid; i < nsq; i += NT) {
         const float2 x = sh_pass[i / L] ? sq_buf[i] : make_float2(0.0f, 0.0f);
         if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
+        if (P.tap_sq && i < P.tap_sq_cap) P.tap_sq[i] = x;  // selectorBuffer readers
         if (P.sf_n > 0) P.sf_buf[sf_fill + i] = x;  // Selector output -> secondary FFT
         float v;
         if (P.demod == 0 || P.demod == 3) {
@@ -737,6 +738,11 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                         a = g * q.x;
                     }
                     as_[ch & 1][j][lane] = a;
+                    {   // audioBuffer readers (a secondary demodulator on the audio)
+                        const int64_t qi = base + j;
+                        if (sl.active && Pp->tap_agc && (full || qi < n) && qi < Pp->tap_agc_cap)
+                            gp(Pp->tap_agc)[qi] = a;
+                    }
                     if (DEBUG) {
                         const int64_t qi = base + j;
                         const bool valid = sl.active && (full || qi < n);

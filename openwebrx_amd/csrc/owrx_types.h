@@ -142,6 +142,13 @@ struct ChainPost {
     const float2* sf_tw;
     uint8_t* sf_out;       // staging (rows of FftAdpcm bytes or f32 dB)
     int64_t sf_out_cap;
+    // taps for secondary readers of ClientDemodulatorChain's buffers (owrx/dsp.py:185-206):
+    // the squelched Selector output (selectorBuffer, cf32) and the demodulator chain's audio
+    // before ClientAudioChain (audioBuffer, f32); null when nothing reads them
+    float2* tap_sq;
+    int64_t tap_sq_cap;
+    float* tap_agc;
+    int64_t tap_agc_cap;
 };
 
 // Per-chain counters written by the post kernels for the host (and n_sq for post_serial).

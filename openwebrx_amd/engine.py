@@ -234,6 +234,25 @@ class Chain:
                                              max_values), "read_smeter")
         return buf[:n].copy()
 
+    def set_taps(self, selector=False, audio=False):
+        """Publish the Selector output (cf32) and / or the pre-ClientAudioChain audio (f32) for
+        secondary readers (owrx/dsp.py:185-206)."""
+        check(lib.owrx_chain_set_taps(self.engine.handle, self.id, 1 if selector else 0,
+                                      1 if audio else 0), "owrx_chain_set_taps")
+
+    def read_tap(self, which):
+        """which: "selector" -> complex64 array, "audio" -> float32 array (all available)."""
+        w = {"selector": 0, "audio": 1}[which]
+        out = []
+        buf = _scratch(1 << 20)
+        while True:
+            n = check(lib.owrx_chain_read_tap(self.engine.handle, self.id, w, buf.ctypes.data,
+                                              buf.size), "read_tap")
+            if n <= 0:
+                break
+            out.append(buf[:n].tobytes())
+        return np.frombuffer(b"".join(out), np.complex64 if w == 0 else np.float32)
+
     def set_secondary_fft(self, fft_size, every_n_samples=0, avg_number=0, add_db=-70.0,
                           adpcm=True):
         """FftChain on this chain's Selector output (owrx/dsp.py:220-225); fft_size 0 removes
@@ -296,6 +315,10 @@ class Module:
         r = check(lib.owrx_module_process(self._h, a.ctypes.data, n, out.ctypes.data, out.size),
                   "owrx_module_process")
         return out[:r].tobytes()
+
+    def set(self, p0, p1=0.0, p2=0.0):
+        """Shift.setRate / Bandpass.setBandpass on a running standalone module."""
+        check(lib.owrx_module_set(self._h, float(p0), float(p1), float(p2)), "owrx_module_set")
 
     def close(self):
         if self._h:

@@ -66,19 +66,46 @@ def _readers_of(buf):
     return [r.module for r in buf._readers if r.module is not None and not r._stopped]
 
 
+# Modules a client chain continues into, in the order a branch point prefers them
+# (selectorBuffer: the demodulator; audioBuffer: ClientAudioChain's first module)
+def _continuations():
+    from . import modules as M
+    return (M.FmDemod, M.AmDemod, M.RealPart, M.FractionalDecimator, M.Bandpass, M.Squelch,
+            M.Limit, M.NfmDeemphasis, M.WfmDeemphasis, M.DcBlock, M.Agc, M.NoiseFilter,
+            M.Convert, M.AdpcmEncoder, M.FirDecimate, M.LogAveragePower, M.LogPower, M.FftSwap,
+            M.FftAdpcm)
+
+
 def _downstream(module):
-    """The single module a segment continues into.  An Fft reading the same buffer is a tap,
-    not the continuation: ClientDemodulatorChain hangs its secondary FftChain on the Selector
-    output next to the demodulator (owrx/dsp.py:220-225)."""
-    from .modules import Buffer, Fft
+    """The module a segment continues into.  Other readers of the same buffer are taps, not the
+    continuation: ClientDemodulatorChain hangs its secondary FftChain on the Selector output
+    next to the demodulator (owrx/dsp.py:220-225), a SecondarySelector or a COMPLEX_FLOAT
+    secondary demodulator on selectorBuffer and a FLOAT secondary demodulator on audioBuffer
+    (:185-206).  The continuation is the first reader (in attachment order) of the most
+    preferred class; a Shift or Fft is never one (they only start segments)."""
+    from .modules import Buffer
     w = module.writer
     if not isinstance(w, Buffer):
         return None
-    readers = [m for m in _readers_of(w) if not isinstance(m, Fft)]
-    if len(readers) != 1:
-        return None
-    nxt = readers[0]
-    return nxt if nxt.fusable else None
+    readers = [m for m in _readers_of(w) if m.fusable]
+    for cls in _continuations():
+        for m in readers:
+            if type(m) is cls:
+                return m
+    return None
+
+
+def _taps_of(module, continuation):
+    """Live readers of `module`'s output buffer other than the chain's continuation and a fused
+    secondary FFT: native modules, or Python modules (csdr.module, e.g. a decoder) whose readers
+    carry no module -- they receive the tapped stream the engine driver writes there."""
+    from . import modules as M
+    w = module.writer
+    if not isinstance(w, M.Buffer):
+        return []
+    with w._cond:
+        rs = [r for r in w._readers if not (r._stopped or r._detached)]
+    return [r for r in rs if r.module is not continuation and not isinstance(r.module, M.Fft)]
 
 
 def _plan_fft(mods):
@@ -199,6 +226,7 @@ def plan_segment(head):
     agc = take(M.Agc) if wfm is None else None
     if agc is None and wfm is None:
         return None
+    demod_last = mods[i - 1]  # writes audioBuffer (ClientDemodulatorChain._connect, dsp.py:86-92)
     nr = take(M.NoiseFilter)
     output = _lib.OUT_F32
     if take(M.Convert) is not None:
@@ -230,6 +258,11 @@ def plan_segment(head):
         p.update(sq_length=sq.length, sq_decimation=sq.decimation, sq_hang=sq.hang_length,
                  sq_flush=sq.flush_length, sq_report=sq.report_interval, sq_level=sq.level,
                  power_writer=sq.power_writer)
+    sel_cont = mods[mods.index(selector_last) + 1]
+    aud_cont = mods[mods.index(demod_last) + 1] if mods.index(demod_last) + 1 < len(mods) else None
+    p["tap_selector"] = selector_last.writer if _taps_of(selector_last, sel_cont) else None
+    p["tap_audio"] = demod_last.writer if aud_cont is not None and _taps_of(demod_last, aud_cont) \
+        else None
     sec = _secondary_fft(selector_last)
     p["secondary_fft"] = sec[0] if sec is not None else None
     p["secondary_modules"] = sec[1] if sec is not None else []
@@ -241,7 +274,8 @@ def chain_params_struct(p):
     from .. import _lib
     s = _lib.ChainParams()
     for k, v in p.items():
-        if k not in ("power_writer", "secondary_fft", "secondary_modules", "secondary_writer"):
+        if k not in ("power_writer", "secondary_fft", "secondary_modules", "secondary_writer",
+                     "tap_selector", "tap_audio"):
             setattr(s, k, v)
     return s
 
@@ -298,6 +332,8 @@ class EngineDriver:
                 obj = self.engine.chain(chain_params_struct(p))
                 if p.get("secondary_fft") is not None:
                     _apply_secondary(obj, p["secondary_fft"])
+                if p.get("tap_selector") is not None or p.get("tap_audio") is not None:
+                    obj.set_taps(p.get("tap_selector") is not None, p.get("tap_audio") is not None)
             self.segments[hid] = (kind, p, mods, obj)
             self._absorb(mods, True)
             self._absorb(p.get("secondary_modules", []), True)
@@ -324,6 +360,9 @@ class EngineDriver:
                 obj.set_squelch_level(p["sq_level"])
             if old.get("secondary_fft") != p.get("secondary_fft"):
                 _apply_secondary(obj, p.get("secondary_fft"))
+            if (old.get("tap_selector") is None, old.get("tap_audio") is None) != \
+                    (p.get("tap_selector") is None, p.get("tap_audio") is None):
+                obj.set_taps(p.get("tap_selector") is not None, p.get("tap_audio") is not None)
             olds, news = old.get("secondary_modules", []), p.get("secondary_modules", [])
             if olds != news:
                 self._absorb([m for m in olds if m not in news], False)
@@ -350,6 +389,14 @@ class EngineDriver:
                     rows = obj.read_secondary_fft()
                     if rows.size:
                         sw.write(rows.tobytes())
+                # taps: the Selector output into selectorBuffer, the demodulator chain's audio
+                # into audioBuffer, for their secondary readers
+                for key, which in (("tap_selector", "selector"), ("tap_audio", "audio")):
+                    buf = p.get(key)
+                    if buf is not None:
+                        t = obj.read_tap(which)
+                        if t.size:
+                            buf.write(t.tobytes())
 
     def close(self):
         """Stop reading the source; the thread pushes what it holds, syncs and drains."""

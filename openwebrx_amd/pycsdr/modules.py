@@ -199,6 +199,9 @@ class _NativeModule(Module):
         self.reader = reader
         if reader is not None:
             reader.module = self
+            # Chain.replace hands the stopped predecessor's reader to its replacement
+            # (csdr/chain/__init__.py:54-64; the modules re-arm it, cf. csdr/module/__init__.py:188)
+            reader.resume()
         _graph.changed(self)
         self._check_start()
 
@@ -236,7 +239,8 @@ class _NativeModule(Module):
         return False
 
     def _run(self):
-        runner = None  # created on the first data: idle (fused) modules hold no GPU state
+        # the runner is created on the first data: idle (fused) modules hold no GPU state
+        self._runner = None
         try:
             while not self._stopped:
                 reader = self.reader
@@ -247,15 +251,35 @@ class _NativeModule(Module):
                     break
                 if self.absorbed:
                     continue
-                if runner is None:
-                    runner = self._make_runner()
-                out = runner(np.frombuffer(data, dtype=np.uint8))
+                with self._lock:
+                    if self._runner is None:
+                        self._runner = self._make_runner()
+                    out = self._runner(np.frombuffer(data, dtype=np.uint8))
                 if out and self.writer is not None:
                     self.writer.write(out)
         finally:
-            close = getattr(runner, "close", None)
+            with self._lock:
+                close = getattr(self._runner, "close", None)
+                self._runner = None
             if close:
                 close()
+
+    def _reads_module_output(self):
+        """The input buffer is written by another module (a tap such as ClientDemodulatorChain's
+        selectorBuffer, owrx/dsp.py:185-206), not by the wideband source a fused segment reads."""
+        r = self.reader
+        w = r._buffer.writer_module if r is not None else None
+        return w is not None and getattr(w, "fusable", False)
+
+    def _update_runner(self, *params):
+        with self._lock:
+            r = getattr(self, "_runner", None)
+            if r is None:
+                return
+            if hasattr(r, "set"):
+                r.set(*params)
+            else:  # a stand-in (e.g. a pass-through): rebuilt from the new parameters
+                self._runner = None
 
     def _make_runner(self):
         raise NotImplementedError
@@ -275,6 +299,9 @@ class _GpuModuleRunner:
         x = raw.view(self._in_dtype)
         cap = int(x.size * self._out_per_in * self._out_itemsize) + 64
         return self._m.process(x, cap)
+
+    def set(self, *params):
+        self._m.set(*params)
 
     def close(self):
         self._m.close()
@@ -365,7 +392,17 @@ class Shift(_NativeModule):
 
     def setRate(self, rate):
         self.rate = float(rate)
+        self._update_runner(self.rate)
         _graph.changed(self, structural=False)
+
+    # standalone on a module's output (the SecondarySelector on selectorBuffer); at the head of
+    # a chain on the wideband buffer it runs fused in the engine's DDC
+    def _standalone_supported(self):
+        return self._reads_module_output()
+
+    def _make_runner(self):
+        from .. import _lib
+        return _GpuModuleRunner(_lib.MOD_SHIFT, np.complex64, 8, 1.0, self.rate)
 
 
 class FirDecimate(_NativeModule):
@@ -410,7 +447,20 @@ class Bandpass(_NativeModule):
     def setBandpass(self, low_cut, high_cut):
         self.low_cut = float(low_cut)
         self.high_cut = float(high_cut)
+        self._update_runner(self.low_cut, self.high_cut, self.transition)
         _graph.changed(self, structural=False)
+
+    # standalone outside a fused chain (the SecondarySelector's Bandpass, csdr/chain/
+    # selector.py:212-224); inside a client chain it is part of the fused Selector
+    def _standalone_supported(self):
+        return self._reads_module_output() and self.transition > 0
+
+    def _make_runner(self):
+        from .. import _lib
+        if self.low_cut is None or self.high_cut is None:
+            return lambda raw: raw.tobytes()  # no cuts: Bandpass passes through
+        return _GpuModuleRunner(_lib.MOD_BANDPASS, np.complex64, 8, 1.0, self.low_cut,
+                                self.high_cut, self.transition)
 
 
 class Squelch(_NativeModule):
@@ -668,6 +718,29 @@ class TcpSource(_NativeModule):
                 pass
 
 
+class AudioResampler(_Unary):
+    """AudioResampler(inputRate, outputRate) (csdr/chain/clientaudio.py:15-16): FLOAT, run
+    standalone on the GPU behind a fused chain's F32 audio (ClientAudioChain inserts it when the
+    demodulator's audio rate differs from the client rate, owrx/dsp.py:157-166).  Rational L/M
+    polyphase lowpass; csdr's filter design is not in the reference (parity unpinned)."""
+    input_format = Format.FLOAT
+    output_format = Format.FLOAT
+    _mod = "MOD_AUDIO_RESAMPLER"
+
+    def __init__(self, inputRate, outputRate):
+        super().__init__()
+        self.input_rate = int(inputRate)
+        self.output_rate = int(outputRate)
+
+    def _params(self):
+        return (self.input_rate, self.output_rate)
+
+    def _make_runner(self):
+        from .. import _lib
+        return _GpuModuleRunner(_lib.MOD_AUDIO_RESAMPLER, np.float32, 4,
+                                self.output_rate / self.input_rate + 0.01, *self._params())
+
+
 # ---- present for imports only (SURVEY.md 8b: may raise when instantiated) -----------------
 
 def _unsupported(name):
@@ -677,7 +750,7 @@ def _unsupported(name):
     return type(name, (_NativeModule,), {"__init__": __init__, "fusable": False})
 
 
-for _name in ("Afc", "AudioResampler", "BaudotDecoder", "Ccir476Decoder", "Ccir493Decoder",
+for _name in ("Afc", "BaudotDecoder", "Ccir476Decoder", "Ccir493Decoder",
               "CwDecoder", "DBPskDecoder", "Downmix", "DscDecoder", "ExecModule", "FaxDecoder",
               "Lowpass", "MFRttyDecoder", "NavtexDecoder", "RttyDecoder",
               "SitorBDecoder", "SnrSquelch", "SstvDecoder", "Throttle", "TimingRecovery",

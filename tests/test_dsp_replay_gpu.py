@@ -1,0 +1,115 @@
+"""GPU replay of the graph the reference's ClientDemodulatorChain builds with a secondary
+demodulator behind a SecondarySelector (owrx/dsp.py:188-202; recorded in
+tests/golden/dsp_graph.json by tests/golden/make_dsp_graph.py): the primary chain stays fused
+and its audio is byte-identical to the same chain without the secondary; the Selector output
+the engine publishes into selectorBuffer equals the oracle's squelch stage; the SecondarySelector
+(Shift + Bandpass at 12 kHz, standalone on the GPU) turns it into the oracle's shifted and
+band-passed stream."""
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import dsp_replay  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def _collect(buf):
+    r = buf.getReader()
+    out = []
+    t = threading.Thread(target=lambda: [out.append(bytes(x)) for x in iter(r.read, None)])
+    t.start()
+    return r, t, out
+
+
+def _iq(fs, n):
+    from openwebrx_amd import synth
+    x, _ = synth.make_iq(fs, n, ["am", "usb"])  # other carriers, not in the channel
+    t = np.arange(n) / fs
+    ph = 2 * np.pi * (-200000.0) * t + 2.5 * np.sin(2 * np.pi * 1000.0 * t)
+    x += (0.05 * np.exp(1j * ph)).astype(np.complex64)          # NFM at the chain's offset
+    x += (0.02 * np.exp(2j * np.pi * (-199000.0 + 10.0) * t)).astype(np.complex64)  # +1 kHz
+    return x.astype(np.complex64)
+
+
+def _run(step, iq):
+    from openwebrx_amd.pycsdr import _graph
+    s = dsp_replay.steps()[step]
+    wide, mods, outs, power = dsp_replay.build(s)
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    audio = _collect(outs[cls.index("AdpcmEncoder")])
+    sq = cls.index("Squelch")
+    tap = _collect(outs[sq]) if s["tap_selector"] else None
+    sec = None
+    if s["tap_selector"]:  # the SecondarySelector: the Bandpass fed by the second Shift
+        bp2 = [i for i, d, src in s["graph"] if d["class"] == "Bandpass" and
+               s["graph"][src][1]["class"] == "Shift" and src != 0][0]
+        sec = _collect(outs[bp2])
+    for i in range(0, iq.size, 100003):
+        wide.write(iq[i:i + 100003].tobytes())
+    drv = _graph._drivers.get(id(wide))
+    while drv.reader.available() > 0:
+        time.sleep(0.01)
+    _graph.finish(wide)
+    res = {"fused": drv.engine is not None and len(drv.segments) == 1}
+    def settle(col):  # the collector has read everything written so far
+        t0 = time.time()
+        while col[0].available() > 0 and time.time() - t0 < 20:
+            time.sleep(0.02)
+
+    for col in [audio] + ([tap] if tap else []):
+        settle(col)
+    # standalone secondary modules run on their own threads: let them drain
+    if sec is not None:
+        want = sum(len(b) for b in tap[2])
+        t0 = time.time()
+        while sum(len(b) for b in sec[2]) < want and time.time() - t0 < 20:
+            time.sleep(0.05)
+        settle(sec)
+    for col in [audio] + ([tap, sec] if tap else []):
+        col[0].stop()
+        col[1].join(5)
+    res["audio"] = b"".join(audio[2])
+    if tap:
+        res["tap"] = np.frombuffer(b"".join(tap[2]), np.complex64)
+        res["sec"] = np.frombuffer(b"".join(sec[2]), np.complex64)
+        res["sec_params"] = [d for _, d, _ in s["graph"]]
+    return res
+
+
+def rel_rms(a, b):
+    return float(np.sqrt(np.mean(np.abs(a - b) ** 2) / np.mean(np.abs(b) ** 2)))
+
+
+@pytest.mark.gpu
+def test_secondary_selector_keeps_primary_fused_and_gets_the_selector_output():
+    import oracle
+    from openwebrx_amd import params
+    fs = 10000000
+    iq = _iq(fs, 3 * (1 << 20))
+    base = _run("nfm_again", iq)
+    withsec = _run("nfm_secondary_selector", iq)
+    assert base["fused"] and withsec["fused"]
+    assert len(base["audio"]) > 1000 and withsec["audio"] == base["audio"]
+    # selectorBuffer carries the Selector output: the oracle's squelch stage
+    p = params.chain_params(fs, -200000, "nfm")
+    p.sq_level = 1e-15  # ClientDemodulatorChain's default squelch level (-150 dB)
+    ref = oracle.stages(iq, p)["squelch"]
+    tap = withsec["tap"]
+    assert tap.size == ref.size, (tap.size, ref.size)
+    assert rel_rms(tap, ref) < 1e-5
+    # SecondarySelector = Shift(-1000 / 12000) + Bandpass(+-100 / 12000) on that stream
+    g = withsec["sec_params"]
+    sh = [d for d in g if d["class"] == "Shift"][1]
+    bp = [d for d in g if d["class"] == "Bandpass"][1]
+    taps = oracle.bandpass_taps(oracle.filter_len(bp["transition"]), bp["low_cut"], bp["high_cut"])
+    want = oracle.fir_complex(oracle.shift(ref, sh["rate"]), taps)
+    got = withsec["sec"]
+    assert got.size == want.size, (got.size, want.size)
+    assert rel_rms(got, want) < 1e-5
