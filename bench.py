@@ -60,44 +60,89 @@ def gen_stream_torch(torch, dev, fs, n, modes, offsets, seed=20251114):
     return out
 
 
-def cpu_baseline(fs, n_fft, hop, avg, plist, seconds_target=15.0):
-    """Oracle (C restatement, double-precision filters) timed on the host: waterfall + the same
-    chains on a bounded sample, OpenMP over chains (csdr runs one thread per module per chain)."""
+def _host_cpu():
+    """nproc, the CPU model, the cores this process may use (affinity) and the cgroup CPU quota."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota_cpus"] = quota
+    return info
+
+
+def cpu_baseline(fs, n_fft, hop, avg, plist):
+    """The CPU baseline: oracle/cpu_baseline.c -- the same waterfall + chains
+    with the costly stages in fp32 / AVX2-FMA like csdr (Shift + FirDecimate, waterfall FFT),
+    the 12 kHz tail from the oracle -- timed on this host: once on 1 core and once on every core
+    this process may use (the cgroup quota if one is set, else the affinity set).  `value` is
+    the all-cores rate."""
+    import ctypes
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
     from openwebrx_amd import synth
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n = 1 << 20
-    iq, _ = synth.make_iq(fs, n, ["nfm"])
+    host = _host_cpu()
+    allc = host["affinity"]
+    if host["cgroup_quota_cpus"]:
+        allc = max(1, min(allc, int(host["cgroup_quota_cpus"])))
+    lib = orc.lib()
+    fn = lib.cpb_run_workload
+    fn.restype = ctypes.c_int64
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_float, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     cps = [orc.chain_from_engine_params(p) for p in plist]
     arr = (orc.ChainParams * len(cps))(*cps)
-    lib = orc.lib()
-    t0 = time.perf_counter()
-    lib.orc_run_workload(iq.ctypes.data, n, n_fft, hop, avg, -70.0, arr, len(cps), threads)
-    dt = time.perf_counter() - t0
-    # scale the sample up to ~seconds_target of CPU work when the first pass was short
-    if dt < seconds_target / 4:
-        reps = int(max(1, min(8, seconds_target / max(dt, 1e-3) / 2)))
-        n2 = n * reps
-        iq, _ = synth.make_iq(fs, n2, ["nfm"])
+
+    def timed(n, threads):
+        iq, _ = synth.make_iq(fs, n, ["nfm"])
         t0 = time.perf_counter()
-        lib.orc_run_workload(iq.ctypes.data, n2, n_fft, hop, avg, -70.0, arr, len(cps), threads)
-        dt = time.perf_counter() - t0
-        n = n2
-    return {"value": n / dt / 1e6, "unit": "Msps", "cores": threads, "kind": "port",
-            "sample": "%d samples (%.2f s of 10 Msps IQ) through the waterfall + %d chains, "
-                      "oracle/csdr_oracle.c with %d OpenMP threads, %.2f s wall"
-                      % (n, n / fs, len(plist), threads, dt)}
+        fn(iq.ctypes.data, n, n_fft, hop, avg, -70.0, arr, len(cps), threads)
+        return time.perf_counter() - t0
+
+    # sized for a few seconds each: 2^21 samples on one core, 2^22 x cores/8 on all of them
+    n1 = 1 << 21
+    dt1 = timed(n1, 1)
+    nall = max(n1, (1 << 22) * max(1, allc) // 8)
+    dta = timed(nall, allc)
+    return {"value": round(nall / dta / 1e6, 3), "unit": "Msps", "cores": allc,
+            "kind": "port",
+            "one_core_msps": round(n1 / dt1 / 1e6, 4),
+            "host": host,
+            "sample": "%d samples (%.2f s of %.2f Msps IQ) through the waterfall + %d chains on %d "
+                      "cores, %.2f s wall (1 core: %d samples, %.2f s); oracle/cpu_baseline.c "
+                      "(fp32, AVX2+FMA, OpenMP over chains)"
+                      % (nall, nall / fs, fs / 1e6, len(plist), allc, dta, n1, dt1)}
 
 
-def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block):
+def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block,
+                   ddc_mode="fast"):
     """SURVEY.md 8d measurement 1: feed the stream at its nominal rate through the host push path
     (SDR -> host cf32 -> PCIe -> HBM, owrx_push_iq) to a fresh engine with the same waterfall and
     chains; every block is pushed on its wall-clock deadline, then synced and drained.  Keeps up
     when no output ring overran and every block finished within its own period."""
+    t_setup = time.perf_counter()
     eng = Engine(fs, max_block=block)
+    eng.set_ddc_mode(ddc_mode)
     wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
     chains = [eng.chain(p) for p in plist]
+    eng.sync()
+    t_setup = time.perf_counter() - t_setup
     period = block / fs
     nblocks = max(1, int(seconds / period))
     lat = []
@@ -115,12 +160,41 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     st = eng.stats()
     eng.close()
     return {"seconds": round(nblocks * period, 2), "stream_msps": fs / 1e6, "chains": len(plist),
+            "setup_s": round(t_setup, 2),
             "blocks": nblocks, "block_period_ms": round(1e3 * period, 2),
             "max_block_latency_ms": round(1e3 * max(lat), 3),
             "mean_block_latency_ms": round(1e3 * sum(lat) / len(lat), 3),
             "overruns": int(st["overruns"]),
             "keeps_up": bool(st["overruns"] == 0 and max(lat) < period),
             "path": "host cf32 -> owrx_push_iq (PCIe) -> engine, sync + drain per block"}
+
+
+def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, stream_host,
+                        seconds, block, ladder, ddc_mode, budget_s):
+    """BASELINE.md 3 / SURVEY.md 8d: the largest chain count C (from `ladder`) for which the paced
+    real-time check at the config's stream rate keeps up (no overrun, every block within its
+    period), with the waterfall running too.  Stops at the first failure or when the next level
+    would exceed the time budget (chain creation grows with C)."""
+    levels, best = [], 0
+    t0 = time.perf_counter()
+    for C in ladder:
+        if levels and time.perf_counter() - t0 + 4 * levels[-1]["setup_s"] + seconds > budget_s:
+            levels.append({"chains": C, "skipped": "time budget"})
+            break
+        ms = [modes[c % len(modes)] for c in range(C)]
+        plist = [params.chain_params(fs, o, m) for o, m in zip(offsets_of(C), ms)]
+        r = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block,
+                           ddc_mode)
+        levels.append({k: r[k] for k in ("chains", "keeps_up", "max_block_latency_ms",
+                                         "mean_block_latency_ms", "overruns", "setup_s")})
+        if not r["keeps_up"]:
+            break
+        best = C
+    return {"max_realtime_chains": best, "stream_msps": fs / 1e6, "block_samples": block,
+            "seconds_per_level": seconds, "levels": levels,
+            "note": "paced pushes of host cf32 through owrx_push_iq at the stream's wall-clock rate, "
+                    "waterfall + C chains (modes cycled), sync + drain per block; largest C that kept "
+                    "up; the ladder stops at the first level that did not (or the time budget)"}
 
 
 def pmc_traffic(prefix, config):
@@ -155,6 +229,12 @@ def main():
                     help="paced real-time check at 10 Msps through the host push path (0: skip)")
     ap.add_argument("--no-timing", action="store_true",
                     help="skip the per-kernel HIP-event brackets (roofline fields become null)")
+    ap.add_argument("--ddc", default="fast", choices=("fast", "direct"),
+                    help="DDC form: fast-convolution filter bank (default) or direct polyphase FIR")
+    ap.add_argument("--capacity-ladder", default="256,1024,4096,16384",
+                    help="chain counts tried by the max_realtime_chains sweep ('' = skip)")
+    ap.add_argument("--capacity-seconds", type=float, default=2.0,
+                    help="seconds of paced stream per sweep level")
     args = ap.parse_args()
 
     import torch
@@ -193,6 +273,7 @@ def main():
 
     block = args.block
     eng = Engine(fs, max_block=block, device=local)
+    eng.set_ddc_mode(args.ddc)
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:
@@ -311,7 +392,14 @@ def main():
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
         rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
-                            args.realtime_seconds, 1 << 20)
+                            args.realtime_seconds, 1 << 20, args.ddc)
+    cap = None
+    if rank == 0 and world == 1 and args.capacity_ladder:
+        host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        ladder = [int(v) for v in args.capacity_ladder.split(",") if v]
+        cap = max_realtime_chains(Engine, params, fs, n_fft, hop, avg, cfg["modes"],
+                                  lambda c: carrier_offsets(fs, c), host,
+                                  args.capacity_seconds, 1 << 20, ladder, args.ddc, 150.0)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -386,6 +474,8 @@ def main():
                                  ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots",
                                   "host_ms_wait_rows")},
             "realtime": rt,
+            "max_realtime_chains": cap["max_realtime_chains"] if cap else None,
+            "capacity": cap,
             "cpu_baseline": cpu,
             "output_bytes": out_bytes,
         }

@@ -23,13 +23,13 @@ for st in $STAGES; do
       rc=$?; echo "bench rc=$rc" >> gpurun_out/${R}_bench.err; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${R} -o bench \
-        -- python -u bench.py --config $CFG --steps 20 --warmup 10 --no-cpu-baseline --realtime-seconds 0 > gpurun_out/${R}_prof.json 2> gpurun_out/${R}_prof.log
+        -- python -u bench.py --config $CFG --steps 20 --warmup 10 --no-cpu-baseline --realtime-seconds 0 --capacity-ladder "" > gpurun_out/${R}_prof.json 2> gpurun_out/${R}_prof.log
       rc=$?; echo "prof rc=$rc" >> gpurun_out/${R}_prof.log; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       # HBM traffic of the dominant kernel: FETCH_SIZE and WRITE_SIZE in separate passes
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${R}_${CFG}_$c -o pmc \
-          -- python -u bench.py --config $CFG --steps 5 --warmup 3 --no-cpu-baseline --no-timing --realtime-seconds 0 > gpurun_out/${R}_pmc_$c.log 2>&1
+          -- python -u bench.py --config $CFG --steps 5 --warmup 3 --no-cpu-baseline --no-timing --realtime-seconds 0 --capacity-ladder "" > gpurun_out/${R}_pmc_$c.log 2>&1
         rc=$?; echo "pmc $c rc=$rc" >> gpurun_out/${R}_pmc_$c.log; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac
