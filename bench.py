@@ -87,6 +87,14 @@ def _host_cpu():
     return info
 
 
+def _log(msg):
+    """progress on stderr (a long run must keep writing: gpurun takes 180 s of silence as a hang)"""
+    print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
+
+
 def cpu_baseline(fs, n_fft, hop, avg, plist):
     """The CPU baseline: oracle/cpu_baseline.c -- the same waterfall + chains
     with the costly stages in fp32 / AVX2-FMA like csdr (Shift + FirDecimate, waterfall FFT),
@@ -140,7 +148,11 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     eng = Engine(fs, max_block=block)
     eng.set_ddc_mode(ddc_mode)
     wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
-    chains = [eng.chain(p) for p in plist]
+    chains = []
+    for i, p in enumerate(plist):
+        chains.append(eng.chain(p))
+        if i % 1024 == 1023:
+            _log("  %d chains created" % (i + 1))
     eng.sync()
     t_setup = time.perf_counter() - t_setup
     period = block / fs
@@ -183,8 +195,16 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
             break
         ms = [modes[c % len(modes)] for c in range(C)]
         plist = [params.chain_params(fs, o, m) for o, m in zip(offsets_of(C), ms)]
-        r = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block,
-                           ddc_mode)
+        _log("capacity level: %d chains" % C)
+        try:
+            r = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds,
+                               block, ddc_mode)
+        except Exception as exc:  # e.g. out of device memory: this level does not run
+            levels.append({"chains": C, "keeps_up": False, "error": str(exc)[:200]})
+            _log("  failed: %s" % exc)
+            break
+        _log("  setup %.2f s, keeps_up %s, max block latency %.2f ms"
+             % (r["setup_s"], r["keeps_up"], r["max_block_latency_ms"]))
         levels.append({k: r[k] for k in ("chains", "keeps_up", "max_block_latency_ms",
                                          "mean_block_latency_ms", "overruns", "setup_s")})
         if not r["keeps_up"]:
@@ -231,7 +251,7 @@ def main():
                     help="skip the per-kernel HIP-event brackets (roofline fields become null)")
     ap.add_argument("--ddc", default="fast", choices=("fast", "direct"),
                     help="DDC form: fast-convolution filter bank (default) or direct polyphase FIR")
-    ap.add_argument("--capacity-ladder", default="256,1024,4096,16384",
+    ap.add_argument("--capacity-ladder", default="256,1024,4096,16384,32768,65536",
                     help="chain counts tried by the max_realtime_chains sweep ('' = skip)")
     ap.add_argument("--capacity-seconds", type=float, default=2.0,
                     help="seconds of paced stream per sweep level")
@@ -391,6 +411,7 @@ def main():
     rt = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        _log("real-time check")
         rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
                             args.realtime_seconds, 1 << 20, args.ddc)
     cap = None
@@ -403,6 +424,7 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
+            _log("cpu baseline")
             cpu = cpu_baseline(fs, n_fft, hop, avg, plist)
         res = {
             "metric": METRIC,

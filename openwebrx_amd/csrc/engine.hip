@@ -776,13 +776,16 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         fprintf(stderr, "owrx: DDC group D=%d P=%d chains=%d: %lld tile groups x %d segments, "
                 "%lld resident workgroups\n", g->D, g->P, n, (long long)base, nseg, (long long)slots);
     const size_t need = (size_t)nseg * std::max(1, n) * nk_max;
+    // geometric growth (x1.5): adding chains one at a time must not reallocate every time
+    // (buffers proportional to the membership: quadratic setup time at thousands of chains)
     if (need > g->partial_elems) {
         RCCHK(drain_all(e));
+        const size_t alloc = need + need / 2;
         for (int i = 0; i < kSlots; ++i) {
             dfree(g->d_partial[i]);
-            HIPCHK(dalloc(&g->d_partial[i], need));
+            HIPCHK(dalloc(&g->d_partial[i], alloc));
         }
-        g->partial_elems = need;
+        g->partial_elems = alloc;
     }
     g->nseg = nseg;
     if (g->fc_logm) {  // fast-convolution product rows Y[chains][Fs][M]
@@ -790,8 +793,8 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         if (ny > g->fc_y_elems) {
             RCCHK(drain_all(e));
             dfree(g->d_fc_y);
-            HIPCHK(dalloc(&g->d_fc_y, ny));
-            g->fc_y_elems = ny;
+            HIPCHK(dalloc(&g->d_fc_y, ny + ny / 2));
+            g->fc_y_elems = ny + ny / 2;
         }
     }
     return OWRX_OK;

@@ -16,3 +16,18 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(scope="session")
+def parity_report():
+    """report(test, **metrics): appends one JSON line to gpurun_out/parity_metrics.jsonl (the
+    measured parity figures -- exact-match fractions, rel-RMS -- kept beside the pass/fail)."""
+    import json
+    path = os.path.join(ROOT, "gpurun_out", "parity_metrics.jsonl")
+
+    def report(test, **metrics):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test, **metrics}) + "\n")
+        print(test, metrics)
+    return report
