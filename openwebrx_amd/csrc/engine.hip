@@ -84,7 +84,7 @@ constexpr int kSelPad = 64 * 4 * 6;    // serial lane lists: 64-lane padding per
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
 constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
-constexpr int kRowSlots = 4;  // waterfall row blocks in flight (encoded in order on stream R)
+constexpr int kRowSlots = 4;  // waterfall row blocks in flight (each on its own stream, R CUs)
 
 #define HIPCHK(expr)                                                                    \
     do {                                                                                \
@@ -318,7 +318,7 @@ struct Slot {  // one block's outputs in flight on streams B / C
 };
 
 struct RowSlot {  // one block's waterfall rows being encoded / copied on stream R
-    hipStream_t stream = nullptr;  // = engine sR
+    hipStream_t stream = nullptr;  // own stream on the R CUs (row slots encode concurrently)
     hipEvent_t evWf = nullptr;  // stream A finished the block's finalize
     hipEvent_t evC = nullptr;   // rows copied to host
     bool pending = false;
@@ -1351,7 +1351,10 @@ static hipError_t create_streams(owrx_engine* e) {
     int ncu = 0;
     hipError_t err = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device);
     if (err != hipSuccess) return err;
-    int nb = 4, nc = 4, nr = 4;
+    // R (8 CUs) holds the output gathers and the waterfall row encoders: one stream per row
+    // slot, so the rows of consecutive blocks (independent: FftAdpcm restarts every row)
+    // encode concurrently instead of queueing behind each other
+    int nb = 4, nc = 4, nr = 8;
     if (const char* v = getenv("OWRX_SERIAL_CUS")) {
         if (sscanf(v, "%d,%d,%d", &nb, &nc, &nr) != 3) nb = nc = nr = 0;
     }
@@ -1359,6 +1362,10 @@ static hipError_t create_streams(owrx_engine* e) {
     if (nb <= 0 || nc <= 0 || nr <= 0 || nb + nc + nr > ncu / 2) {
         for (hipStream_t* st : {&e->sA, &e->sB, &e->sC, &e->sR}) {
             err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+            if (err != hipSuccess) return err;
+        }
+        for (auto& r : e->rslots) {
+            err = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking);
             if (err != hipSuccess) return err;
         }
         return hipSuccess;
@@ -1379,6 +1386,10 @@ static hipError_t create_streams(owrx_engine* e) {
         {&e->sA, &mA}, {&e->sB, &mB}, {&e->sC, &mC}, {&e->sR, &mR}};
     for (auto& x : sm) {
         err = hipExtStreamCreateWithCUMask(x.first, (uint32_t)words, x.second->data());
+        if (err != hipSuccess) return err;
+    }
+    for (auto& r : e->rslots) {
+        err = hipExtStreamCreateWithCUMask(&r.stream, (uint32_t)words, mR.data());
         if (err != hipSuccess) return err;
     }
     return hipSuccess;
@@ -1407,7 +1418,6 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
     };
     if (create_streams(e) != hipSuccess) return fail("stream");
     for (auto& r : e->rslots) {
-        r.stream = e->sR;
         if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
             return fail("row stream");
@@ -1444,6 +1454,8 @@ int owrx_engine_destroy(owrx_engine* e) {
     hipSetDevice(e->device);
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR})
         if (st) hipStreamSynchronize(st);
+    for (auto& r : e->rslots)
+        if (r.stream) hipStreamSynchronize(r.stream);
     for (auto& kv : e->chains) free_chain(kv.second.get());
     for (auto& kv : e->wfs) free_wf(kv.second.get());
     dfree(e->d_nr_win);
@@ -1473,6 +1485,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     for (auto& r : e->rslots) {
         if (r.evWf) hipEventDestroy(r.evWf);
         if (r.evC) hipEventDestroy(r.evC);
+        if (r.stream) hipStreamDestroy(r.stream);
     }
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR})
         if (st) hipStreamDestroy(st);

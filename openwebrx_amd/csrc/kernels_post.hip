@@ -602,8 +602,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                   const int* __restrict__ sel, int nsel) {
     __shared__ float2 ue[2][kSerChunk][64];  // wave 0 -> waves 1, 2: (u, envelope)
     __shared__ float as_[2][kSerChunk][65];  // waves 1-3: AGC output, [sample][chain], padded
-    __shared__ int64_t s_lim[64];            // per chain: samples to store (0: inactive lane)
-    __shared__ void* s_ptr[64];              // per chain: destination of sample 0
+    __shared__ float in_[2][kSerChunk][65];  // waves 1-3 -> wave 0: demodulator output, staged
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const SerLane sl = ser_lane(sel, nsel);
@@ -622,25 +621,56 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     ChainStateS* sp = Pp->sstate;
     const int demod = __builtin_amdgcn_readfirstlane(Pp->demod);  // uniform (see ser_lane)
 
+    // Waves 1-3 move the data, lane = chain, in quads of samples: quad q (samples 4q .. 4q+3 of
+    // a chunk) belongs to wave 1 + q % 3.  Input staging: the recurrences are a few dependent
+    // VALU ops per sample, so a global load per sample (an L2 / MALL round trip: the
+    // demodulator output was written by other CUs) would set the pace; instead chunk c + 1 is
+    // loaded (16-B loads from each chain's own buffer) while wave 0 walks chunk c out of LDS.
+    constexpr int kQuads = kSerChunk / 4;
+    constexpr int kQPerWave = (kQuads + 2) / 3;
+    const auto dem_in = gp(reinterpret_cast<const float4*>(Pp->dem));
+    float4 pre[kQPerWave];
+    auto stage_load = [&](int ch) {
+#pragma unroll
+        for (int k = 0; k < kQPerWave; ++k) {
+            const int q = wave - 1 + 3 * k;
+            const int i = ch * kSerChunk + 4 * q;
+            pre[k] = (q < kQuads && i < n) ? dem_in[i >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto stage_store = [&](int ch) {
+#pragma unroll
+        for (int k = 0; k < kQPerWave; ++k) {
+            const int q = wave - 1 + 3 * k;
+            if (q < kQuads) {
+                in_[ch & 1][4 * q][lane] = pre[k].x;
+                in_[ch & 1][4 * q + 1][lane] = pre[k].y;
+                in_[ch & 1][4 * q + 2][lane] = pre[k].z;
+                in_[ch & 1][4 * q + 3][lane] = pre[k].w;
+            }
+        }
+    };
+    if (wave != 0 && nchunks > 0) {
+        stage_load(0);
+        stage_store(0);
+    }
+    __syncthreads();
+
     if (wave == 0) {
         // ---- recurrences: NfmDeemphasis | DcBlock, AGC envelope -> (u, env)
         float deemph_y = sp->deemph_y, dc_xp = sp->dc_xp, dc_yp = sp->dc_yp;
         AgcState agc = sp->agc;
         const float alpha = Pp->deemph_alpha, beta = Pp->deemph_beta;
-        const auto dem = gp(Pp->dem);
-        // inputs stream through 8 registers, the next 8 always in flight (across chunks too;
-        // the demodulator slot has slack past the end)
-        float cur[8], nxt[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) cur[j] = dem[j];
         auto run = [&](auto dm, auto fl, int ch) {
             constexpr int DM = decltype(dm)::value;
             constexpr bool FULL = decltype(fl)::value;
             const int base = ch * kSerChunk;
             float2(*dst)[64] = ue[ch & 1];
+            const float(*src)[65] = in_[ch & 1];
             for (int i = 0; i < kSerChunk; i += 8) {
+                float cur[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) nxt[j] = dem[base + i + 8 + j];
+                for (int j = 0; j < 8; ++j) cur[j] = src[i + j][lane];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float v = cur[j];
@@ -667,8 +697,6 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                         agc.env = ke;
                     }
                 }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
             }
         };
         auto run_dm = [&](auto dm, int ch) {
@@ -695,33 +723,34 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     } else {
         // ---- gain + Convert (waves 1..3 take every third sample), one chunk behind; a chain
         // with a NoiseFilter stores the AGC output for chain_nr instead (Convert follows it).
-        // The results go through LDS (as_) and are written out one more chunk behind,
-        // transposed: lane = sample, so each chain's chunk is one contiguous store per wave
-        // instead of 64 lanes touching 64 chains' cache lines per sample.
-        if (wave == 1) {
-            const bool nr = NR && sl.active;
-            const int64_t nr_fill = nr ? kNrHop + Pp->nr_state->pend : 0;
-            int64_t lim = 0;
-            void* dptr = nullptr;
-            if (sl.active) {
-                if (NR) {
-                    lim = n;
-                    dptr = Pp->nr_in + nr_fill;
-                } else if (OUT == 2) {
-                    lim = min((int64_t)n, Pp->out_cap / 4);
-                    dptr = Pp->out;
-                } else if (OUT == 0) {
-                    lim = min((int64_t)n, Pp->out_cap / 2);
-                    dptr = Pp->out;
-                } else {
-                    lim = INT64_MAX;  // the ADPCM scratch's slack covers the ragged chunk
-                    dptr = Pp->s16;
-                }
+        // The results go through LDS (as_) and are written out one more chunk behind, lane =
+        // chain, a quad of samples per store (8-B int16 / 16-B float vectors where aligned).
+        const bool nr = NR && sl.active;
+        const int64_t nr_fill = nr ? kNrHop + Pp->nr_state->pend : 0;
+        int64_t lim = 0;
+        void* dptr = nullptr;
+        if (sl.active) {
+            if (NR) {
+                lim = n;
+                dptr = Pp->nr_in + nr_fill;
+            } else if (OUT == 2) {
+                lim = min((int64_t)n, Pp->out_cap / 4);
+                dptr = Pp->out;
+            } else if (OUT == 0) {
+                lim = min((int64_t)n, Pp->out_cap / 2);
+                dptr = Pp->out;
+            } else {
+                lim = n;  // the chain's int16 scratch (read by chain_adpcm)
+                dptr = Pp->s16;
             }
-            s_lim[lane] = lim;
-            s_ptr[lane] = dptr;
         }
+        constexpr bool kF32 = NR || OUT == 2;
+        const bool vec = ((uintptr_t)dptr & (kF32 ? 15 : 7)) == 0;
+        float* const tap = sl.active ? Pp->tap_agc : nullptr;
+        const int64_t tap_cap = Pp->tap_agc_cap;
         for (int it = 0; it < nchunks + 2; ++it) {
+            const bool ld = it + 1 < nchunks;  // stage chunk it + 1 for wave 0
+            if (ld) stage_load(it + 1);
             const int ch = it - 1;
             if (ch >= 0 && ch < nchunks) {
                 const int base = ch * kSerChunk;
@@ -740,8 +769,7 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     as_[ch & 1][j][lane] = a;
                     {   // audioBuffer readers (a secondary demodulator on the audio)
                         const int64_t qi = base + j;
-                        if (sl.active && Pp->tap_agc && (full || qi < n) && qi < Pp->tap_agc_cap)
-                            gp(Pp->tap_agc)[qi] = a;
+                        if (tap && (full || qi < n) && qi < tap_cap) gp(tap)[qi] = a;
                     }
                     if (DEBUG) {
                         const int64_t qi = base + j;
@@ -756,16 +784,41 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             const int w = it - 2;  // chunk written out this iteration (as_ complete since the
             if (w >= 0) {          // previous barrier)
                 const float(*src)[65] = as_[w & 1];
-                const int64_t qi = (int64_t)w * kSerChunk + lane;
-                for (int cc = wave - 1; cc < 64; cc += kFrontThreads / 64 - 1) {
-                    const int64_t lim = s_lim[cc];
-                    if (qi < lim) {
-                        const float a = src[lane][cc];
-                        if (NR || OUT == 2) gp(reinterpret_cast<float*>(s_ptr[cc]))[qi] = a;
-                        else gp(reinterpret_cast<int16_t*>(s_ptr[cc]))[qi] = convert_s16(a);
+#pragma unroll
+                for (int k = 0; k < kQPerWave; ++k) {
+                    const int q = wave - 1 + 3 * k;
+                    const int64_t i0 = (int64_t)w * kSerChunk + 4 * q;
+                    if (q >= kQuads || i0 >= lim) continue;
+                    const float v0 = src[4 * q][lane], v1 = src[4 * q + 1][lane];
+                    const float v2 = src[4 * q + 2][lane], v3 = src[4 * q + 3][lane];
+                    if (kF32) {
+                        float* d = reinterpret_cast<float*>(dptr) + i0;
+                        if (vec && i0 + 4 <= lim) {
+                            *gp(reinterpret_cast<float4*>(d)) = make_float4(v0, v1, v2, v3);
+                        } else {
+                            gp(d)[0] = v0;
+                            if (i0 + 1 < lim) gp(d)[1] = v1;
+                            if (i0 + 2 < lim) gp(d)[2] = v2;
+                            if (i0 + 3 < lim) gp(d)[3] = v3;
+                        }
+                    } else {
+                        int16_t* d = reinterpret_cast<int16_t*>(dptr) + i0;
+                        const int16_t s0 = convert_s16(v0), s1 = convert_s16(v1);
+                        const int16_t s2 = convert_s16(v2), s3 = convert_s16(v3);
+                        if (vec && i0 + 4 <= lim) {
+                            const uint2 pk = make_uint2((uint32_t)(uint16_t)s0 | ((uint32_t)(uint16_t)s1 << 16),
+                                                        (uint32_t)(uint16_t)s2 | ((uint32_t)(uint16_t)s3 << 16));
+                            *gp(reinterpret_cast<uint2*>(d)) = pk;
+                        } else {
+                            gp(d)[0] = s0;
+                            if (i0 + 1 < lim) gp(d)[1] = s1;
+                            if (i0 + 2 < lim) gp(d)[2] = s2;
+                            if (i0 + 3 < lim) gp(d)[3] = s3;
+                        }
                     }
                 }
             }
+            if (ld) stage_store(it + 1);
             __syncthreads();
         }
     }

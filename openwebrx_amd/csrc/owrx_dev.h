@@ -42,6 +42,8 @@ struct AdpcmState {
 // ext_vector type.)
 template <typename T> struct GNative { using type = T; };
 template <> struct GNative<float2> { using type = float __attribute__((ext_vector_type(2))); };
+template <> struct GNative<float4> { using type = float __attribute__((ext_vector_type(4))); };
+template <> struct GNative<uint2> { using type = unsigned int __attribute__((ext_vector_type(2))); };
 
 template <typename T>
 struct GRef {
