@@ -46,6 +46,11 @@ extern "C" {
 #define OWRX_OUT_F32 2      /* raw float audio (no Convert) */
 #define OWRX_OUT_IQ 3       /* Shift + FirDecimate output only, cf32 at in/D: the service
                                Resampler (owrx/source/resampler.py:11-26) */
+#define OWRX_OUT_SEL 4      /* the whole Selector's output, cf32 at the output rate (Shift,
+                               FirDecimate, FractionalDecimator, Bandpass, Squelch if any): an
+                               IQ-input decoder behind Selector(withSquelch=False), the
+                               ServiceDemodulatorChain (owrx/service/chain.py:7-23); `demod`,
+                               the AGC and the audio fields are unused */
 
 #define OWRX_AGC_FAST 0
 #define OWRX_AGC_SLOW 1

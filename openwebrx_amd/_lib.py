@@ -20,7 +20,7 @@ OWRX_ENOSPC = -28
 OWRX_ENODEV = -19
 
 DEMOD_NFM, DEMOD_AM, DEMOD_SSB, DEMOD_WFM = 0, 1, 2, 3
-OUT_S16, OUT_ADPCM, OUT_F32, OUT_IQ = 0, 1, 2, 3
+OUT_S16, OUT_ADPCM, OUT_F32, OUT_IQ, OUT_SEL = 0, 1, 2, 3, 4
 AGC_FAST, AGC_SLOW, AGC_MID, AGC_LAGGY = 0, 1, 2, 3
 
 MOD_FMDEMOD = 1

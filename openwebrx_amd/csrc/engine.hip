@@ -1730,8 +1730,11 @@ static int chain_validate(const owrx_chain_params* p) {
                    ? OWRX_EINVAL : OWRX_OK;
     if (!p || p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate <= 0 ||
         p->sq_length <= 0 || p->sq_length > (1 << 20) || p->sq_decimation <= 0 || p->demod < 0 ||
-        p->demod > OWRX_DEMOD_WFM || p->output < 0 || p->output > 2 || p->audio_rate <= 0 ||
+        p->demod > OWRX_DEMOD_WFM || p->output < 0 || p->output > OWRX_OUT_SEL ||
+        p->output == OWRX_OUT_IQ || p->audio_rate <= 0 ||
         p->agc_profile < 0 || p->agc_profile > 3)
+        return OWRX_EINVAL;
+    if (p->output == OWRX_OUT_SEL && (p->demod == OWRX_DEMOD_WFM || p->nr_enabled))
         return OWRX_EINVAL;
     if (p->demod == OWRX_DEMOD_WFM && (p->if_rate <= 0 || p->if_rate / p->audio_rate < 1.0))
         return OWRX_EINVAL;
@@ -1836,8 +1839,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     c->rate_fx = rate_to_fx(p->shift_rate);
     c->cap = chain_stage_cap(e, D, p->frac_rate);
     const int64_t scap = c->cap + p->sq_length + 16;
-    c->out_cap = p->output == OWRX_OUT_IQ ? 8 * c->cap + 64
-                                          : 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
+    c->out_cap = p->output == OWRX_OUT_IQ    ? 8 * c->cap + 64
+                 : p->output == OWRX_OUT_SEL ? 8 * scap + 64
+                                             : 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
     c->sm_cap = p->output == OWRX_OUT_IQ ? 4 : (int)(scap / p->sq_length + 4);
     if (p->output != OWRX_OUT_IQ && scap / p->sq_length + 2 > 1024) {  // kMaxSqBlocks
         set_last_error("owrx_chain_create: squelch length %d too short for the block size",

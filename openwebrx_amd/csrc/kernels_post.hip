@@ -411,8 +411,14 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
     // ---- 4. demodulator front (per-sample independent) ------------------------------------
     const int nsq = nb * L;
     const float2 fm_prev0 = S.fm_last;
+    const bool sel_out = P.output == OWRX_OUT_SEL;  // the Selector output is the product
     for (int i = tid; i < nsq; i += NT) {
         const float2 x = sh_pass[i / L] ? sq_buf[i] : make_float2(0.0f, 0.0f);
+        if (sel_out) {
+            if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
+            if ((int64_t)(i + 1) * 8 <= P.out_cap) reinterpret_cast<float2*>(P.out)[i] = x;
+            continue;
+        }
         if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
         if (P.tap_sq && i < P.tap_sq_cap) P.tap_sq[i] = x;  // selectorBuffer readers
         if (P.sf_n > 0) P.sf_buf[sf_fill + i] = x;  // Selector output -> secondary FFT
@@ -433,7 +439,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
     }
     __syncthreads();
     int n_audio = nsq;
-    if (P.demod == 3) n_audio = wfm_audio(P, S, nsq);
+    if (P.demod == 3 && !sel_out) n_audio = wfm_audio(P, S, nsq);
     {   // move the incomplete squelch block to the front
         const int rem = total - nsq;
         float2 last = S.fm_last;
@@ -473,6 +479,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
             c.n_sq = n_audio;
             c.n_front = n_audio;
             c.n_gate = nsq;
+            if (sel_out) c.out_bytes = min((int64_t)nsq * 8, P.out_cap & ~(int64_t)7);
         }
     }
 }
@@ -573,10 +580,12 @@ bp_long(const ChainPost* __restrict__ posts, const ChainCounts* __restrict__ cou
 // post_serial_front: the per-chain recurrences after the demodulator, one LANE per chain
 // (64 chains per workgroup), four waves pipelined by chunks of kSerChunk samples through LDS:
 //   wave 0    NfmDeemphasis | DcBlock and the AGC envelope (chunk c) -> (u, env) in LDS
-//   wave 1-3  gain = reference / env (clamped), a = u * gain, Convert (chunk c-1, every third
-//             sample each -- the IEEE division makes this the heavier half): int16 to the
-//             output slot (S16), float (F32), or the chain's int16 scratch for the ADPCM
-//             encoder (chain_adpcm below)
+//   wave 1    loads chunk c + 1 of every chain into LDS (the only wave with global loads, so
+//             its waits never cover outstanding stores), and a quarter of the gain work
+//   wave 1-3  gain = reference / env (clamped), a = u * gain (chunk c - 1; the IEEE division
+//             makes this the heavier half)
+//   wave 2-3  Convert + store (chunk c - 2): int16 to the output slot (S16), float (F32), or
+//             the chain's int16 scratch for the ADPCM encoder (chain_adpcm below)
 // The arithmetic is exactly deemph_step / dcblock_step / agc_step / convert_s16 split at the
 // AGC gain, so the result is bit-identical to the sequential order (oracle orc_agc etc.).
 constexpr int kSerChunk = 64;
@@ -621,36 +630,31 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     ChainStateS* sp = Pp->sstate;
     const int demod = __builtin_amdgcn_readfirstlane(Pp->demod);  // uniform (see ser_lane)
 
-    // Waves 1-3 move the data, lane = chain, in quads of samples: quad q (samples 4q .. 4q+3 of
-    // a chunk) belongs to wave 1 + q % 3.  Input staging: the recurrences are a few dependent
-    // VALU ops per sample, so a global load per sample (an L2 / MALL round trip: the
-    // demodulator output was written by other CUs) would set the pace; instead chunk c + 1 is
-    // loaded (16-B loads from each chain's own buffer) while wave 0 walks chunk c out of LDS.
+    // Data movement is lane = chain, in quads of samples (samples 4q .. 4q+3 of a chunk).
+    // Input staging: the recurrences are a few dependent VALU ops per sample, so a global load
+    // per sample (an L2 / MALL round trip: the demodulator output was written by other CUs)
+    // would set the pace; wave 1 loads chunk c + 1 (16-B loads from each chain's own buffer)
+    // while wave 0 walks chunk c out of LDS.
     constexpr int kQuads = kSerChunk / 4;
-    constexpr int kQPerWave = (kQuads + 2) / 3;
     const auto dem_in = gp(reinterpret_cast<const float4*>(Pp->dem));
-    float4 pre[kQPerWave];
+    float4 pre[kQuads];
     auto stage_load = [&](int ch) {
 #pragma unroll
-        for (int k = 0; k < kQPerWave; ++k) {
-            const int q = wave - 1 + 3 * k;
+        for (int q = 0; q < kQuads; ++q) {
             const int i = ch * kSerChunk + 4 * q;
-            pre[k] = (q < kQuads && i < n) ? dem_in[i >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
+            pre[q] = i < n ? dem_in[i >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
     auto stage_store = [&](int ch) {
 #pragma unroll
-        for (int k = 0; k < kQPerWave; ++k) {
-            const int q = wave - 1 + 3 * k;
-            if (q < kQuads) {
-                in_[ch & 1][4 * q][lane] = pre[k].x;
-                in_[ch & 1][4 * q + 1][lane] = pre[k].y;
-                in_[ch & 1][4 * q + 2][lane] = pre[k].z;
-                in_[ch & 1][4 * q + 3][lane] = pre[k].w;
-            }
+        for (int q = 0; q < kQuads; ++q) {
+            in_[ch & 1][4 * q][lane] = pre[q].x;
+            in_[ch & 1][4 * q + 1][lane] = pre[q].y;
+            in_[ch & 1][4 * q + 2][lane] = pre[q].z;
+            in_[ch & 1][4 * q + 3][lane] = pre[q].w;
         }
     };
-    if (wave != 0 && nchunks > 0) {
+    if (wave == 1 && nchunks > 0) {
         stage_load(0);
         stage_store(0);
     }
@@ -747,29 +751,36 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
         constexpr bool kF32 = NR || OUT == 2;
         const bool vec = ((uintptr_t)dptr & (kF32 ? 15 : 7)) == 0;
         float* const tap = sl.active ? Pp->tap_agc : nullptr;
-        const int64_t tap_cap = Pp->tap_agc_cap;
-        for (int it = 0; it < nchunks + 2; ++it) {
-            const bool ld = it + 1 < nchunks;  // stage chunk it + 1 for wave 0
-            if (ld) stage_load(it + 1);
-            const int ch = it - 1;
-            if (ch >= 0 && ch < nchunks) {
-                const int base = ch * kSerChunk;
-                const float2(*srcu)[64] = ue[ch & 1];
-                const bool full = ch < nfull;
-#pragma unroll 8
-                for (int j = wave - 1; j < kSerChunk; j += kFrontThreads / 64 - 1) {
+        int tap_lim = tap ? (int)min<int64_t>(Pp->tap_agc_cap, INT_MAX) : 0;
+        float g_ref = agcp.reference, g_max = agcp.max_gain;
+        // materialise the descriptor loads here: a first use inside the loop would wait for
+        // every load in flight there (vmcnt(0)), including wave 1's staging loads
+        asm volatile("" : "+v"(tap_lim), "+v"(g_ref), "+v"(g_max), "+v"(lim), "+v"(dptr));
+        // gain samples of a chunk: j % 8 in {0, 1} (wave 1), {2, 3, 4} (wave 2), {5, 6, 7} (3);
+        // fully unrolled per wave (no inner loop: a loop header would make the compiler wait
+        // for wave 1's in-flight loads before the gain work instead of after it)
+        auto gain = [&](auto lo_c, auto cnt_c, int ch) {
+            constexpr int LO = decltype(lo_c)::value, CNT = decltype(cnt_c)::value;
+            const int base = ch * kSerChunk;
+            const float2(*srcu)[64] = ue[ch & 1];
+            const bool full = ch < nfull;
+#pragma unroll
+            for (int g8 = 0; g8 < kSerChunk / 8; ++g8) {
+#pragma unroll
+                for (int r = 0; r < CNT; ++r) {
+                    const int j = g8 * 8 + LO + r;
                     const float2 q = srcu[j][lane];
                     float a;
                     {
 #pragma clang fp contract(off)
-                        float g = (q.y > 0.0f) ? agcp.reference / q.y : agcp.max_gain;
-                        if (g > agcp.max_gain) g = agcp.max_gain;
+                        float g = (q.y > 0.0f) ? g_ref / q.y : g_max;
+                        if (g > g_max) g = g_max;
                         a = g * q.x;
                     }
                     as_[ch & 1][j][lane] = a;
                     {   // audioBuffer readers (a secondary demodulator on the audio)
-                        const int64_t qi = base + j;
-                        if (tap && (full || qi < n) && qi < tap_cap) gp(tap)[qi] = a;
+                        const int qi = base + j;
+                        if ((full || qi < n) && qi < tap_lim) gp(tap)[qi] = a;
                     }
                     if (DEBUG) {
                         const int64_t qi = base + j;
@@ -781,14 +792,28 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     }
                 }
             }
+        };
+        using I0 = std::integral_constant<int, 0>;
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        using I5 = std::integral_constant<int, 5>;
+        for (int it = 0; it < nchunks + 2; ++it) {
+            const bool ld = wave == 1 && it + 1 < nchunks;  // stage chunk it + 1 for wave 0
+            if (ld) stage_load(it + 1);
+            const int ch = it - 1;
+            if (ch >= 0 && ch < nchunks) {
+                if (wave == 1) gain(I0{}, I2{}, ch);
+                else if (wave == 2) gain(I2{}, I3{}, ch);
+                else gain(I5{}, I3{}, ch);
+            }
             const int w = it - 2;  // chunk written out this iteration (as_ complete since the
-            if (w >= 0) {          // previous barrier)
+            if (w >= 0 && wave >= 2) {  // previous barrier); quads alternate waves 2, 3
                 const float(*src)[65] = as_[w & 1];
 #pragma unroll
-                for (int k = 0; k < kQPerWave; ++k) {
-                    const int q = wave - 1 + 3 * k;
+                for (int k = 0; k < kQuads / 2; ++k) {
+                    const int q = wave - 2 + 2 * k;
                     const int64_t i0 = (int64_t)w * kSerChunk + 4 * q;
-                    if (q >= kQuads || i0 >= lim) continue;
+                    if (i0 >= lim) continue;
                     const float v0 = src[4 * q][lane], v1 = src[4 * q + 1][lane];
                     const float v2 = src[4 * q + 2][lane], v3 = src[4 * q + 3][lane];
                     if (kF32) {
@@ -824,36 +849,78 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     }
 }
 
-// AdpcmEncoder(sync=True), one LANE per chain (64 chains per wave).  IMA-ADPCM's predictor
-// carries offsets indefinitely (two encoders started apart on the same audio do not re-merge),
-// so unlike the waterfall rows the chain audio cannot be encoded speculatively in segments;
-// this kernel is the serial recurrence with the per-sample work cut to the state update:
-// samples prefetched 8 ahead from the int16 scratch, successor index / step from the LDS
-// table (adpcm_encode_tab), one byte per sample pair (low nibble first) and a "SYNC" +
-// (index, predictor) frame before the byte whose data count is a multiple of 1001
-// (AudioEngine.js:449-491).  It runs on its own stream behind post_serial_front, so block k's
-// encoding overlaps block k+1's front and block k+2's DDC.
-__global__ void __launch_bounds__(64)
+// AdpcmEncoder(sync=True), one LANE per chain (64 chains per workgroup).  IMA-ADPCM's
+// predictor carries offsets indefinitely (two encoders started apart on the same audio do not
+// re-merge), so unlike the waterfall rows the chain audio cannot be encoded speculatively in
+// segments; this kernel is the serial recurrence with everything else moved off its path:
+//   wave 1  stages the int16 input (16-B loads, lane = chain) into an LDS ring one chunk of
+//           kAdChunk samples ahead, so the encoder never waits on memory;
+//   wave 0  encodes groups of 8 samples out of LDS (one ds_read_b128 per group) with the
+//           table step (adpcm_encode_tab: successor index / step in one LDS read) and emits the
+//           group's 4 completed bytes as one store.
+// Byte stream: low nibble first; a byte started by the last sample of a block completes with
+// the next block's first sample (has_left).  Frames: "SYNC" + (index, predictor) before every
+// byte whose index in the chain's byte stream is a multiple of 1001 (AudioEngine.js:449-491),
+// written with the state before that byte's first sample.  A group in which any lane starts
+// such a byte, or which runs past a lane's last sample, takes the checked per-sample path.
+// Runs on stream C behind post_serial_front, so block k's encoding overlaps block k+1's front
+// and block k+2's DDC.
+constexpr int kAdChunk = 128;                  // samples per staged chunk (16 groups of 8)
+constexpr int kAdGroups = kAdChunk / 8;
+
+typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
+
+__global__ void __launch_bounds__(128)
 chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
             const int* __restrict__ sel, int nsel) {
     __shared__ __align__(16) uint32_t NS[kAdpcmTabEntries];
-    const int lane = threadIdx.x;
-    adpcm_tab_fill(NS, lane, 64);
-    __syncthreads();
+    __shared__ uint4 ring[2][kAdGroups][64];  // [slot][group][lane]: 8 int16 samples
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    adpcm_tab_fill(NS, threadIdx.x, 128);
     const SerLane sl = ser_lane(sel, nsel);
     const int c = sl.c;
     const ChainPost* Pp = posts + c;
     const int n = sl.active ? (int)counts[c].n_sq : 0;
+    int nmax = n, nmin = sl.active ? n : INT_MAX;
+    for (int o = 32; o > 0; o >>= 1) {
+        nmax = max(nmax, __shfl_xor(nmax, o));
+        nmin = min(nmin, __shfl_xor(nmin, o));
+    }
+    const int nchunks = (nmax + kAdChunk - 1) / kAdChunk;
+    const auto src = gp(reinterpret_cast<const uint4*>(Pp->s16));  // 16-B aligned slot
+
+    auto stage = [&](int ch) {  // wave 1: chunk ch -> ring slot ch & 1
+        uint4 v[kAdGroups];
+#pragma unroll
+        for (int g = 0; g < kAdGroups; ++g) {
+            const int i = ch * kAdChunk + 8 * g;
+            v[g] = i < n ? src[i >> 3] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < kAdGroups; ++g) ring[ch & 1][g][lane] = v[g];
+    };
+    if (wave == 1 && nchunks > 0) stage(0);
+    __syncthreads();
+
+    if (wave == 1) {
+        for (int ch = 0; ch < nchunks; ++ch) {
+            if (ch + 1 < nchunks) stage(ch + 1);
+            __syncthreads();
+        }
+        return;
+    }
+
+    // ---- wave 0: the encoder
     ChainStateS* sp = Pp->sstate;
     const ChainStateS st0 = *sp;
-    const auto src = gp(Pp->s16);
+    AdpcmTab ad = adpcm_tab_state(st0.adpcm);
+    const int pend = st0.has_left;  // 1: bytes start at odd samples of this block
+    int left = st0.left_code;       // the started byte's low nibble (pend == 1)
+    int64_t K = st0.adpcm_bytes + pend;  // index of the next byte to start
+    int kmod = (int)(K % kAdpcmSyncPeriod);
     const auto out = gp(Pp->out);
     const int64_t cap = Pp->out_cap;
-    AdpcmTab ad = adpcm_tab_state(st0.adpcm);
-    int has_left = st0.has_left;
-    int left = st0.left_code;
-    int64_t bytes = st0.adpcm_bytes;
-    int until_sync = 0;  // data bytes before the next "SYNC" frame (set below)
     int ob = 0;  // bytes staged this block (< 2^31)
     auto frame = [&]() {
         if (sl.active && ob + 8 <= cap) {
@@ -865,116 +932,73 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
             for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
         }
         ob += 8;
-        until_sync = kAdpcmSyncPeriod;
     };
-    // a pending nibble pairs with sample 0
-    int i0 = 0;
-    if (has_left && n > 0) {
-        const int code = adpcm_encode_tab(ad, src[0], NS);
-        if (ob < cap) out[ob] = (uint8_t)(left | (code << 4));
-        ob++;
-        bytes++;  // this byte's frame (if due) went out with its first nibble, last block
-        has_left = 0;
-        i0 = 1;
-    }
-    until_sync = (int)((kAdpcmSyncPeriod - (bytes % kAdpcmSyncPeriod)) % kAdpcmSyncPeriod);
-    // pairs (i0 + 2j, i0 + 2j + 1); a byte starts at every pair
-    const int np = (n - i0) >> 1;
-    // idle lanes run along on their workgroup's first chain (reads only; stores are masked)
-    int npmax = np, npmin = sl.active ? np : INT_MAX;
-    for (int o = 32; o > 0; o >>= 1) {
-        npmax = max(npmax, __shfl_xor(npmax, o));
-        npmin = min(npmin, __shfl_xor(npmin, o));
-    }
-    const auto x = src + i0;
-    // samples stream through registers two quads ahead (scratch slack: never out of bounds)
-    int cur[8], nx1[8], nxt[8];
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const uint4(*rg)[64] = ring[ch & 1];
+        uint4 vnext = rg[0][lane];
+        for (int g = 0; g < kAdGroups; ++g) {
+            const int i0 = ch * kAdChunk + 8 * g;
+            if (i0 >= nmax) break;
+            const uint4 v = vnext;  // the next group's read is in flight while this one encodes
+            if (g + 1 < kAdGroups) vnext = rg[g + 1][lane];
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            // four byte starts in the group: bytes K .. K + 3; a frame precedes byte k when
+            // k % 1001 == 0
+            const bool frame_here = kmod == 0 || kmod > kAdpcmSyncPeriod - 4;
+            const bool slow = sl.active && (frame_here || i0 + 8 > n);
+            if (!__any(slow) && i0 + 8 <= nmin) {
+                uint32_t w = 0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        cur[q] = x[q];
-        nx1[q] = x[8 + q];
-    }
-    // Whole quads (4 pairs) of every active lane, in runs that no lane's next "SYNC" frame
-    // interrupts (frames are 1001 bytes apart, so runs average ~30 pairs with 32 lanes): the
-    // run loop has no per-pair checks at all; the quad that reaches a frame is done checked.
-    // No capacity checks (out_cap holds a block's worst case).
-    auto quad_fast = [&](int jq) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * jq + 16 + q];
-        int b[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
-            const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
-            b[u] = c0 | (c1 << 4);
+                for (int t = 0; t < 8; ++t) {
+                    const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
+                    w |= (uint32_t)adpcm_encode_tab(ad, x, NS) << (4 * t);
+                }
+                const uint32_t bytes4 = pend ? ((w << 4) | (uint32_t)left) : w;
+                if (pend) left = (int)(w >> 28);
+                if (sl.active) *reinterpret_cast<__attribute__((address_space(1))) u32_unaligned*>(
+                                   &out.p[ob]) = bytes4;
+                ob += 4;
+                kmod += 4;
+                if (kmod >= kAdpcmSyncPeriod) kmod -= kAdpcmSyncPeriod;
+                continue;
+            }
+            // checked path: per sample, lanes past their end keep their state
+            int nib = left;
+#pragma unroll 1
+            for (int t = 0; t < 8; ++t) {
+                if (!sl.active || i0 + t >= n) break;
+                const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
+                const bool start = (t & 1) == pend;
+                if (start) {
+                    if (kmod == 0) frame();
+                    if (++kmod == kAdpcmSyncPeriod) kmod = 0;
+                }
+                const int code = adpcm_encode_tab(ad, x, NS);
+                if (start) {
+                    nib = code;
+                } else {
+                    if (ob < cap) out[ob] = (uint8_t)(nib | (code << 4));
+                    ob++;
+                }
+            }
+            left = nib;
         }
-        if (sl.active) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) out[ob + u] = (uint8_t)b[u];
-        }
-        ob += 4;
-        until_sync -= 4;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            cur[q] = nx1[q];
-            nx1[q] = nxt[q];
-        }
-    };
-    int j = 0;
-    while (j + 4 <= npmin) {
-        int us = sl.active ? until_sync : INT_MAX;
-        for (int o = 32; o > 0; o >>= 1) us = min(us, __shfl_xor(us, o));
-        const int run = min(us >> 2, (npmin - j) >> 2);
-        for (int r = 0; r < run; ++r, j += 4) quad_fast(j);
-        if (j + 4 > npmin) break;
-        // a frame falls inside this quad for some lane
-#pragma unroll
-        for (int q = 0; q < 8; ++q) nxt[q] = x[2 * j + 16 + q];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (until_sync == 0) frame();
-            const int c0 = adpcm_encode_tab(ad, cur[2 * u], NS);
-            const int c1 = adpcm_encode_tab(ad, cur[2 * u + 1], NS);
-            if (sl.active) out[ob] = (uint8_t)(c0 | (c1 << 4));
-            ob++;
-            until_sync--;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            cur[q] = nx1[q];
-            nx1[q] = nxt[q];
-        }
-        j += 4;
-    }
-    // ragged tail: per pair, lanes past their end keep state
-    for (; j < npmax; ++j) {
-        const bool valid = j < np;
-        const int v0 = x[2 * j], v1 = x[2 * j + 1];
-        const AdpcmTab keep = ad;
-        if (valid && until_sync == 0) frame();
-        const int c0 = adpcm_encode_tab(ad, v0, NS);
-        const int c1 = adpcm_encode_tab(ad, v1, NS);
-        if (valid) {
-            if (ob < cap) out[ob] = (uint8_t)(c0 | (c1 << 4));
-            ob++;
-            until_sync--;
-        } else {
-            ad = keep;
-        }
-    }
-    bytes += np;
-    // an odd last sample starts a byte that the next block completes
-    if ((n - i0) & 1) {
-        if (until_sync == 0) frame();
-        left = adpcm_encode_tab(ad, x[2 * np], NS);
-        has_left = 1;
+        __syncthreads();  // chunk ch + 1 staged; slot ch & 1 free for chunk ch + 2
     }
     if (!sl.active) return;
+    // bytes completed this block: ob minus frame bytes; the state carries the parity
+    const int pend_out = (pend + n) & 1;
+    int64_t K_end = st0.adpcm_bytes + pend;
+    {
+        // starts this block = samples at start positions: (n + (1 - pend)) / 2 for pend = 0
+        const int starts = pend ? n / 2 : (n + 1) / 2;
+        K_end += starts;
+    }
     sp->adpcm.index = ad.index();
     sp->adpcm.pred = ad.pred;
-    sp->has_left = has_left;
+    sp->has_left = pend_out;
     sp->left_code = left;
-    sp->adpcm_bytes = bytes;
+    sp->adpcm_bytes = K_end - pend_out;
     counts[c].out_bytes = ob;
 }
 
@@ -1027,7 +1051,7 @@ hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
-    hipLaunchKernelGGL(chain_adpcm, dim3((nsel + 63) / 64), dim3(64), 0, st, posts, counts, sel,
+    hipLaunchKernelGGL(chain_adpcm, dim3((nsel + 63) / 64), dim3(128), 0, st, posts, counts, sel,
                        nsel);
     return hipGetLastError();
 }

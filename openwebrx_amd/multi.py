@@ -9,6 +9,8 @@ wideband IQ broadcast from rank 0 as the only exchange step.
   "nccl" backend, gloo in the CPU tests).  Ranks > 0 assemble [history | block] windows,
   alternating two, because the engine still reads block k (asynchronously) while k+1 arrives
   (owrx_process_device contract, include/owrx_amd.h).
+* Placement -- the same balance for the in-process drop-in (pycsdr shim, one engine per GPU
+  in one OpenWebRX process), where chains come and go one at a time.
 No reduction: every rank returns its own chains' outputs to the host.
 """
 from collections import OrderedDict
@@ -27,6 +29,28 @@ def shard_chains(items, world, rank, key=lambda it: it):
                 mine.append(it)
             pos += 1
     return mine
+
+
+class Placement:
+    """Online version of shard_chains for n engines: a new segment goes to the engine with
+    the fewest segments of its group (same FirDecimate design, or the waterfalls), ties to the
+    fewest segments overall, then the lowest index; release() when it leaves."""
+
+    def __init__(self, n):
+        self.n = n
+        self.total = [0] * n
+        self.groups = {}
+
+    def place(self, key):
+        g = self.groups.setdefault(key, [0] * self.n)
+        slot = min(range(self.n), key=lambda k: (g[k], self.total[k], k))
+        g[slot] += 1
+        self.total[slot] += 1
+        return slot
+
+    def release(self, slot, key):
+        self.groups[key][slot] -= 1
+        self.total[slot] -= 1
 
 
 class IqBroadcast:

@@ -5,23 +5,59 @@ wideband IQ buffer fed by TcpSource / the SDR source, owrx/source/__init__.py:30
 Every reader of a source buffer that belongs to a Shift (Selector, csdr/chain/selector.py:95)
 or an Fft (FftChain, csdr/chain/fft.py:34) starts a *segment*: the modules linked through
 single-reader Buffers downstream of it.  plan_segment() recognises the two hot-path shapes
-and returns the engine parameters; one EngineDriver per source buffer owns one engine, runs
-every recognised segment on it (one DDC launch for all chains that share a FirDecimate
-design) and writes each segment's output into the writer of its last module.
+and returns the engine parameters; one EngineDriver per source buffer owns one engine per GPU
+(OWRX_AMD_DEVICES, default every visible device), places each recognised segment on one of
+them (multi.Placement: balanced within FirDecimate designs, so each engine keeps one DDC
+launch per design), feeds every engine the source's blocks and writes each segment's output
+into the writer of its last module.
+
+Failure (owrx/source/__init__.py:224-227 fail() -> clients' onFail()): an engine
+error stops the driver, marks it FAILED, ends every output buffer it was writing (their
+readers' read() returns None once drained, so the pumps of owrx/dsp.py:858-861 finish instead
+of blocking forever) and calls the callbacks registered with on_failure(source).
 
 The graph is re-planned at the next block boundary after any (re)wiring; setters that do not
 change the shape (Shift.setRate, Bandpass.setBandpass, Squelch.setSquelchLevel,
 Fft.setEveryNSamples) are applied to the live engine objects.
 """
+import logging
+import os
 import threading
 import weakref
 
 import numpy as np
 
+logger = logging.getLogger(__name__)
+
 _drivers = weakref.WeakValueDictionary()  # id(source buffer) -> EngineDriver
 _lock = threading.RLock()
 
 BLOCK = 1 << 18  # IQ samples per engine block (26 ms at 10 Msps)
+
+_failure_callbacks = {}  # id(source buffer) -> [callable(exception)]
+
+
+def devices():
+    """GPUs the drop-in spreads its engines over: OWRX_AMD_DEVICES ("0,1,2"; a repeated index
+    runs several engines on one GPU), else every visible device."""
+    env = os.environ.get("OWRX_AMD_DEVICES", "").strip()
+    if env:
+        return [int(v) for v in env.split(",") if v.strip()]
+    from ..engine import device_count
+    return list(range(max(1, device_count())))
+
+
+def on_failure(source, callback):
+    """Register callback(exception), called once if the engine driving `source` fails (an
+    SdrSource would call its fail() here, owrx/source/__init__.py:224-227)."""
+    with _lock:
+        _failure_callbacks.setdefault(id(source), []).append(callback)
+
+
+def state(source):
+    """"RUNNING", "FAILED" or "STOPPED" for the driver of a source buffer (None: no driver)."""
+    drv = _drivers.get(id(source))
+    return None if drv is None else drv.state
 
 
 def changed(module, structural=True):
@@ -221,6 +257,26 @@ def plan_segment(head):
         demod, audio_rate = _lib.DEMOD_AM, 12000
     elif take(M.RealPart) is not None:
         demod, audio_rate = _lib.DEMOD_SSB, 12000
+    elif selector_last.writer is not None and selector_last is not fir:
+        # Selector output read by something the engine does not fuse (an IQ-input decoder:
+        # ServiceDemodulatorChain with Selector(withSquelch=False), owrx/service/chain.py:7-23):
+        # the engine emits the cf32 Selector output itself
+        p = dict(shift_rate=shift.rate, decimation=fir.decimation, transition=fir.transition,
+                 cutoff=fir.cutoff, frac_rate=frac.rate if frac is not None else 1.0,
+                 bandpass=0, bp_low=0.0, bp_high=0.0, bp_transition=0.0,
+                 sq_length=750, sq_decimation=5, sq_hang=0, sq_flush=0, sq_report=0,
+                 sq_level=0.0, demod=_lib.DEMOD_SSB, agc_profile=0, agc_initial_gain=-1.0,
+                 agc_max_gain=-1.0, audio_rate=12000, output=_lib.OUT_SEL, power_writer=None,
+                 tap_selector=None, tap_audio=None, secondary_fft=None, secondary_modules=[],
+                 secondary_writer=None)
+        if bp is not None and bp.low_cut is not None and bp.high_cut is not None:
+            p.update(bandpass=1, bp_low=bp.low_cut, bp_high=bp.high_cut,
+                     bp_transition=bp.transition)
+        if sq is not None:
+            p.update(sq_length=sq.length, sq_decimation=sq.decimation, sq_hang=sq.hang_length,
+                     sq_flush=sq.flush_length, sq_report=sq.report_interval, sq_level=sq.level,
+                     power_writer=sq.power_writer)
+        return ("chain", p, mods[:i])
     else:
         return None
     agc = take(M.Agc) if wfm is None else None
@@ -281,17 +337,27 @@ def chain_params_struct(p):
 
 
 class EngineDriver:
-    """One engine per source buffer: reads it, runs every fused segment, writes outputs."""
+    """One driver per source buffer: reads it, runs every fused segment on one of its engines
+    (one per entry of devices()), writes outputs."""
 
     def __init__(self, source):
+        from ..multi import Placement
         self.source = source
-        self.engine = None
-        self.segments = {}  # head id -> (kind, params, modules, engine object)
+        self.devices = devices()
+        self.engines = {}   # slot (index into self.devices) -> Engine
+        self.placement = Placement(len(self.devices))
+        self.segments = {}  # head id -> (kind, params, modules, engine object, slot)
+        self.state = "RUNNING"
+        self.error = None
         self._dirty = True
         self._closing = False
         self.reader = source.getReader()  # before any further write: nothing is missed
         self._thread = threading.Thread(target=self._run, name="owrx-engine", daemon=True)
         self._thread.start()
+
+    @property
+    def engine(self):  # the first engine (single-GPU callers and tests)
+        return self.engines.get(min(self.engines)) if self.engines else None
 
     def mark_dirty(self, structural=True):
         self._dirty = True
@@ -303,38 +369,53 @@ class EngineDriver:
         return [r.module for r in rs if isinstance(r.module, (M.Shift, M.Fft))
                 and not r.module._stopped]
 
-    def _replan(self):
+    @staticmethod
+    def _group_key(kind, p):
+        if kind == "waterfall":
+            return ("waterfall",)
+        return ("chain", p["decimation"], p["transition"], p["cutoff"])
+
+    def _engine(self, slot):
         from ..engine import Engine
+        eng = self.engines.get(slot)
+        if eng is None:
+            eng = Engine(1.0, max_block=BLOCK, device=self.devices[slot])
+            self.engines[slot] = eng
+        return eng
+
+    def _replan(self):
         plans = {}
         for h in self._heads():
             seg = plan_segment(h)
             if seg is not None:
                 plans[id(h)] = seg
-        if plans and self.engine is None:
-            self.engine = Engine(1.0, max_block=BLOCK)
+        self._planned = plans  # outputs to end should creating their engine objects fail
         # drop segments that vanished or changed shape / design parameters
         for hid in list(self.segments):
-            kind, p, mods, obj = self.segments[hid]
+            kind, p, mods, obj, slot = self.segments[hid]
             new = plans.get(hid)
             if new is None or new[0] != kind or new[2] != mods or not _compatible(kind, p, new[1]):
                 self._absorb(mods, False)
                 self._absorb(p.get("secondary_modules", []), False)
                 obj.close()
+                self.placement.release(slot, self._group_key(kind, p))
                 del self.segments[hid]
         for hid, (kind, p, mods) in plans.items():
             if hid in self.segments:
                 self._update(hid, p)
                 continue
+            slot = self.placement.place(self._group_key(kind, p))
+            eng = self._engine(slot)
             if kind == "waterfall":
-                obj = self.engine.waterfall(p["fft_size"], p["hop"], max(1, p["avg"]),
-                                            p["add_db"], p["adpcm"])
+                obj = eng.waterfall(p["fft_size"], p["hop"], max(1, p["avg"]), p["add_db"],
+                                    p["adpcm"])
             else:
-                obj = self.engine.chain(chain_params_struct(p))
+                obj = eng.chain(chain_params_struct(p))
                 if p.get("secondary_fft") is not None:
                     _apply_secondary(obj, p["secondary_fft"])
                 if p.get("tap_selector") is not None or p.get("tap_audio") is not None:
                     obj.set_taps(p.get("tap_selector") is not None, p.get("tap_audio") is not None)
-            self.segments[hid] = (kind, p, mods, obj)
+            self.segments[hid] = (kind, p, mods, obj, slot)
             self._absorb(mods, True)
             self._absorb(p.get("secondary_modules", []), True)
 
@@ -345,7 +426,7 @@ class EngineDriver:
                 m.reader._detach()   # the engine reads the source through its own reader
 
     def _update(self, hid, p):
-        kind, old, mods, obj = self.segments[hid]
+        kind, old, mods, obj, slot = self.segments[hid]
         if kind == "waterfall":
             if (old["hop"], old["avg"], old["adpcm"]) != (p["hop"], p["avg"], p["adpcm"]):
                 obj.set(p["hop"], max(1, p["avg"]), p["adpcm"])
@@ -367,10 +448,10 @@ class EngineDriver:
             if olds != news:
                 self._absorb([m for m in olds if m not in news], False)
                 self._absorb(news, True)
-        self.segments[hid] = (kind, p, mods, obj)
+        self.segments[hid] = (kind, p, mods, obj, slot)
 
     def _drain(self):
-        for kind, p, mods, obj in list(self.segments.values()):
+        for kind, p, mods, obj, slot in list(self.segments.values()):
             out = mods[-1].writer
             if kind == "waterfall":
                 data = obj.read()
@@ -398,6 +479,12 @@ class EngineDriver:
                         if t.size:
                             buf.write(t.tobytes())
 
+    def _push(self, blk):
+        # every engine gets the block from host memory over its own PCIe link (8 B per
+        # sample: 0.5 GB/s per GPU at 61.44 Msps), then all run concurrently
+        for eng in self.engines.values():
+            eng.push(blk)
+
     def close(self):
         """Stop reading the source; the thread pushes what it holds, syncs and drains."""
         self._closing = True
@@ -405,25 +492,60 @@ class EngineDriver:
             self.reader.stop()
         self._thread.join()
 
+    def _outputs(self):
+        segs = [(p, mods) for kind, p, mods, obj, slot in self.segments.values()]
+        segs += [(p, mods) for kind, p, mods in getattr(self, "_planned", {}).values()]
+        for p, mods in segs:
+            for buf in (mods[-1].writer, p.get("power_writer"), p.get("secondary_writer"),
+                        p.get("tap_selector"), p.get("tap_audio")):
+                if buf is not None:
+                    yield buf
+
+    def _fail(self, exc):
+        logger.error("GPU engine failed: %s", exc)
+        self.state = "FAILED"
+        self.error = exc
+        self.reader.stop()
+        for buf in list(self._outputs()):
+            end = getattr(buf, "end", None)
+            if end is not None:
+                end()
+        for cb in _failure_callbacks.get(id(self.source), []):
+            try:
+                cb(exc)
+            except Exception:
+                logger.exception("failure callback")
+
     def _run(self):
+        try:
+            self._loop()
+        except Exception as exc:  # engine / HIP error: surface it, do not leave readers hanging
+            with _lock:
+                self._fail(exc)
+            return
+        if self.state == "RUNNING":
+            self.state = "STOPPED"
+
+    def _loop(self):
         pending = []
         npend = 0
         while True:
             data = self.reader.read()
             if data is None:
-                if pending and self.engine is not None:
+                if pending and self.engines:
                     with _lock:
-                        self.engine.push(np.concatenate(pending))
-                if self.engine is not None:
+                        self._push(np.concatenate(pending))
+                if self.engines:
                     with _lock:
-                        self.engine.sync()
+                        for eng in self.engines.values():
+                            eng.sync()
                         self._drain()
                 break
             with _lock:
                 if self._dirty:
                     self._dirty = False
                     self._replan()
-            if self.engine is None:
+            if not self.engines:
                 continue
             x = np.frombuffer(data, dtype=np.complex64)
             pending.append(x)
@@ -433,7 +555,7 @@ class EngineDriver:
             blk = np.concatenate(pending)
             pending, npend = [], 0
             with _lock:
-                self.engine.push(blk)
+                self._push(blk)
                 self._drain()
 
 

@@ -59,6 +59,7 @@ class Buffer(Writer):
         self._start = 0          # stream offset of the first retained byte
         self._end = 0            # stream offset past the last written byte
         self._readers = []
+        self._ended = False
         self.writer_module = None  # native module that writes here (graph planning)
 
     def getFormat(self):
@@ -70,6 +71,13 @@ class Buffer(Writer):
             r._pos = self._end
             self._readers.append(r)
         return r
+
+    def end(self):
+        """No more data will come (the engine writing here failed): readers drain what is
+        buffered, then read() returns None."""
+        with self._cond:
+            self._ended = True
+            self._cond.notify_all()
 
     def write(self, data):
         b = bytes(data)
@@ -136,6 +144,8 @@ class Reader:
                 data = b._take(self)
                 if data:
                     return memoryview(data)
+                if b._ended:
+                    return None
                 b._cond.wait(0.5)
 
     def available(self):

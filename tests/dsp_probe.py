@@ -18,7 +18,8 @@ def main(ROOT, REF):
     shim.install()
     sys.path.append(REF)
     from csdr.chain.analog import NFm, Am, Ssb, WFm
-    from csdr.chain.demodulator import SecondaryDemodulator, SecondarySelectorChain
+    from csdr.chain.demodulator import SecondaryDemodulator, SecondarySelectorChain, ServiceDemodulator
+    from owrx.service.chain import ServiceDemodulatorChain
     from csdr.module import ThreadModule
     from owrx.dsp import ClientDemodulatorChain, ClientDemodulatorSecondaryDspEventClient
     from pycsdr.modules import Buffer
@@ -63,6 +64,26 @@ def main(ROOT, REF):
 
         def __init__(self):
             super().__init__([Sink(Format.FLOAT)])
+
+    class IqService(ServiceDemodulator):
+        """A service decoder that takes the Selector's IQ (getInputFormat COMPLEX_FLOAT):
+        ServiceDemodulatorChain wires Selector(withSquelch=False) straight into it."""
+
+        def __init__(self):
+            super().__init__([Sink(Format.COMPLEX_FLOAT)])
+
+        def getFixedAudioRate(self):
+            return 12000
+
+    class AudioService(ServiceDemodulator):
+        """A service decoder on audio (FT8-like): ServiceDemodulatorChain puts the primary
+        demodulator between the Selector and it."""
+
+        def __init__(self):
+            super().__init__([Sink(Format.FLOAT)])
+
+        def getFixedAudioRate(self):
+            return 12000
 
     class Events(ClientDemodulatorSecondaryDspEventClient):
         def onSecondaryDspRateChange(self, rate):
@@ -118,7 +139,8 @@ def main(ROOT, REF):
     steps = []
 
     def record(name, chain, wide):
-        seg = _graph.plan_segment(chain.selector.workers[0])
+        seg = _graph.plan_segment(chain.selector.workers[0] if hasattr(chain, "selector")
+                                  else chain.workers[0].workers[0])
         entry = {"step": name, "fused": seg is not None}
         if seg is not None:
             kind, p, used = seg
@@ -168,6 +190,16 @@ def main(ROOT, REF):
     chain.setNrEnabled(False)
     record("nfm_plain", chain, wide)
     _graph.finish(wide)
+
+    # background services (owrx/service/__init__.py): ServiceDemodulatorChain on a service
+    # Resampler's buffer -- any COMPLEX_FLOAT source; offset / bandpass as a USB-family decoder
+    for name, sec in (("service_iq", IqService()), ("service_audio", AudioService())):
+        src = Buffer(Format.COMPLEX_FLOAT)
+        svc = ServiceDemodulatorChain(Ssb(), sec, 250000, 31000)
+        svc.setBandPass(0, 3000)
+        svc.setReader(src.getReader())
+        record(name, svc, src)
+        _graph.finish(src)
     print(json.dumps(steps))
 
 

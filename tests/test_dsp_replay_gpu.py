@@ -113,3 +113,52 @@ def test_secondary_selector_keeps_primary_fused_and_gets_the_selector_output():
     got = withsec["sec"]
     assert got.size == want.size, (got.size, want.size)
     assert rel_rms(got, want) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("step", ["service_iq", "service_audio"])
+def test_service_demodulator_chain_replay(step):
+    """ServiceDemodulatorChain (owrx/service/chain.py:7-23) as the reference builds it
+    (tests/golden/dsp_graph.json): Selector(withSquelch=False) at 250 kHz, offset 31 kHz,
+    bandpass 0-3 kHz, straight into an IQ-input decoder (OWRX_OUT_SEL: the engine writes the
+    Selector's cf32 output into the decoder's buffer) or through the primary Ssb demodulator
+    into an audio decoder (OWRX_OUT_F32).  Fused, and equal to the oracle's stages."""
+    import oracle
+    from openwebrx_amd import _lib, synth
+    from openwebrx_amd.pycsdr import _graph
+    s = dsp_replay.steps()[step]
+    assert s["fused"]
+    fs = 250000
+    iq, _ = synth.make_iq(fs, 1 << 20, ["usb", "nfm", "am"])
+    t = np.arange(iq.size) / fs
+    iq += (0.05 * np.exp(2j * np.pi * (31000.0 + 1000.0) * t)).astype(np.complex64)  # USB tone
+    iq = iq.astype(np.complex64)
+    wide, mods, outs, power = dsp_replay.build(s)
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    last = max(i for i, c in enumerate(cls) if c != "PythonReader")
+    col = _collect(outs[last])
+    for i in range(0, iq.size, 100003):
+        wide.write(iq[i:i + 100003].tobytes())
+    drv = _graph._drivers.get(id(wide))
+    while drv.reader.available() > 0:
+        time.sleep(0.01)
+    fused = drv.engine is not None and len(drv.segments) == 1
+    _graph.finish(wide)
+    t0 = time.time()
+    while col[0].available() > 0 and time.time() - t0 < 20:
+        time.sleep(0.02)
+    col[0].stop()
+    col[1].join(5)
+    assert fused
+    p = _graph.chain_params_struct(s["params"])
+    ref = oracle.stages(iq, p)
+    if step == "service_iq":
+        assert p.output == _lib.OUT_SEL
+        got = np.frombuffer(b"".join(col[2]), np.complex64)
+        want = ref["squelch"]  # level 0: the gate is always open (Selector without squelch)
+    else:
+        assert p.output == _lib.OUT_F32
+        got = np.frombuffer(b"".join(col[2]), np.float32)
+        want = ref["agc"]
+    assert got.size == want.size > 10000, (got.size, want.size)
+    assert rel_rms(got, want) < 1e-5

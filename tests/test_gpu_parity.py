@@ -339,6 +339,27 @@ def test_adpcm_chain_output_decodes(amd):
     eng.close()
 
 
+def test_adpcm_chains_many_lanes_ragged_blocks(amd):
+    """chain_adpcm across two workgroups (70 chains, mixed modes and so different audio
+    lengths per block), blocks of ragged sizes (odd sample counts: bytes spanning blocks) and
+    ~12 SYNC frames per chain: every chain's AdpcmEncoder(sync=True) bytes equal the oracle's
+    encoding of its own AGC output (debug tap 5)."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    modes = [("nfm", "am", "usb", "cw", "lsb")[c % 5] for c in range(70)]
+    n = 5 << 20
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_ADPCM)
+             for o, m in zip(offs, modes)]
+    eng, chains = _run_chains(amd, iq, fs, plist, 1 << 18)
+    for c, ch in enumerate(chains):
+        data = ch.read_audio()
+        agc = ch.read_debug(5)
+        ref = oracle.adpcm_encode(oracle.convert_s16(agc), 1)
+        assert len(data) > 10000 and data == ref[:len(data)] and len(ref) - len(data) <= 9, c
+    eng.close()
+
+
 @pytest.mark.parametrize("N,fs", [(4096, 2400000), (16384, 10000000), (65536, 61440000)])
 def test_waterfall_adpcm_rows_bit_exact(amd, N, fs):
     """The row-parallel speculative IMA-ADPCM encoder is bit-identical to the sequential

@@ -421,3 +421,106 @@ def test_planner_recognises_service_resampler():
     assert kind == "chain" and used == [shift, fir]
     assert q["output"] == _lib.OUT_IQ and q["decimation"] == 50 and q["cutoff"] == 0.5
     _graph.finish(wide)
+
+
+# ---- multi-GPU placement and failure propagation ---------------------------------------------
+
+def test_placement_balances_groups():
+    """multi.Placement (the drop-in's chain -> engine assignment): balanced within each
+    FirDecimate design, then by total load; released slots are reused."""
+    from openwebrx_amd.multi import Placement
+    pl = Placement(3)
+    a = [pl.place(("chain", 833)) for _ in range(7)]
+    assert a == [0, 1, 2, 0, 1, 2, 0]
+    assert [pl.place(("chain", 200)) for _ in range(2)] == [1, 2]
+    assert pl.place(("waterfall",)) == 0  # every engine holds 3: lowest index
+    pl.release(1, ("chain", 833))
+    assert pl.place(("chain", 833)) == 1
+
+
+def _graph_with_outputs(fs, offs, modes, wf=None):
+    wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 22)
+    cols = []
+    for off, mode in zip(offs, modes):
+        mods = selector(fs, off, mode) + demodulator(mode) + client_audio()
+        ch = Chain(mods)
+        out, pw = M.Buffer(Format.CHAR, size=1 << 22), M.Buffer(Format.FLOAT, size=1 << 20)
+        [m for m in mods if isinstance(m, M.Squelch)][0].setPowerWriter(pw)
+        cols.append((_collect(out), _collect(pw)))
+        ch.setWriter(out)
+        ch.setReader(wide.getReader())
+    wcol = None
+    if wf is not None:
+        wmods = fft_chain(*wf)
+        wch = Chain(wmods)
+        wout = M.Buffer(Format.CHAR, size=1 << 22)
+        wcol = _collect(wout)
+        wch.setWriter(wout)
+        wch.setReader(wide.getReader())
+    return wide, cols, wcol
+
+
+def test_engine_failure_ends_outputs(monkeypatch):
+    """An engine that cannot run (here: a GPU index that does not exist) puts the driver in
+    FAILED, calls the on_failure callbacks (an SdrSource's fail(), owrx/source/__init__.py:
+    224-227) and ends the output buffers, so the DSP pumps' read() returns None instead of
+    blocking forever (owrx/dsp.py:858-861)."""
+    monkeypatch.setenv("OWRX_AMD_DEVICES", "97")
+    fs = 2400000
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    mods = selector(fs, 1000, "nfm") + demodulator("nfm") + client_audio()
+    ch = Chain(mods)
+    out = M.Buffer(Format.CHAR)
+    ch.setWriter(out)
+    ch.setReader(wide.getReader())
+    r = out.getReader()
+    failed = []
+    _graph.on_failure(wide, failed.append)
+    wide.write(np.zeros(1000, np.complex64).tobytes())
+    got = []
+    t = threading.Thread(target=lambda: got.append(r.read()), daemon=True)
+    t.start()
+    t.join(20)
+    assert got == [None]
+    assert len(failed) == 1 and _graph.state(wide) == "FAILED"
+    _graph.finish(wide)
+
+
+@pytest.mark.gpu
+def test_pycsdr_sharded_engines_equal_single(monkeypatch):
+    """The drop-in over several engines in one process (OWRX_AMD_DEVICES="0,0,0": three
+    engines on the test box's one GPU -- the code path of one engine per GPU) writes
+    byte-identical audio, s-meter and waterfall bytes to the single-engine run."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    modes = ["nfm", "am", "usb", "nfm", "cw", "am", "nfm"]
+    iq, offs = synth.make_iq(fs, 1 << 20, modes)
+    avg, hop = params.fft_parameters(fs, 4096, 9, 0.3)
+
+    def run(devs):
+        monkeypatch.setenv("OWRX_AMD_DEVICES", devs)
+        wide, cols, wcol = _graph_with_outputs(fs, offs, modes, wf=(4096, hop, avg))
+        i = 0
+        for s in [100003, 77777, 300001] * 10:
+            if i >= iq.size:
+                break
+            wide.write(iq[i:i + s].tobytes())
+            i += s
+        drv = _graph._drivers.get(id(wide))
+        while drv.reader.available() > 0:
+            time.sleep(0.01)
+        nengines = len(drv.engines)
+        _graph.finish(wide)
+        res = []
+        for col in [c for pair in cols for c in pair] + [wcol]:
+            col[0].stop()
+            col[1].join(5)
+            res.append(b"".join(col[2]))
+        return nengines, res
+
+    n1, single = run("0")
+    n3, sharded = run("0,0,0")
+    assert (n1, n3) == (1, 3)
+    assert all(len(b) > 0 for b in single)
+    for k, (a, b) in enumerate(zip(single, sharded)):
+        assert a == b, k

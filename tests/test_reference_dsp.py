@@ -76,7 +76,25 @@ def test_taps_and_secondary_fft_follow_the_secondary_readers():
     assert s["nfm_nr"]["params"]["nr_enabled"] == 1
 
 
-@pytest.mark.parametrize("step", sorted(MODES))
+@pytest.mark.parametrize("step,output", [("service_iq", 4), ("service_audio", 2)])
+def test_service_demodulator_chains_fuse(step, output):
+    """ServiceDemodulatorChain (owrx/service/chain.py:7-23): Selector(withSquelch=False) at the
+    service's 250 kHz IF into an IQ decoder (OWRX_OUT_SEL: the engine emits the Selector output)
+    or through Ssb into an audio decoder (OWRX_OUT_F32); the Selector design is the reference's
+    (decimation / FractionalDecimator / bandpass of csdr/chain/selector.py for 250 kHz -> 12 kHz)
+    and no squelch gate (level 0)."""
+    from openwebrx_amd import params
+    s = dsp_replay.steps()[step]
+    assert s["fused"] and s["kind"] == "chain"
+    p = s["params"]
+    d, frac, tbw, cutoff = params.decimation(250000, 12000)
+    assert (p["output"], p["decimation"], p["demod"]) == (output, d, 2)
+    assert p["frac_rate"] == pytest.approx(frac) and p["transition"] == pytest.approx(tbw)
+    assert (p["bandpass"], p["bp_low"], p["bp_high"]) == (1, 0.0, pytest.approx(3000 / 12000))
+    assert p["sq_level"] == 0.0 and not s["tap_selector"] and not s["tap_audio"]
+
+
+@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio"])
 def test_replayed_graph_plans_like_the_reference(step):
     """The shim-built replay of each recorded graph is planned exactly as the reference's."""
     from openwebrx_amd.pycsdr import _graph
