@@ -142,14 +142,15 @@ def test_service_demodulator_chain_replay(step):
     drv = _graph._drivers.get(id(wide))
     while drv.reader.available() > 0:
         time.sleep(0.01)
+    _graph.finish(wide)  # the driver replans on its first read: look after it has finished
     fused = drv.engine is not None and len(drv.segments) == 1
-    _graph.finish(wide)
+    diag = (drv.state, drv.error, len(drv.segments), len(getattr(drv, "_planned", {})))
     t0 = time.time()
     while col[0].available() > 0 and time.time() - t0 < 20:
         time.sleep(0.02)
     col[0].stop()
     col[1].join(5)
-    assert fused
+    assert fused, diag
     p = _graph.chain_params_struct(s["params"])
     ref = oracle.stages(iq, p)
     if step == "service_iq":

@@ -509,8 +509,8 @@ def test_pycsdr_sharded_engines_equal_single(monkeypatch):
         drv = _graph._drivers.get(id(wide))
         while drv.reader.available() > 0:
             time.sleep(0.01)
+        _graph.finish(wide)  # the driver replans on its first read: count after it finished
         nengines = len(drv.engines)
-        _graph.finish(wide)
         res = []
         for col in [c for pair in cols for c in pair] + [wcol]:
             col[0].stop()
