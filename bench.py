@@ -449,7 +449,12 @@ def main():
                 "parallelism": "1 GPU" if world == 1 else
                 "IQ broadcast over RCCL from rank 0, %d chains per rank" % C,
             },
+            "value_definition": ("wideband IQ Msamples/s processed summed over the GPUs: each GPU "
+                                 "runs the whole stream (waterfall on GPU 0) for its own %d chains, "
+                                 "so at N GPUs this is N x the single-stream rate below; ONE stream "
+                                 "is ingested (iq_msps_stream)" % C),
             "iq_msps_stream": round(samples / dt / 1e6, 2),
+            "chain_msamples_per_s": round(C * world * samples / dt / 1e6, 1),
             "realtime_factor": round(samples / dt / fs, 1),
             "chains_total": C * world,
             "roofline": {
