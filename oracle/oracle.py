@@ -390,3 +390,26 @@ def stages(iq, p):
     else:
         out["s16"] = convert_s16(ag)
     return out
+
+
+def audio_resample(x, in_rate, out_rate):
+    """AudioResampler(inputRate, clientRate) (csdr/chain/clientaudio.py:15-16), restated in
+    float64: rational L/M with L = out/g, M = in/g; y[m] = L sum_j h[j] x_up[m M - j] with x_up
+    the input upsampled by L (zeros between samples); h = lowpass at 0.5 / max(L, M) of the
+    upsampled rate, transition a fifth of that (csdr's own design is not in the reference:
+    parity unpinned, the build's documented choice)."""
+    from math import gcd
+    x = np.asarray(x, np.float64)
+    g = gcd(int(in_rate), int(out_rate))
+    L, M = int(out_rate) // g, int(in_rate) // g
+    c = 0.5 / max(L, M)
+    h = lowpass(filter_len(np.float32(0.2 * c)), c).astype(np.float64)
+    n_out = ((x.size - 1) * L) // M + 1 if x.size else 0
+    y = np.zeros(n_out)
+    for m in range(n_out):
+        up = m * M
+        j = np.arange(up % L, h.size, L)
+        i = (up - j) // L
+        ok = i >= 0
+        y[m] = L * np.dot(h[j[ok]], x[i[ok]])
+    return y
