@@ -524,3 +524,68 @@ def test_pycsdr_sharded_engines_equal_single(monkeypatch):
     assert all(len(b) > 0 for b in single)
     for k, (a, b) in enumerate(zip(single, sharded)):
         assert a == b, k
+
+
+class _Registry:
+    """The part of owrx.metrics.Metrics (owrx/metrics.py:29-70) register() uses."""
+
+    def __init__(self):
+        self.metrics = {}
+
+    def addMetric(self, name, metric):
+        self.metrics[name] = metric
+
+    def getFlatMetrics(self):
+        return {k: m.getValue() for k, m in self.metrics.items()}
+
+
+def test_engine_metrics_report_failed_driver(monkeypatch):
+    """Engine counters as OpenWebRX metrics: a driver whose engine cannot start counts under
+    gpu.failed, with no engines."""
+    from openwebrx_amd.pycsdr import metrics
+    monkeypatch.setenv("OWRX_AMD_DEVICES", "97")
+    reg = _Registry()
+    names = metrics.register(reg)
+    assert "gpu.blocks" in names and "gpu.failed" in names
+    fs = 2400000
+    wide = M.Buffer(Format.COMPLEX_FLOAT)
+    mods = selector(fs, 1000, "nfm") + demodulator("nfm") + client_audio()
+    ch = Chain(mods)
+    ch.setWriter(M.Buffer(Format.CHAR))
+    ch.setReader(wide.getReader())
+    failed = []
+    _graph.on_failure(wide, failed.append)
+    wide.write(np.zeros(1000, np.complex64).tobytes())
+    t0 = time.time()
+    while not failed and time.time() - t0 < 20:
+        time.sleep(0.02)
+    flat = reg.getFlatMetrics()
+    assert flat["gpu.failed"] >= 1 and flat["gpu.engines"] == 0
+    _graph.finish(wide)
+
+
+@pytest.mark.gpu
+def test_engine_metrics_count_blocks_and_audio():
+    """After a fused graph ran, gpu.blocks / gpu.samples_in / gpu.audio_bytes count its work."""
+    from openwebrx_amd import synth
+    from openwebrx_amd.pycsdr import metrics
+    reg = _Registry()
+    metrics.register(reg)
+    fs = 2400000
+    iq, offs = synth.make_iq(fs, 1 << 20, ["nfm"])
+    wide, cols, _ = _graph_with_outputs(fs, offs, ["nfm"])
+    for i in range(0, iq.size, 200003):
+        wide.write(iq[i:i + 200003].tobytes())
+    drv = _graph._drivers.get(id(wide))
+    while drv.reader.available() > 0:
+        time.sleep(0.01)
+    time.sleep(0.2)
+    flat = reg.getFlatMetrics()
+    _graph.finish(wide)
+    for pair in cols:
+        for col in pair:
+            col[0].stop()
+            col[1].join(5)
+    assert flat["gpu.engines"] >= 1 and flat["gpu.segments"] >= 1
+    assert flat["gpu.blocks"] >= 3 and flat["gpu.samples_in"] >= 3 * _graph.BLOCK
+    assert flat["gpu.audio_bytes"] > 0 and flat["gpu.failed"] == 0
