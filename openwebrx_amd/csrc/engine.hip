@@ -1807,6 +1807,11 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         ng->fc_P = (T + D - 1) / D;
         const int64_t nk_max = e->max_block / D + 4;
         ng->fc_logm = ng->fc_P <= 64 ? fc_choose_logm(D, ng->fc_P, nk_max) : 0;
+        if (const char* v = getenv("OWRX_FC_LOGM")) {  // A/B: force the frame length
+            const int lm = atoi(v);
+            if (ng->fc_logm && lm >= 6 && lm <= 8 && (1 << lm) - ng->fc_P + 1 >= (1 << lm) / 2)
+                ng->fc_logm = lm;
+        }
         if (ng->fc_logm) {
             const int M = 1 << ng->fc_logm;
             ng->fc_V = M - ng->fc_P + 1;

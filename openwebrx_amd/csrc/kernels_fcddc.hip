@@ -24,6 +24,9 @@
 // f32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 products and sums; the complex product is the
 // real GEMM [Ur Ui] x [[Wr Wi] [-Wi Wr]]).  Its operands stream once per block: W (C M Dp 8 B,
 // unique per chain) from HBM, U from L2, so fc_mac sits between the HBM and the f32 MFMA roof.
+#include <stdlib.h>
+#include <string.h>
+
 #include "owrx_types.h"
 #include "fft_lds.h"
 
@@ -131,18 +134,30 @@ constexpr int kFcKSplit = 4;
 template <int FTT, int CTT, bool NT>
 __global__ void __launch_bounds__(64 * kFcKSplit)
 fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs, int64_t w_ks,
-       int nchains, int Fs, int F, int Dp, int M, int ncg, float2* __restrict__ Y) {
+       int nchains, int Fs, int F, int Dp, int M, int ncg, int chain_fastest,
+       float2* __restrict__ Y) {
     // XCD-aware decode: consecutive workgroup ids land on different XCDs (round robin), so the
-    // ids one XCD receives are mapped to one contiguous kappa range; the 8-B Y stores of
-    // neighbouring kappas (one Y line) then meet in that XCD's L2
+    // ids one XCD receives are mapped to one contiguous kappa range (the 8-B Y stores of
+    // neighbouring kappas -- one Y line -- meet in that XCD's L2).  Within an XCD the chain
+    // groups of one (kappa, frame group) come consecutively, so the workgroups that read the
+    // same U tile run together and fetch it from HBM once (the kappa-fastest order re-read it
+    // per chain group: 770 MB of HBM reads per C3 launch against 510 MB of W + U)
     const int w = blockIdx.x;
     const int xcd = w & 7;
     const int q = w >> 3;
     const int mper = M >> 3;
-    const int kap = xcd * mper + q % mper;
-    const int rest = q / mper;
-    const int cg = rest % ncg;
-    const int fg = rest / ncg;
+    int kap, cg, fg;
+    if (chain_fastest) {
+        cg = q % ncg;
+        const int r1 = q / ncg;
+        kap = xcd * mper + r1 % mper;
+        fg = r1 / mper;
+    } else {
+        kap = xcd * mper + q % mper;
+        const int rest = q / mper;
+        cg = rest % ncg;
+        fg = rest / ncg;
+    }
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int g = lane >> 4;
@@ -351,11 +366,15 @@ hipError_t launch_fc_ddc(int logm, const float2* blk, int64_t blk_start, int64_t
     const int nfg = (F + 16 * ftt - 1) / (16 * ftt);
     const dim3 gm(M * ncg * nfg);
     if (Dp % kFcDpAlign) return hipErrorInvalidValue;
+    static const int chain_fastest = [] {  // OWRX_FC_ORDER=kappa: the previous order (A/B)
+        const char* v = getenv("OWRX_FC_ORDER");
+        return (v && strcmp(v, "kappa") == 0) ? 0 : 1;
+    }();
     if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
     if (wide)
-        hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, Y);
+        hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     else
-        hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, Y);
+        hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     HIPCHK_RET(hipGetLastError());
     if (mac1) HIPCHK_RET(hipEventRecord(mac1, st));
     const int rw = 1024 / M;

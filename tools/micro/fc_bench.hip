@@ -47,11 +47,11 @@ int main(int argc, char** argv) {
         for (const L& l : ls) {
             auto run = [&]() {
                 if (wide) {
-                    if (l.nt) hipLaunchKernelGGL((fc_mac<2, 4, true>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, Y);
-                    else hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, Y);
+                    if (l.nt) hipLaunchKernelGGL((fc_mac<2, 4, true>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, 1, Y);
+                    else hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, 1, Y);
                 } else {
-                    if (l.nt) hipLaunchKernelGGL((fc_mac<1, 8, true>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, Y);
-                    else hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, Y);
+                    if (l.nt) hipLaunchKernelGGL((fc_mac<1, 8, true>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, 1, Y);
+                    else hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, 0, U, W, l.cs, l.ks, C, Fs, F, Dp, M, ncg, 1, Y);
                 }
             };
             run();
