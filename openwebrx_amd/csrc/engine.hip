@@ -56,9 +56,10 @@ hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_e
 int ddc_padded_p(int p);
 int ddc_segments(int D, int nseg, int P, int nchains);
 int ddc_blocks_per_cu(int P, int nchains);
-hipError_t launch_fc_make_w(int logm, const float* h, int T, int D, int Dp, int P,
+int fc_frame_supported(int m);  // kernels_fcddc.hip
+hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
                             uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st);
-hipError_t launch_fc_ddc(int logm, const float2* blk, int64_t blk_start, int64_t blk_end,
+hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
@@ -205,8 +206,8 @@ struct ChainGroup {
     int nseg = 1;
     DdcChain* h_chains[2] = {};  // pinned copy sources, per block parity
     int h_cap = 0;
-    // fast-convolution form (kernels_fcddc.hip); fc_logm == 0: direct form only
-    int fc_logm = 0;
+    // fast-convolution form (kernels_fcddc.hip): frame length M; 0: direct form only
+    int fc_M = 0;
     int fc_P = 0;                 // ceil(T / D), unpadded
     int fc_V = 0;                 // valid outputs per frame, M - P + 1
     int fc_Dp = 0;                // branches padded to a multiple of 96
@@ -788,8 +789,8 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         g->partial_elems = alloc;
     }
     g->nseg = nseg;
-    if (g->fc_logm) {  // fast-convolution product rows Y[chains][Fs][M]
-        const size_t ny = (size_t)std::max(1, n) * g->fc_Fs * ((size_t)1 << g->fc_logm);
+    if (g->fc_M) {  // fast-convolution product rows Y[chains][Fs][M]
+        const size_t ny = (size_t)std::max(1, n) * g->fc_Fs * (size_t)g->fc_M;
         if (ny > g->fc_y_elems) {
             RCCHK(drain_all(e));
             dfree(g->d_fc_y);
@@ -800,16 +801,15 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     return OWRX_OK;
 }
 
-// Frame length M = 2^logm of the fast-convolution DDC for a group: the M (64, 128, 256) with
+// Frame length M of the fast-convolution DDC for a group: the M (64, 128, 192, 256, 384) with
 // the least modelled time per block and chain, max(f32 MFMA time of the padded frame tiles, HBM
 // time of the W reads), ties to the longer frame (fewer frames: less U / Y traffic).  0 when
 // the branch filters are too long for these frames (the group then runs the direct form).
-static int fc_choose_logm(int D, int P, int64_t nk_max) {
+static int fc_choose_m(int D, int P, int64_t nk_max) {
     const int Dp = (D + 95) / 96 * 96;
     int best = 0;
     double best_t = 0;
-    for (int logm = 8; logm >= 6; --logm) {
-        const int M = 1 << logm;
+    for (int M : {384, 256, 192, 128, 64}) {
         const int V = M - P + 1;
         if (V < M / 2) continue;
         const int64_t F = (nk_max + V - 1) / V;
@@ -819,7 +819,7 @@ static int fc_choose_logm(int D, int P, int64_t nk_max) {
         const double wbytes = 8.0 * M * Dp * (Fp / ft);
         const double t = std::max(flop / 150e12, wbytes / 5e12);
         if (!best || t < best_t * 0.999) {
-            best = logm;
+            best = M;
             best_t = t;
         }
     }
@@ -831,8 +831,8 @@ static int fc_choose_logm(int D, int P, int64_t nk_max) {
 // old spectra).
 static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
     ChainGroup* g = c->group;
-    if (!g->fc_logm) return OWRX_OK;
-    HIPCHK(launch_fc_make_w(g->fc_logm, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P, c->rate_fx,
+    if (!g->fc_M) return OWRX_OK;
+    HIPCHK(launch_fc_make_w(g->fc_M, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P, c->rate_fx,
                             g->d_fc_w + (int64_t)slot * g->fc_Dp, g->fc_w_ks(), e->sA));
     return OWRX_OK;
 }
@@ -840,8 +840,8 @@ static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
 // Room for `slots` members' spectra (the engine is drained): grows W[kappa][slot][Dp] by
 // doubling, moving the existing rows with one strided copy.
 static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
-    if (!g->fc_logm || slots <= g->fc_w_cap) return OWRX_OK;
-    const int M = 1 << g->fc_logm;
+    if (!g->fc_M || slots <= g->fc_w_cap) return OWRX_OK;
+    const int M = g->fc_M;
     const int cap = std::max(std::max(32, 2 * g->fc_w_cap), slots);
     float2* nw = nullptr;
     HIPCHK(dalloc(&nw, (size_t)M * cap * g->fc_Dp));
@@ -1058,7 +1058,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         }
         HIPCHK(kcopy(g->d_chains, g->h_chains[bp], sizeof(DdcChain) * g->members.size(), e->sA));
         work.push_back(GroupWork{g, k_end, (int)nk64,
-                                 g->fc_logm != 0 && e->ddc_mode == OWRX_DDC_FAST});
+                                 g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST});
     }
     if (timed) {
         HIPCHK(hipEventRecord(S.a1, e->sA));
@@ -1071,7 +1071,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         if (gw.fast) {
             // the first fast group's GEMM is timed (one group in the benchmark configurations)
             const bool tm = timed && !S.timed_mac;
-            HIPCHK(launch_fc_ddc(g->fc_logm, blk, blk_start, blk_end, g->d_chains, g->d_fc_w,
+            HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, blk_end, g->d_chains, g->d_fc_w,
                                  g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
                                  g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
                                  g->d_fc_y, g->d_partial[si], e->sA, tm ? S.m0 : nullptr,
@@ -1079,7 +1079,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             if (tm) {
                 // algorithmic work of that GEMM: 8 flop per complex MAC over the frames that
                 // carry outputs; bytes = W (every member's spectra) + U + Y, each moved once
-                const double M = (double)(1 << g->fc_logm);
+                const double M = (double)g->fc_M;
                 const double F = (double)((nk + g->fc_V - 1) / g->fc_V);
                 const double C = (double)g->members.size();
                 e->stats.ddc_mac_flop += 8.0 * M * g->fc_Dp * C * F;
@@ -1806,14 +1806,13 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         // fast-convolution form: frame length, branch padding, U and twiddles
         ng->fc_P = (T + D - 1) / D;
         const int64_t nk_max = e->max_block / D + 4;
-        ng->fc_logm = ng->fc_P <= 64 ? fc_choose_logm(D, ng->fc_P, nk_max) : 0;
-        if (const char* v = getenv("OWRX_FC_LOGM")) {  // A/B: force the frame length
-            const int lm = atoi(v);
-            if (ng->fc_logm && lm >= 6 && lm <= 8 && (1 << lm) - ng->fc_P + 1 >= (1 << lm) / 2)
-                ng->fc_logm = lm;
+        ng->fc_M = ng->fc_P <= 64 ? fc_choose_m(D, ng->fc_P, nk_max) : 0;
+        if (const char* v = getenv("OWRX_FC_M")) {  // A/B: force the frame length
+            const int m = atoi(v);
+            if (ng->fc_M && fc_frame_supported(m) && m - ng->fc_P + 1 >= m / 2) ng->fc_M = m;
         }
-        if (ng->fc_logm) {
-            const int M = 1 << ng->fc_logm;
+        if (ng->fc_M) {
+            const int M = ng->fc_M;
             ng->fc_V = M - ng->fc_P + 1;
             ng->fc_Dp = (D + 95) / 96 * 96;  // kFcDpAlign (kernels_fcddc.hip)
             ng->fc_Fs = (int)((nk_max + ng->fc_V - 1) / ng->fc_V + 15) & ~15;
@@ -1899,7 +1898,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         free_chain(c.get());
         return rc;
     }
-    if (g->fc_logm) {
+    if (g->fc_M) {
         int wrc = fc_reserve(e, g, (int)g->members.size() + 1);
         if (!wrc) wrc = fc_build_w(e, c.get(), (int)g->members.size());
         if (wrc) {
@@ -1927,8 +1926,8 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     // swap-remove: the last member takes the slot (and its filter spectra move with it)
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
     const int last = (int)g->members.size() - 1;
-    if (slot != last && g->fc_logm) {
-        const int M = 1 << g->fc_logm;
+    if (slot != last && g->fc_M) {
+        const int M = g->fc_M;
         const size_t pitch = sizeof(float2) * (size_t)g->fc_w_ks();
         HIPCHK(hipMemcpy2DAsync(g->d_fc_w + (int64_t)slot * g->fc_Dp, pitch,
                                 g->d_fc_w + (int64_t)last * g->fc_Dp, pitch,

@@ -44,14 +44,60 @@ typedef __attribute__((address_space(1))) const fc_f4 gf4;  // global (not flat)
 constexpr int kFcRT = 16;   // branches (r) per fc_fwd / fc_make_w workgroup
 constexpr int kFcDpAlign = 96;  // Dp: a multiple of kFcRT and of 4 (K split) x 3 K-blocks of 8
 
+// Frame lengths: powers of two (64, 128, 256) and three times one (192, 384).  A row of
+// M = 3 L is kept as three sub-rows of L (stride SRS), x[L n1 + n2] at sub-row n1, so the
+// M-point DFT is a radix-3 pass over n1 (twiddled by W_M^(n2 k1)) then L-point DFTs of the
+// sub-rows; bin k = k1 + 3 k2 lands in sub-row k1 at k2.  (M = 192 fits the C2 / C3 block:
+// 31 frames of V = 166 in two 16-frame MFMA tiles, where M = 256 needs 22 of 32.)
+template <int M>
+struct FcM {
+    static constexpr bool R3 = (M % 3) == 0;
+    static constexpr int L = R3 ? M / 3 : M;
+    static constexpr int LOGL = L == 32 ? 5 : L == 64 ? 6 : L == 128 ? 7 : 8;
+    static_assert((1 << LOGL) == L, "frame length");
+    static constexpr int SRS = L + 1;                 // sub-row stride (float2), R3 only
+    static constexpr int RS = R3 ? 3 * SRS : M + 1;   // row stride
+    // LDS position of time sample i / of bin k within a row
+    OWRX_DEV static int tpos(int i) { return R3 ? (i / L) * SRS + i % L : i; }
+    OWRX_DEV static int kpos(int k) { return R3 ? (k % 3) * SRS + k / 3 : k; }
+};
+
+// forward M-point DFT of R rows (row stride FcM<M>::RS) in place; tw: the M-point table
+template <int M, int R, int NT>
+OWRX_DEV void fc_fft_rows(float2* sm, const float2* __restrict__ tw) {
+    using F = FcM<M>;
+    if constexpr (!F::R3) {
+        lds_fft_rows<F::LOGL, R, NT>(sm, F::RS, tw, 1);
+    } else {
+        constexpr int L = F::L, SRS = F::SRS;
+        const float c3 = -0.5f, s3 = -0.86602540378443865f;  // W_3 = e^{-j 2 pi / 3}
+        for (int e = threadIdx.x; e < R * L; e += NT) {
+            const int row = e / L, n2 = e % L;
+            float2* b = sm + row * F::RS + n2;
+            const float2 a0 = b[0], a1 = b[SRS], a2 = b[2 * SRS];
+            const float2 sp = make_float2(a1.x + a2.x, a1.y + a2.y);
+            const float2 sm_ = make_float2(a1.x - a2.x, a1.y - a2.y);
+            const float2 y0 = make_float2(a0.x + sp.x, a0.y + sp.y);
+            const float2 t = make_float2(a0.x + c3 * sp.x, a0.y + c3 * sp.y);
+            // y1 = t + j s3 sm_, y2 = t - j s3 sm_
+            const float2 y1 = make_float2(t.x - s3 * sm_.y, t.y + s3 * sm_.x);
+            const float2 y2 = make_float2(t.x + s3 * sm_.y, t.y - s3 * sm_.x);
+            b[0] = y0;
+            b[SRS] = n2 ? cmul(y1, tw[n2]) : y1;
+            b[2 * SRS] = n2 ? cmul(y2, tw[2 * n2]) : y2;
+        }
+        __syncthreads();
+        lds_fft_rows<F::LOGL, 3 * R, NT>(sm, SRS, tw, 3);  // W_L^m = W_M^(3 m)
+    }
+}
+
 // ---- W_c[kappa][r], fp64, one chain per launch --------------------------------------------
 // grid: Dp / kFcRT workgroups; block 256.  h: the group's linear taps (T floats); the chain's
 // row kappa is written at W + kappa * w_ks.
-template <int LOGM>
+template <int M>
 __global__ void __launch_bounds__(256)
 fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rate_fx,
           float2* __restrict__ W, int64_t w_ks) {
-    constexpr int M = 1 << LOGM;
     __shared__ double2 g[kFcRT][64];   // P <= 64
     __shared__ double2 tw[M];          // e^{+j 2 pi m / M}
     const int tid = threadIdx.x;
@@ -83,7 +129,7 @@ fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rat
         double re = 0.0, im = 0.0;
         for (int p = 0; p < P; ++p) {
             const double2 a = g[j][p];
-            const double2 b = tw[(p * kap) & (M - 1)];
+            const double2 b = tw[(p * kap) % M];
             re += a.x * b.x - a.y * b.y;
             im += a.x * b.y + a.y * b.x;
         }
@@ -93,12 +139,12 @@ fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rat
 
 // ---- U[kappa][f][r]: M-point DFT of every branch frame --------------------------------------
 // grid: (Dp / kFcRT, F); block 256.  tw: M-point table e^{-j 2 pi m / M}.
-template <int LOGM>
+template <int M>
 __global__ void __launch_bounds__(256)
 fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64_t k_begin,
        int V, int D, int Dp, int Fs, const float2* __restrict__ tw, float2* __restrict__ U) {
-    constexpr int M = 1 << LOGM;
-    constexpr int RS = M + 1;          // LDS row stride (float2): column writes hit distinct banks
+    using FM = FcM<M>;
+    constexpr int RS = FM::RS;         // LDS row stride (float2): column writes hit distinct banks
     __shared__ float2 sm[kFcRT * RS];
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * kFcRT;
@@ -112,14 +158,14 @@ fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64
         const int64_t n = (k0 + i) * (int64_t)D + r;
         float2 x = make_float2(0.0f, 0.0f);
         if (r < D && n < blk_end) x = blk[n - blk_start];
-        sm[j * RS + i] = x;
+        sm[j * RS + FM::tpos(i)] = x;
     }
     __syncthreads();
-    lds_fft_rows<LOGM, kFcRT, 256>(sm, RS, tw, 1);
+    fc_fft_rows<M, kFcRT, 256>(sm, tw);
     float2* out = U + (int64_t)f * Dp + r0 + j;
 #pragma unroll 4
     for (int kap = tid / kFcRT; kap < M; kap += 256 / kFcRT)
-        out[(int64_t)kap * Fs * Dp] = sm[j * RS + kap];
+        out[(int64_t)kap * Fs * Dp] = sm[j * RS + FM::kpos(kap)];
 }
 
 // ---- Y_c[f][kappa] = sum_r U[kappa][f][r] W_c[kappa][r] on the f32 MFMA ---------------------
@@ -287,14 +333,14 @@ OWRX_DEV float2 fc_rotator(const DdcChain& ch, int64_t n) {
     return make_float2(c, s);
 }
 
-template <int LOGM>
+template <int M>
 __global__ void __launch_bounds__(256)
 fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nchains, int Fs,
        int F, int V, int D, int64_t k_begin, int nk, const float2* __restrict__ tw,
        float2* __restrict__ out) {
-    constexpr int M = 1 << LOGM;
-    constexpr int RW = 1024 / M;
-    constexpr int RS = M + 4;
+    using FM = FcM<M>;
+    constexpr int RW = FM::R3 ? 3072 / M : 1024 / M;
+    constexpr int RS = FM::RS;
     __shared__ float2 sm[RW * RS];
     const int tid = threadIdx.x;
     const int row0 = blockIdx.x * RW;
@@ -308,10 +354,10 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
             const int c = row / F, f = row % F;
             v = Y[((int64_t)c * Fs + f) * M + kap];
         }
-        sm[rr * RS + kap] = make_float2(v.x, -v.y);
+        sm[rr * RS + FM::tpos(kap)] = make_float2(v.x, -v.y);
     }
     __syncthreads();
-    lds_fft_rows<LOGM, RW, 256>(sm, RS, tw, 1);
+    fc_fft_rows<M, RW, 256>(sm, tw);
     const float inv = 1.0f / (float)M;
     for (int e = tid; e < RW * M; e += 256) {
         const int rr = e / M, m = e % M;
@@ -320,7 +366,7 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
         const int c = row / F, f = row % F;
         const int kk = f * V + m;
         if (kk >= nk) continue;
-        const float2 z = sm[rr * RS + m];
+        const float2 z = sm[rr * RS + FM::kpos(m)];
         const float2 y = make_float2(z.x * inv, -z.y * inv);
         const float2 rot = fc_rotator(chains[c], (k_begin + kk) * (int64_t)D);
         out[(int64_t)c * nk + kk] = cmul(y, rot);
@@ -329,34 +375,39 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
 
 // ---- host launchers ----------------------------------------------------------------------
 
-hipError_t launch_fc_make_w(int logm, const float* h, int T, int D, int Dp, int P,
+#define OWRX_FC_SWITCH(m, CALL)          \
+    switch (m) {                         \
+        case 64: CALL(64); break;        \
+        case 128: CALL(128); break;      \
+        case 192: CALL(192); break;      \
+        case 256: CALL(256); break;      \
+        case 384: CALL(384); break;      \
+        default: return hipErrorInvalidValue; \
+    }
+
+int fc_frame_supported(int m) { return m == 64 || m == 128 || m == 192 || m == 256 || m == 384; }
+
+hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
                             uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st) {
     const dim3 grid(Dp / kFcRT);
-    switch (logm) {
-        case 6: hipLaunchKernelGGL(fc_make_w<6>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks); break;
-        case 7: hipLaunchKernelGGL(fc_make_w<7>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks); break;
-        case 8: hipLaunchKernelGGL(fc_make_w<8>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks); break;
-        default: return hipErrorInvalidValue;
-    }
+#define OWRX_FC_W(MM) hipLaunchKernelGGL(fc_make_w<MM>, grid, dim3(256), 0, st, h, T, D, Dp, P, rate_fx, W, w_ks)
+    OWRX_FC_SWITCH(m, OWRX_FC_W)
+#undef OWRX_FC_W
     return hipGetLastError();
 }
 
 // frames per block F = ceil(nk / V); U: [M][Fs][Dp], Y: [nchains][Fs][M], out: [nchains][nk]
-hipError_t launch_fc_ddc(int logm, const float2* blk, int64_t blk_start, int64_t blk_end,
+hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
                          hipEvent_t mac0, hipEvent_t mac1) {
-    const int M = 1 << logm;
     const int F = (nk + V - 1) / V;
     if (F > Fs || nk <= 0 || nchains <= 0) return hipErrorInvalidValue;
     const dim3 gf(Dp / kFcRT, F);
-    switch (logm) {
-        case 6: hipLaunchKernelGGL(fc_fwd<6>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U); break;
-        case 7: hipLaunchKernelGGL(fc_fwd<7>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U); break;
-        case 8: hipLaunchKernelGGL(fc_fwd<8>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U); break;
-        default: return hipErrorInvalidValue;
-    }
+#define OWRX_FC_F(MM) hipLaunchKernelGGL(fc_fwd<MM>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U)
+    OWRX_FC_SWITCH(M, OWRX_FC_F)
+#undef OWRX_FC_F
     HIPCHK_RET(hipGetLastError());
     // wave tiles: 32 frames x 32 chains, or 16 frames x 64 chains when a block has <= 16 frames
     const bool wide = F > 16;
@@ -377,14 +428,14 @@ hipError_t launch_fc_ddc(int logm, const float2* blk, int64_t blk_start, int64_t
         hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     HIPCHK_RET(hipGetLastError());
     if (mac1) HIPCHK_RET(hipEventRecord(mac1, st));
-    const int rw = 1024 / M;
+    const int rw = (M % 3 == 0) ? 3072 / M : 1024 / M;
     const dim3 go((nchains * F + rw - 1) / rw);
-    switch (logm) {
-        case 6: hipLaunchKernelGGL(fc_out<6>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out); break;
-        case 7: hipLaunchKernelGGL(fc_out<7>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out); break;
-        case 8: hipLaunchKernelGGL(fc_out<8>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out); break;
-    }
+#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out)
+    OWRX_FC_SWITCH(M, OWRX_FC_O)
+#undef OWRX_FC_O
     return hipGetLastError();
 }
+
+#undef OWRX_FC_SWITCH
 
 }  // namespace owrx

@@ -445,6 +445,30 @@ def test_ddc_fast_convolution_equals_direct(amd, fs, modes, block):
     eng_d.close()
 
 
+@pytest.mark.parametrize("m", [64, 128, 192, 256, 384])
+def test_ddc_fast_convolution_frame_lengths(amd, m, monkeypatch):
+    """Every frame length the engine can pick -- powers of two and the radix-3 ones (192 = 3 x
+    64, 384 = 3 x 128: a radix-3 pass then sub-row FFTs) -- forced on the C2 design (D = 833,
+    22223 taps), ragged blocks: the DDC of sampled chains <= 1e-5 rel-RMS vs the oracle."""
+    from openwebrx_amd import synth
+    monkeypatch.setenv("OWRX_FC_M", str(m))
+    fs = 10000000
+    modes = ["nfm", "usb", "am", "cw"] * 5
+    block = 1 << 19
+    n = 2 * block + 54321
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, m_, output=amd._lib.OUT_S16)
+             for o, m_ in zip(offs, modes)]
+    eng, chains = _run_chains(amd, iq, fs, plist, block, ddc_mode="fast")
+    assert eng.stats()["ddc_fast_launches"] == eng.stats()["ddc_launches"] > 0
+    for c in (0, 7, 19):
+        ref = oracle.stages(iq, plist[c])
+        got = chains[c].read_debug(0)
+        assert got.size == ref["ddc"].size, (c, got.size, ref["ddc"].size)
+        assert rel_rms(got, ref["ddc"]) < 1e-5, (m, c, rel_rms(got, ref["ddc"]))
+    eng.close()
+
+
 def test_ddc_fast_convolution_membership_churn(amd):
     """Chains leaving a fast-convolution group mid-stream: the last member takes the freed slot
     of the group's filter-spectra matrix (swap-remove) and a retuned chain gets rebuilt spectra;
