@@ -139,11 +139,13 @@ def cpu_baseline(fs, n_fft, hop, avg, plist):
 
 
 def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block,
-                   ddc_mode="fast"):
+                   ddc_mode="fast", churn=False):
     """SURVEY.md 8d measurement 1: feed the stream at its nominal rate through the host push path
     (SDR -> host cf32 -> PCIe -> HBM, owrx_push_iq) to a fresh engine with the same waterfall and
     chains; every block is pushed on its wall-clock deadline, then synced and drained.  Keeps up
-    when no output ring overran and every block finished within its own period."""
+    when no output ring overran and every block finished within its own period.  With `churn`,
+    one client leaves and another joins (owrx_chain_destroy + owrx_chain_create) while every
+    other block is still in flight: their latency is reported (both drain the pipeline)."""
     t_setup = time.perf_counter()
     eng = Engine(fs, max_block=block)
     eng.set_ddc_mode(ddc_mode)
@@ -157,7 +159,7 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     t_setup = time.perf_counter() - t_setup
     period = block / fs
     nblocks = max(1, int(seconds / period))
-    lat = []
+    lat, joins, leaves = [], [], []
     t0 = time.perf_counter()
     for i in range(nblocks):
         wait = t0 + i * period - time.perf_counter()
@@ -165,13 +167,27 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             time.sleep(wait)
         a = time.perf_counter()
         eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
+        if churn and i % 2 == 1 and chains:
+            c0 = time.perf_counter()
+            chains.pop(i % len(chains)).close()
+            c1 = time.perf_counter()
+            chains.append(eng.chain(plist[(i * 7) % len(plist)]))
+            c2 = time.perf_counter()
+            leaves.append(c1 - c0)
+            joins.append(c2 - c1)
         eng.sync()
         eng.read_chains(chains)
         wf.read()
         lat.append(time.perf_counter() - a)
     st = eng.stats()
     eng.close()
-    return {"seconds": round(nblocks * period, 2), "stream_msps": fs / 1e6, "chains": len(plist),
+    extra = {}
+    if joins:
+        extra = {"client_join_ms": {"mean": round(1e3 * sum(joins) / len(joins), 3),
+                                    "max": round(1e3 * max(joins), 3), "n": len(joins)},
+                 "client_leave_ms": {"mean": round(1e3 * sum(leaves) / len(leaves), 3),
+                                     "max": round(1e3 * max(leaves), 3), "n": len(leaves)}}
+    return {**extra, "seconds": round(nblocks * period, 2), "stream_msps": fs / 1e6, "chains": len(plist),
             "setup_s": round(t_setup, 2),
             "blocks": nblocks, "block_period_ms": round(1e3 * period, 2),
             "max_block_latency_ms": round(1e3 * max(lat), 3),
@@ -413,7 +429,7 @@ def main():
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
         _log("real-time check")
         rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
-                            args.realtime_seconds, 1 << 20, args.ddc)
+                            args.realtime_seconds, 1 << 20, args.ddc, churn=True)
     cap = None
     if rank == 0 and world == 1 and args.capacity_ladder:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
