@@ -253,6 +253,10 @@ int owrx_set_ddc_mode(owrx_engine* e, int mode);
 #define OWRX_MOD_GAIN 13          /* Gain(format, p0); p1 = 1 complex (n samples), 0 float */
 #define OWRX_MOD_SHIFT 14         /* Shift(p0 = rate), cf32; phase continuous across calls */
 #define OWRX_MOD_BANDPASS 15      /* Bandpass(p0 = low, p1 = high, p2 = transition), cf32 */
+#define OWRX_MOD_AFC 17            /* Afc(p0 = updatePeriod, p1 = samplePeriod), cf32 -> cf32:
+                                     carrier frequency tracking of SAm / RawSAm
+                                     (csdr/chain/analog.py:141-167); csdr's algorithm is not in
+                                     the reference: the build's documented choice */
 #define OWRX_MOD_AUDIO_RESAMPLER 16 /* AudioResampler(p0 = input rate, p1 = output rate), f32:
                                        rational L/M polyphase lowpass (the build's choice) */
 typedef struct owrx_module owrx_module;

@@ -39,6 +39,7 @@ MOD_GAIN = 13
 MOD_SHIFT = 14
 MOD_BANDPASS = 15
 MOD_AUDIO_RESAMPLER = 16
+MOD_AFC = 17
 
 
 class ChainParams(ctypes.Structure):

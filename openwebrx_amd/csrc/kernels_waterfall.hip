@@ -187,6 +187,22 @@ OWRX_DEV void dft4(c2& a0, c2& a1, c2& a2, c2& a3) {
     a3 = pk_sub_mi(t1, d);
 }
 
+// W_32^m = exp(-2 pi i m / 32), m < 32 (compile-time after unrolling)
+OWRX_DEV c2 w32(int m) {
+    const float c[8] = {1.0f, 0.98078528040323043f, 0.92387953251128676f, 0.83146961230254524f,
+                        0.70710678118654752f, 0.55557023301960218f, 0.38268343236508977f,
+                        0.19509032201612827f};
+    // cos / sin of 2 pi m / 32 from the first octant
+    const int q = (m >> 3) & 3, r = m & 7;
+    const float cr = c[r], sr = r ? c[8 - r] : 0.0f;
+    float cs, sn;
+    if (q == 0) { cs = cr; sn = sr; }
+    else if (q == 1) { cs = -sr; sn = cr; }
+    else if (q == 2) { cs = -cr; sn = -sr; }
+    else { cs = sr; sn = -cr; }
+    return c2{cs, -sn};
+}
+
 template <int R>
 OWRX_DEV void dft_r(c2* a) {
     if constexpr (R == 2) {
@@ -207,6 +223,26 @@ OWRX_DEV void dft_r(c2* a) {
             const c2 t = k1 ? pk_mul(b1[k1], w[k1]) : b1[k1];
             a[k1] = b0[k1] + t;
             a[k1 + 4] = b0[k1] - t;
+        }
+    } else if constexpr (R == 32) {
+        // n = 4 n1 + n2 (n1 < 8, n2 < 4), k = k1 + 8 k2: DFT8 over n1, twiddle W32^(n2 k1),
+        // DFT4 over n2
+        c2 b[4][8];
+#pragma unroll
+        for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+            for (int n1 = 0; n1 < 8; ++n1) b[n2][n1] = a[4 * n1 + n2];
+            dft_r<8>(b[n2]);
+        }
+#pragma unroll
+        for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+            for (int k1 = 1; k1 < 8; ++k1) b[n2][k1] = pk_mul(b[n2][k1], w32(n2 * k1));
+#pragma unroll
+        for (int k1 = 0; k1 < 8; ++k1) {
+            dft4(b[0][k1], b[1][k1], b[2][k1], b[3][k1]);
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) a[k1 + 8 * k2] = b[k2][k1];
         }
     } else {
         static_assert(R == 16, "radix");
@@ -348,6 +384,108 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = acc[r].x + acc[r].y;
+    }
+}
+
+// ---- wf_fft_rx<LOGN, R>: the same product with radix-R passes, N/R threads -----------------
+// R = 32: 512 threads of 32 points at N = 16384, two LDS round trips per frame (radix 32, 32,
+// then a last radix 16) instead of three; |X|^2 summed in fp32 per bin (one register per bin).
+// The LDS image is padded one element in R.  Selected by OWRX_WF_KERNEL=r32 (A/B).
+template <int LOGN, int R>
+struct WfRx {
+    static constexpr int LOGR = R == 16 ? 4 : 5;
+    static constexpr int N = 1 << LOGN;
+    static constexpr int NT = N / R;
+    static constexpr int PR = LOGN / LOGR;                      // radix-R passes
+    static constexpr int RL = 1 << (LOGN - LOGR * PR);          // last radix (1: none)
+    static constexpr int BL = RL > 1 ? N / RL / NT : 1;         // butterflies / thread, last
+    static constexpr int NACC = RL > 1 ? BL * RL : R;           // bins per thread
+    static constexpr size_t kLds = sizeof(float2) * (N + N / R);
+    OWRX_DEV static int pad(int i) { return i + (i >> LOGR); }
+};
+
+template <int LOGN, int R>
+__global__ void __launch_bounds__((WfRx<LOGN, R>::NT))
+wf_fft_rx(const float2* __restrict__ blk, int64_t blk_start,
+          const WfGroup* __restrict__ groups, const float* __restrict__ window,
+          const float2* __restrict__ tw, float* __restrict__ partial) {
+    using K = WfRx<LOGN, R>;
+    constexpr int N = K::N, NT = K::NT, PR = K::PR, RL = K::RL, BL = K::BL;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int tid0 = threadIdx.x;
+    const WfGroup g = groups[blockIdx.x];
+    float acc[K::NACC];  // sum |X|^2 per bin
+#pragma unroll
+    for (int m = 0; m < K::NACC; ++m) acc[m] = 0.0f;
+    c2 nx[R];  // the next frame's samples, loaded while this frame's LDS passes run
+#pragma unroll
+    for (int r = 0; r < R; ++r) nx[r] = c2_of(blk[g.start - blk_start + tid0 + r * NT]);
+#pragma unroll 1
+    for (int f = 0; f < g.nframes; ++f) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));  // keeps each pass's address arithmetic in the loop
+        c2 a[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) a[r] = nx[r] * window[tid + r * NT];
+        int ns = 1;
+#pragma unroll
+        for (int pass = 0; pass < PR; ++pass) {
+            if (pass > 0) {
+                __syncthreads();  // the previous pass's stores
+#pragma unroll
+                for (int r = 0; r < R; ++r) a[r] = c2_of(sm[K::pad(tid + r * NT)]);
+                const int k = tid & (ns - 1);
+                if (k) twiddle_r<R>(a, c2_of(tw[k * (N / (ns * R))]));  // W_(R Ns)^k
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dft_r<R>(a);
+            __builtin_amdgcn_sched_barrier(0);
+            const bool last = (pass == PR - 1) && RL == 1;
+            if (last) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] = fmaf(a[r].x, a[r].x, fmaf(a[r].y, a[r].y, acc[r]));
+            } else {
+                if (pass > 0) __syncthreads();  // every load of this pass before any store
+                const int k = tid & (ns - 1);
+                const int d = ((tid / ns) * ns * R) + k;
+#pragma unroll
+                for (int r = 0; r < R; ++r) sm[K::pad(d + r * ns)] = f2_of(a[r]);
+                if (pass == 0 && f + 1 < g.nframes) {
+                    const float2* xn = blk + (g.start + (int64_t)(f + 1) * g.hop - blk_start);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) nx[r] = c2_of(xn[tid + r * NT]);
+                }
+            }
+            ns *= R;
+        }
+        if constexpr (RL > 1) {
+            // last pass: radix RL, Ns = N / RL, butterflies j = tid + b NT, outputs j + r N/RL
+            __syncthreads();
+#pragma unroll
+            for (int b = 0; b < BL; ++b) {
+                const int j = tid + b * NT;
+                c2 c[RL];
+#pragma unroll
+                for (int r = 0; r < RL; ++r) c[r] = c2_of(sm[K::pad(j + r * (N / RL))]);
+                if (j) twiddle_r<RL>(c, c2_of(tw[j]));  // W_N^(r j)
+                dft_r<RL>(c);
+#pragma unroll
+                for (int r = 0; r < RL; ++r)
+                    acc[b * RL + r] = fmaf(c[r].x, c[r].x, fmaf(c[r].y, c[r].y, acc[b * RL + r]));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();  // LDS reused by the next frame
+    }
+    float* out = partial + (int64_t)blockIdx.x * N;
+    if constexpr (RL > 1) {
+#pragma unroll
+        for (int b = 0; b < BL; ++b)
+#pragma unroll
+            for (int r = 0; r < RL; ++r) out[tid0 + b * NT + r * (N / RL)] = acc[b * RL + r];
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) out[tid0 + r * NT] = acc[r];
     }
 }
 
@@ -508,6 +646,32 @@ static hipError_t launch_fft_r16(const float2* blk, int64_t blk_start, const WfG
     return hipGetLastError();
 }
 
+template <int LOGN>
+static hipError_t launch_fft_r32(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                 int ngroups, const float* window, const float2* tw,
+                                 float* partial, hipStream_t st) {
+    using K = WfRx<LOGN, 32>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_rx<LOGN, 32>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)K::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL((wf_fft_rx<LOGN, 32>), dim3(ngroups), dim3(K::NT), K::kLds, st, blk,
+                       blk_start, groups, window, tw, partial);
+    return hipGetLastError();
+}
+
+static bool wf_radix32() {  // OWRX_WF_KERNEL=r32: the radix-32 kernel (A/B)
+    static const bool v = [] {
+        const char* s = getenv("OWRX_WF_KERNEL");
+        return s && strcmp(s, "r32") == 0;
+    }();
+    return v;
+}
+
 static bool wf_radix4_only() {  // OWRX_WF_KERNEL=radix4: the radix-4 LDS kernel (A/B)
     static const bool v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
@@ -568,22 +732,32 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 10:
+            if (wf_radix32())
+                return launch_fft_r32<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             if (!wf_radix4_only())
                 return launch_fft_r16<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             return launch_fft_t<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 11:
+            if (wf_radix32())
+                return launch_fft_r32<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             if (!wf_radix4_only())
                 return launch_fft_r16<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             return launch_fft_t<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 12:
+            if (wf_radix32())
+                return launch_fft_r32<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             if (!wf_radix4_only())
                 return launch_fft_r16<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             return launch_fft_t<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 13:
+            if (wf_radix32())
+                return launch_fft_r32<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             if (!wf_radix4_only())
                 return launch_fft_r16<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             return launch_fft_t<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 14:
+            if (wf_radix32())
+                return launch_fft_r32<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             if (!wf_radix4_only())
                 return launch_fft_r16<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
             return launch_fft_t<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);

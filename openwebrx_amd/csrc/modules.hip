@@ -18,6 +18,12 @@ struct ModState {
     float2 fm_last;
     float yp, xp, yp2;
     AgcState agc;
+    // Afc: NCO phase / frequency (rad, rad per sample), pair accumulator, the corrected sample
+    // of the last pair point, samples seen, pairs accumulated
+    double afc_ph, afc_w, afc_re, afc_im;
+    float2 afc_prev;
+    int64_t afc_n;
+    int32_t afc_pairs;
     AdpcmState adpcm;
     int64_t adpcm_bytes;
     int32_t has_left;
@@ -27,7 +33,7 @@ struct ModState {
 struct ModParams {
     int type;
     float f0;
-    int i0;
+    int i0, i1;
     AgcParams agc;
     float alpha, beta;
     int fft_size;
@@ -65,6 +71,45 @@ __global__ void mod_serial(ModParams p, const void* __restrict__ in, int64_t n,
             for (int64_t k = 0; k < n; ++k) of[k] = agc_step(iff[k], p.agc, s.agc);
             o = n;
             break;
+        case OWRX_MOD_AFC: {
+            // Afc(updatePeriod U, samplePeriod S), the build's choice (csdr's is not in the
+            // reference): y = x e^{-j ph}, ph += w; every S samples the pair product
+            // y[n] conj(y[n - S]) is summed, and after U pairs w += arg(sum) / (2 S): the
+            // residual rotation per sample, half-corrected per update
+            float2* oc = (float2*)out;
+            const int U = p.i0, S = p.i1;
+            for (int64_t k = 0; k < n; ++k) {
+                double sn, cs;
+                sincos(s.afc_ph, &sn, &cs);
+                const float c = (float)cs, si = (float)sn;
+                const float2 x = ic[k];
+                float2 y;
+                {
+#pragma clang fp contract(off)
+                    y = make_float2(x.x * c + x.y * si, x.y * c - x.x * si);
+                }
+                s.afc_ph += s.afc_w;
+                if (s.afc_ph > M_PI) s.afc_ph -= 2.0 * M_PI;
+                else if (s.afc_ph < -M_PI) s.afc_ph += 2.0 * M_PI;
+                if (s.afc_n % S == 0) {
+                    if (s.afc_n >= S) {
+                        const double pr = s.afc_prev.x, pi = s.afc_prev.y;
+                        s.afc_re += (double)y.x * pr + (double)y.y * pi;
+                        s.afc_im += (double)y.y * pr - (double)y.x * pi;
+                        if (++s.afc_pairs == U) {
+                            s.afc_w += atan2(s.afc_im, s.afc_re) / (2.0 * S);
+                            s.afc_re = s.afc_im = 0.0;
+                            s.afc_pairs = 0;
+                        }
+                    }
+                    s.afc_prev = y;
+                }
+                s.afc_n++;
+                oc[k] = y;
+            }
+            o = n;
+            break;
+        }
         case OWRX_MOD_ADPCM:
             for (int64_t k = 0; k < n; ++k) {
                 if (!s.has_left) {
@@ -240,6 +285,7 @@ static int in_item_bytes(int type) {
         case OWRX_MOD_FMDEMOD:
         case OWRX_MOD_AMDEMOD:
         case OWRX_MOD_REALPART:
+        case OWRX_MOD_AFC:
         case OWRX_MOD_SHIFT:
         case OWRX_MOD_BANDPASS: return 8;
         case OWRX_MOD_AUDIO_RESAMPLER: return 4;
@@ -251,7 +297,7 @@ static int in_item_bytes(int type) {
 
 extern "C" int owrx_module_create(int device, int type, double p0, double p1, double p2,
                                   owrx_module** out) {
-    if (!out || type < OWRX_MOD_FMDEMOD || type > OWRX_MOD_AUDIO_RESAMPLER) {
+    if (!out || type < OWRX_MOD_FMDEMOD || type > OWRX_MOD_AFC) {
         set_last_error("owrx_module_create: bad type %d", type);
         return OWRX_EINVAL;
     }
@@ -278,6 +324,15 @@ extern "C" int owrx_module_create(int device, int type, double p0, double p1, do
             s.agc.env = m->p.agc.reference / m->p.agc.initial_gain;
             break;
         case OWRX_MOD_ADPCM: m->p.i0 = (int)p0; break;
+        case OWRX_MOD_AFC:
+            if (p0 < 1 || p1 < 1 || p0 != (double)(int)p0 || p1 != (double)(int)p1) {
+                delete m;
+                set_last_error("Afc: integer updatePeriod, samplePeriod >= 1 required");
+                return OWRX_EINVAL;
+            }
+            m->p.i0 = (int)p0;
+            m->p.i1 = (int)p1;
+            break;
         case OWRX_MOD_GAIN:
             m->p.f0 = (float)p0;
             m->p.i0 = p1 > 0 ? 1 : 0;  // complex: n samples = 2n floats
@@ -536,12 +591,22 @@ extern "C" int64_t owrx_module_process(owrx_module* m, const void* in, int64_t n
                                items, m->d_out);
         produced = items * item_out;
     } else {
+        // the elementwise serial modules write n outputs unconditionally
+        const int64_t need = (t == OWRX_MOD_AFC) ? 8 * n
+                             : (t == OWRX_MOD_DCBLOCK || t == OWRX_MOD_DEEMPH || t == OWRX_MOD_AGC) ? 4 * n
+                                                                                                   : 0;
+        if (need > out_cap_bytes) {
+            set_last_error("owrx_module_process: output capacity %lld < %lld",
+                           (long long)out_cap_bytes, (long long)need);
+            return OWRX_ENOSPC;
+        }
         hipLaunchKernelGGL(mod_serial, dim3(1), dim3(64), 0, m->stream, m->p, m->d_in, n,
                            m->d_out, out_cap_bytes, m->d_state, m->d_produced);
         hipMemcpyAsync(&produced, m->d_produced, sizeof(int64_t), hipMemcpyDeviceToHost, m->stream);
         if (hipStreamSynchronize(m->stream) != hipSuccess) return OWRX_EIO;
         if (t == OWRX_MOD_DCBLOCK || t == OWRX_MOD_DEEMPH || t == OWRX_MOD_AGC)
             produced *= 4;
+        if (t == OWRX_MOD_AFC) produced *= 8;
         if (produced > out_cap_bytes) {
             set_last_error("owrx_module_process: output capacity %lld < %lld",
                            (long long)out_cap_bytes, (long long)produced);

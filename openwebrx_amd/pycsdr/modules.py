@@ -751,6 +751,27 @@ class AudioResampler(_Unary):
                                 self.output_rate / self.input_rate + 0.01, *self._params())
 
 
+class Afc(_Unary):
+    """Afc(updatePeriod, samplePeriod) of SAm / RawSAm (csdr/chain/analog.py:141-167):
+    COMPLEX_FLOAT carrier frequency tracking ahead of RealPart, standalone on the GPU behind a
+    fused Selector (the planner then emits the Selector output, OWRX_OUT_SEL).  csdr's algorithm
+    is not in the reference: the build's documented choice (OWRX_MOD_AFC; parity
+    unpinned, pinned to oracle.afc)."""
+    input_format = Format.COMPLEX_FLOAT
+    output_format = Format.COMPLEX_FLOAT
+    _mod = "MOD_AFC"
+    _in_dtype = np.complex64
+    _out_size = 8
+
+    def __init__(self, updatePeriod=10, samplePeriod=4):
+        super().__init__()
+        self.update_period = int(updatePeriod)
+        self.sample_period = int(samplePeriod)
+
+    def _params(self):
+        return (self.update_period, self.sample_period)
+
+
 # ---- present for imports only (SURVEY.md 8b: may raise when instantiated) -----------------
 
 def _unsupported(name):
@@ -760,7 +781,7 @@ def _unsupported(name):
     return type(name, (_NativeModule,), {"__init__": __init__, "fusable": False})
 
 
-for _name in ("Afc", "BaudotDecoder", "Ccir476Decoder", "Ccir493Decoder",
+for _name in ("BaudotDecoder", "Ccir476Decoder", "Ccir493Decoder",
               "CwDecoder", "DBPskDecoder", "Downmix", "DscDecoder", "ExecModule", "FaxDecoder",
               "Lowpass", "MFRttyDecoder", "NavtexDecoder", "RttyDecoder",
               "SitorBDecoder", "SnrSquelch", "SstvDecoder", "Throttle", "TimingRecovery",

@@ -413,3 +413,41 @@ def audio_resample(x, in_rate, out_rate):
         ok = i >= 0
         y[m] = L * np.dot(h[j[ok]], x[i[ok]])
     return y
+
+
+def afc(x, update_period=10, sample_period=4):
+    """Afc(updatePeriod, samplePeriod) of SAm / RawSAm (csdr/chain/analog.py:141-167).  csdr's
+    algorithm is not in the reference (parity unpinned); this restates the build's documented
+    choice: y = x e^{-j ph}, ph += w (ph wrapped to [-pi, pi]); every S samples the pair
+    product y[n] conj(y[n - S]) is summed, and after U pairs w += arg(sum) / (2 S).  Phase and
+    frequency in float64, the rotation of each sample in float32 without fused multiply-adds
+    (as the kernel computes it)."""
+    x = np.asarray(x, np.complex64)
+    U, S = int(update_period), int(sample_period)
+    out = np.empty(x.size, np.complex64)
+    ph = w = acc_re = acc_im = 0.0
+    prev = (np.float32(0), np.float32(0))
+    pairs = 0
+    for n in range(x.size):
+        c, s = np.float32(np.cos(ph)), np.float32(np.sin(ph))
+        xr, xi = np.float32(x[n].real), np.float32(x[n].imag)
+        yr = np.float32(np.float32(xr * c) + np.float32(xi * s))
+        yi = np.float32(np.float32(xi * c) - np.float32(xr * s))
+        ph += w
+        if ph > np.pi:
+            ph -= 2.0 * np.pi
+        elif ph < -np.pi:
+            ph += 2.0 * np.pi
+        if n % S == 0:
+            if n >= S:
+                pr, pi_ = float(prev[0]), float(prev[1])
+                acc_re += float(yr) * pr + float(yi) * pi_
+                acc_im += float(yi) * pr - float(yr) * pi_
+                pairs += 1
+                if pairs == U:
+                    w += np.arctan2(acc_im, acc_re) / (2.0 * S)
+                    acc_re = acc_im = 0.0
+                    pairs = 0
+            prev = (yr, yi)
+        out[n] = np.complex64(complex(yr, yi))
+    return out

@@ -34,6 +34,8 @@ def _make(d):
         return getattr(M, c)()
     if c == "Limit":
         return M.Limit(d["max_amplitude"])
+    if c == "Afc":
+        return M.Afc(d["update_period"], d["sample_period"])
     if c == "NfmDeemphasis":
         return M.NfmDeemphasis(d["sample_rate"])
     if c == "WfmDeemphasis":

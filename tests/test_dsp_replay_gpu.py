@@ -163,3 +163,66 @@ def test_service_demodulator_chain_replay(step):
         want = ref["agc"]
     assert got.size == want.size > 10000, (got.size, want.size)
     assert rel_rms(got, want) < 1e-5
+
+
+@pytest.mark.gpu
+def test_sam_chain_replay():
+    """SAm (csdr/chain/analog.py:141-154) on the reference's ClientDemodulatorChain
+    (tests/golden/dsp_graph.json "sam"): the fused Selector writes its output into the buffer
+    the standalone GPU Afc reads (OWRX_OUT_SEL); Afc -> RealPart -> DcBlock -> Agc(Slow, initial
+    gain 200) run as GPU modules.  The Selector output equals the oracle's squelch stage and
+    the Agc output the oracle's afc -> realpart -> dcblock -> agc of it, <=1e-5 rel-RMS; end to
+    end the bound adds the oracle's own sensitivity to the Selector difference (Afc parity
+    unpinned: csdr's Afc is not in the reference)."""
+    import oracle
+    from openwebrx_amd import _lib
+    from openwebrx_amd.pycsdr import _graph
+    s = dsp_replay.steps()["sam"]
+    fs = 10000000
+    n = 8 * (1 << 20)
+    rng = np.random.default_rng(5)
+    t = np.arange(n) / fs
+    env = 0.05 * (1 + 0.5 * np.sin(2 * np.pi * 700.0 * t))
+    iq = (env * np.exp(2j * np.pi * (-200000.0 + 150.0) * t)  # AM, 150 Hz off the chain
+          + 0.001 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))).astype(np.complex64)
+    wide, mods, outs, power = dsp_replay.build(s)
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    sel = _collect(outs[cls.index("Squelch")])
+    agc = _collect(outs[cls.index("Agc")])
+    for i in range(0, iq.size, 100003):
+        wide.write(iq[i:i + 100003].tobytes())
+    drv = _graph._drivers.get(id(wide))
+    while drv.reader.available() > 0:
+        time.sleep(0.01)
+    _graph.finish(wide)
+    fused = drv.engine is not None and len(drv.segments) == 1
+    diag = (drv.state, drv.error, len(drv.segments))
+    t0 = time.time()
+    while sel[0].available() > 0 and time.time() - t0 < 20:
+        time.sleep(0.02)
+    want = sum(len(b) for b in sel[2]) // 2  # float32 bytes the module chain will produce
+    while sum(len(b) for b in agc[2]) < want and time.time() - t0 < 30:
+        time.sleep(0.05)
+    for col in (sel, agc):
+        col[0].stop()
+        col[1].join(5)
+    assert fused, diag
+    p = _graph.chain_params_struct(s["params"])
+    assert p.output == _lib.OUT_SEL
+    tap = np.frombuffer(b"".join(sel[2]), np.complex64)
+    ref = oracle.stages(iq, p)["squelch"]
+    assert tap.size == ref.size > 8000, (tap.size, ref.size)
+    assert rel_rms(tap, ref) < 1e-5
+    got = np.frombuffer(b"".join(agc[2]), np.float32)
+    d = {dd["class"]: dd for _, dd, _ in s["graph"]}
+    ap = oracle.agc_params(_lib.AGC_SLOW, d["Agc"]["initial_gain"])
+    chain = lambda z: oracle.agc(oracle.dcblock(oracle.realpart(
+        oracle.afc(z, d["Afc"]["update_period"], d["Afc"]["sample_period"]))), ap)
+    assert got.size == tap.size, (got.size, tap.size)
+    assert rel_rms(got, chain(tap)) < 1e-5        # the module chain on the engine's output
+    # end to end from the oracle's squelch stage: Afc's frequency loop integrates the Selector's
+    # <=1e-5 difference into a phase drift, so the bound is the oracle's own response to that
+    # input difference (chain(tap) against chain(ref)) plus the 1e-5 of the modules
+    cond = rel_rms(chain(tap), chain(ref))
+    assert cond < 1e-3, cond
+    assert rel_rms(got, chain(ref)) < cond + 1e-5, (rel_rms(got, chain(ref)), cond)

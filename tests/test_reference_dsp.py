@@ -94,7 +94,20 @@ def test_service_demodulator_chains_fuse(step, output):
     assert p["sq_level"] == 0.0 and not s["tap_selector"] and not s["tap_audio"]
 
 
-@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio"])
+def test_sam_keeps_the_selector_fused_and_runs_afc_on_the_gpu():
+    """SAm (csdr/chain/analog.py:141-154: Afc -> RealPart -> DcBlock -> Agc) set on the
+    reference's ClientDemodulatorChain: the Selector (with its squelch and s-meter) stays fused
+    and emits its output (OWRX_OUT_SEL) into the buffer the standalone GPU Afc reads; the rest
+    of the chain runs as standalone GPU modules."""
+    s = dsp_replay.steps()["sam"]
+    assert s["fused"] and s["kind"] == "chain" and s["params"]["output"] == 4
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    assert cls.index("Squelch") < cls.index("Afc") < cls.index("RealPart") < cls.index("Agc")
+    afc = [d for _, d, _ in s["graph"] if d["class"] == "Afc"][0]
+    assert (afc["update_period"], afc["sample_period"]) == (10, 4)
+
+
+@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio", "sam"])
 def test_replayed_graph_plans_like_the_reference(step):
     """The shim-built replay of each recorded graph is planned exactly as the reference's."""
     from openwebrx_amd.pycsdr import _graph
