@@ -293,7 +293,12 @@ struct WfR16 {
     static constexpr int RL = 1 << (LOGN - 4 * P16);              // last radix (1: none)
     static constexpr int BL = RL > 1 ? N / RL / NT : 1;           // butterflies / thread, last
     static constexpr int NACC = RL > 1 ? BL * RL : 16;            // bins per thread
-    static constexpr size_t kLds = sizeof(float2) * (N + N / 16);
+    // twiddle tables behind the padded frame image: passes 1 .. P16-1 (16, 256, ... entries,
+    // W_(16 Ns)^k at (Ns - 16) / 15 + k), then the last pass's bases W_N^tid (NT entries)
+    static constexpr int TW0 = N + N / 16;
+    static constexpr int NTP = P16 > 1 ? ((1 << (4 * P16)) - 16) / 15 : 0;
+    static constexpr int NTL = RL > 1 ? NT : 0;
+    static constexpr size_t kLds = sizeof(float2) * (TW0 + NTP + NTL);
 };
 
 template <int LOGN>
@@ -306,25 +311,65 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int tid0 = threadIdx.x;
     const WfGroup g = groups[blockIdx.x];
-    c2 acc[K::NACC];  // (sum re^2, sum im^2) per bin, added at the end
+    // The twiddles come from LDS tables filled once per workgroup, so the frame loop's only
+    // global loads are the next frame's samples (issued in pass 0, in flight across the passes)
+    // and the window taps at the frame's start.  vmcnt retires loads in order, so a twiddle load
+    // between the prefetch and its use would have waited for the whole prefetch.  Both go through
+    // buffer descriptors: one VGPR of per-lane offset, the frame / tap offsets in SGPRs (64-bit
+    // addresses per load take 32 VGPRs).
+    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
+    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
+    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
+        0x00020000);
+    const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
+                                                      (int)(sizeof(float) * N), 0x00020000);
+    auto load_x = [&](int f, c2* v) {
 #pragma unroll
-    for (int m = 0; m < K::NACC; ++m) acc[m] = c2{0.0f, 0.0f};
+        for (int r = 0; r < 16; ++r) {
+            // two dword loads the compiler pairs into one dwordx2 (this hipcc's vector-returning
+            // raw_buffer_load_b64 / _b128 builtins load one dword and splat it); the frame offset
+            // in the one VGPR, the tap offset r NT in the SGPR soffset
+            const int vo = tid0 * 8 + f * hop * 8;
+            v[r] = c2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
+                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0))};
+        }
+    };
+    auto load_w = [&](float* v) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, tid0 * 4, r * NT * 4, 0));
+    };
+
+    for (int i = tid0; i < K::NTP; i += NT) {
+        int base = 0, ns = 16;
+        while (i >= base + ns) {
+            base += ns;
+            ns *= 16;
+        }
+        sm[K::TW0 + i] = tw[(i - base) * (N / (ns * 16))];
+    }
+    if constexpr (RL > 1) sm[K::TW0 + K::NTP + tid0] = tw[tid0];
+    float acc[K::NACC];  // sum over the group's frames of |X|^2 per bin
+#pragma unroll
+    for (int m = 0; m < K::NACC; ++m) acc[m] = 0.0f;
     // the next frame's samples are loaded while this frame's LDS passes run
     c2 nx[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) nx[r] = c2_of(blk[g.start - blk_start + tid0 + r * NT]);
+    load_x(0, nx);
 #pragma unroll 1
-    for (int f = 0; f < g.nframes; ++f) {
+    for (int f = 0; f < nfr; ++f) {
         // opaque copy of the thread id: keeps every pass's address arithmetic inside the frame
         // loop (hoisted, the addresses of all passes stay live and spill)
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         c2 a[16];
         // pass 1 (Ns = 1, no twiddles): j = tid, inputs j + r N/16
+        {
+            float wv[16];  // L2-resident taps; the wait for them also covers the prefetch
+            load_w(wv);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float wr = window[tid + r * NT];
-            a[r] = nx[r] * wr;
+            for (int r = 0; r < 16; ++r) a[r] = nx[r] * wv[r];
         }
         int ns = 1;
 #pragma unroll
@@ -334,7 +379,7 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
 #pragma unroll
                 for (int r = 0; r < 16; ++r) a[r] = c2_of(sm[wf_pad(tid + r * NT)]);
                 const int k = tid & (ns - 1);
-                if (k) twiddle_r<16>(a, c2_of(tw[k * (N / (ns * 16))]));  // W_(16 Ns)^k
+                if (k) twiddle_r<16>(a, c2_of(sm[K::TW0 + (ns - 16) / 15 + k]));  // W_(16 Ns)^k
             }
             __builtin_amdgcn_sched_barrier(0);
             dft_r<16>(a);
@@ -342,34 +387,37 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
             const bool last = (pass == P16 - 1) && RL == 1;
             if (last) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[r] = __builtin_elementwise_fma(a[r], a[r], acc[r]);
+                for (int r = 0; r < 16; ++r) acc[r] = fmaf(a[r].y, a[r].y, fmaf(a[r].x, a[r].x, acc[r]));
             } else {
                 if (pass > 0) __syncthreads();  // every load of this pass before any store
                 const int k = tid & (ns - 1);
                 const int d = ((tid / ns) * ns * 16) + k;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) sm[wf_pad(d + r * ns)] = f2_of(a[r]);
-                if (pass == 0 && f + 1 < g.nframes) {
-                    const float2* xn = blk + (g.start + (int64_t)(f + 1) * g.hop - blk_start);
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) nx[r] = c2_of(xn[tid + r * NT]);
-                }
+                if (pass == 0 && f + 1 < nfr) load_x(f + 1, nx);
             }
             ns *= 16;
         }
         if constexpr (RL > 1) {
             // last pass: radix RL, Ns = N / RL, butterflies j = tid + b NT, outputs j + r N/RL
             __syncthreads();
+            const c2 tl = c2_of(sm[K::TW0 + K::NTP + tid]);  // W_N^tid
 #pragma unroll
             for (int b = 0; b < BL; ++b) {
                 const int j = tid + b * NT;
                 c2 c[RL];
 #pragma unroll
                 for (int r = 0; r < RL; ++r) c[r] = c2_of(sm[wf_pad(j + r * (N / RL))]);
-                if (j) twiddle_r<RL>(c, c2_of(tw[j]));  // W_N^(r j)
+                // W_N^j = W_N^tid W_16^b (NT = N / 16)
+                if (b == 0) {
+                    if (j) twiddle_r<RL>(c, tl);
+                } else {
+                    twiddle_r<RL>(c, pk_mul(tl, w32(2 * b)));
+                }
                 dft_r<RL>(c);
 #pragma unroll
-                for (int r = 0; r < RL; ++r) acc[b * RL + r] = __builtin_elementwise_fma(c[r], c[r], acc[b * RL + r]);
+                for (int r = 0; r < RL; ++r)
+                    acc[b * RL + r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b * RL + r]));
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -380,10 +428,10 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
 #pragma unroll
         for (int b = 0; b < BL; ++b)
 #pragma unroll
-            for (int r = 0; r < RL; ++r) out[tid0 + b * NT + r * (N / RL)] = acc[b * RL + r].x + acc[b * RL + r].y;
+            for (int r = 0; r < RL; ++r) out[tid0 + b * NT + r * (N / RL)] = acc[b * RL + r];
     } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = acc[r].x + acc[r].y;
+        for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = acc[r];
     }
 }
 
