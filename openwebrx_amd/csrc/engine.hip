@@ -872,7 +872,12 @@ static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
     if (w->N > kWfLdsMaxN) return 1;
     const int64_t hop = std::max(1, w->hop);
     const int64_t per_block = e->max_block / hop;
-    int64_t fpg = (per_block + std::max(1, e->cus_a) - 1) / std::max(1, e->cus_a);
+    static const int wgs_per_cu = [] {  // OWRX_WF_GROUPS_PER_CU: A/B of the group count
+        const char* s = getenv("OWRX_WF_GROUPS_PER_CU");
+        return s ? std::max(1, atoi(s)) : 1;
+    }();
+    const int64_t slots = (int64_t)std::max(1, e->cus_a) * wgs_per_cu;
+    int64_t fpg = (per_block + slots - 1) / slots;
     fpg = std::min<int64_t>(fpg, (e->history - w->N) / hop);
     return (int)std::max<int64_t>(1, std::min<int64_t>(fpg, kWfMaxFramesPerGroup));
 }

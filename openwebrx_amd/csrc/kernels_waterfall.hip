@@ -2,13 +2,14 @@
 // owrx/fft.py:36-59): Fft(size=N, every_n_samples=hop) -> LogAveragePower(add_db, N, avg)
 // -> FftSwap -> FftAdpcm.
 //
-// wf_fft_power: one workgroup (N/4 threads, <= 1024) per group of consecutive frames of one
-//   waterfall row.  Each frame: coalesced cf32 load * Hamming window -> LDS (N complex,
-//   128 KiB at N = 16384, one workgroup per CU), Stockham radix-4 passes (plus one radix-2
-//   pass for odd log2 N) in place through registers, twiddles from an L2-resident table;
-//   |X|^2 accumulated in registers across the group's frames, written once per group.
-//   Bound: HBM (8 B of IQ per input sample; frames overlap by N - hop and the overlap is
-//   re-read from L2).
+// wf_fft_r16 (1024 <= N <= 16384, production): one workgroup (N/16 threads) per group of
+//   consecutive frames of one waterfall row.  Each frame: cf32 samples * Hamming window in
+//   registers (16 per thread, the next frame prefetched during the passes), radix-16 register
+//   DFTs with Stockham exchanges through LDS (N complex + 1-in-16 padding: 136 KiB at
+//   N = 16384, one workgroup per CU), twiddle bases from LDS tables; |X|^2 summed in registers
+//   over the group's frames and written once per group.  A/B alternatives: wf_fft_ip (in-place
+//   DIF, one barrier per stage), wf_fft_rx<.., 32> (radix 32), wf_fft_power (radix 4).
+// wf_fft4_cols / wf_fft4_rows (N = 32768, 65536): four-step FFT through a cf32 scratch frame.
 // wf_finalize: sums each row's group partials in a fixed order onto the carried accumulator
 //   (rows span blocks), 10*log10 + add_db correction, fftshift, quantise (short)(dB*100).
 // wf_adpcm_rows_spec: FftAdpcm (IMA-ADPCM of each padded row), one workgroup per row,
@@ -301,6 +302,21 @@ struct WfR16 {
     static constexpr size_t kLds = sizeof(float2) * (TW0 + NTP + NTL);
 };
 
+// Phase stamps of wave 0 (diagnostic builds only: tools/micro/wf_stamp.hip defines
+// OWRX_WF_STAMPS): kernel start, per frame (first two) its start, loads arrived, each pass done,
+// and the partial row written.
+#ifdef OWRX_WF_STAMPS
+__device__ unsigned long long g_wf_stamp[1024][16];
+#define WF_STAMP(i)                                                                           \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < 16) g_wf_stamp[blockIdx.x][i] = clock64(); \
+    } while (0)
+#else
+#define WF_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
 template <int LOGN>
 __global__ void __launch_bounds__(WfR16<LOGN>::NT)
 wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
@@ -311,6 +327,7 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int tid0 = threadIdx.x;
     const WfGroup g = groups[blockIdx.x];
+    WF_STAMP(0);
     // The twiddles come from LDS tables filled once per workgroup, so the frame loop's only
     // global loads are the next frame's samples (issued in pass 0, in flight across the passes)
     // and the window taps at the frame's start.  vmcnt retires loads in order, so a twiddle load
@@ -342,6 +359,10 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
             v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, tid0 * 4, r * NT * 4, 0));
     };
 
+    // the first frame's samples are requested before the twiddle tables: the table fill waits
+    // for its own loads (vmcnt is in order), by then the frame has arrived as well
+    c2 nx[16];
+    load_x(0, nx);
     for (int i = tid0; i < K::NTP; i += NT) {
         int base = 0, ns = 16;
         while (i >= base + ns) {
@@ -354,9 +375,6 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     float acc[K::NACC];  // sum over the group's frames of |X|^2 per bin
 #pragma unroll
     for (int m = 0; m < K::NACC; ++m) acc[m] = 0.0f;
-    // the next frame's samples are loaded while this frame's LDS passes run
-    c2 nx[16];
-    load_x(0, nx);
 #pragma unroll 1
     for (int f = 0; f < nfr; ++f) {
         // opaque copy of the thread id: keeps every pass's address arithmetic inside the frame
@@ -364,6 +382,8 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
         c2 a[16];
+        const int st0 = 1 + 6 * f;
+        WF_STAMP(st0);
         // pass 1 (Ns = 1, no twiddles): j = tid, inputs j + r N/16
         {
             float wv[16];  // L2-resident taps; the wait for them also covers the prefetch
@@ -371,6 +391,7 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
 #pragma unroll
             for (int r = 0; r < 16; ++r) a[r] = nx[r] * wv[r];
         }
+        WF_STAMP(st0 + 1);
         int ns = 1;
 #pragma unroll
         for (int pass = 0; pass < P16; ++pass) {
@@ -397,6 +418,7 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
                 if (pass == 0 && f + 1 < nfr) load_x(f + 1, nx);
             }
             ns *= 16;
+            WF_STAMP(st0 + 2 + pass);
         }
         if constexpr (RL > 1) {
             // last pass: radix RL, Ns = N / RL, butterflies j = tid + b NT, outputs j + r N/RL
@@ -420,6 +442,7 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
                     acc[b * RL + r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b * RL + r]));
                 __builtin_amdgcn_sched_barrier(0);
             }
+            WF_STAMP(st0 + 5);
         }
         __syncthreads();  // LDS reused by the next frame
     }
@@ -433,6 +456,193 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
 #pragma unroll
         for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = acc[r];
     }
+    WF_STAMP(13);
+}
+
+// ---- wf_fft_ip<LOGN>: in-place decimation-in-frequency (A/B: OWRX_WF_KERNEL=ip) ------------
+// Same product as wf_fft_r16 (|X|^2 of the group's windowed frames summed per bin), with the
+// passes done in place: stage s reads 16 samples of one length-L_s sub-transform (stride
+// S_s = L_s / 16), takes the DFT16, twiddles output q by W_(L_s)^(n q) and writes it back to the
+// addresses it read.  No thread overwrites another's inputs, so a stage needs one barrier (its
+// reads after the previous stage's stores) instead of two, and each wave's stores follow its
+// own DFT without waiting for every wave's reads.  The last stage (radix RL, or the last
+// radix-16 stage when N is a power of 16) reads 16 consecutive samples per thread and leaves the
+// bins in digit-reversed positions; the bin index is recomputed when the partial row goes out
+// (through LDS, coalesced).  With the 1-in-16 padding every stage's reads and stores are free of
+// LDS bank conflicts.  Twiddle bases W_(L_s)^n come from per-stage LDS tables.
+template <int LOGN>
+struct WfIp {
+    static constexpr int N = 1 << LOGN;
+    static constexpr int NT = N / 16;
+    static constexpr int P16 = LOGN / 4;                      // radix-16 stages
+    static constexpr int RL = 1 << (LOGN - 4 * P16);          // last radix (1: none)
+    static constexpr int NS = RL > 1 ? P16 : P16 - 1;         // stages that twiddle and store
+    static constexpr int stride(int s) { return N >> (4 * (s + 1)); }  // S_s
+    static constexpr int tab(int s) {                         // table offset of stage s
+        int o = 0;
+        for (int i = 0; i < s; ++i) o += stride(i);
+        return o;
+    }
+    static constexpr int TW0 = N + N / 16;
+    static constexpr size_t kLds = sizeof(float2) * (TW0 + tab(NS));
+    // The partial row goes through LDS by bin: thread t's bins differ from its neighbours' in
+    // five bin bits (lane bit i moves position bit i + 4, i.e. digit bit kbit(i) of the bin).
+    // The row is stored at k ^ swz(k), swz built from the bits above 4 only, so that those five
+    // bits land on five different bank bits (stores conflict-free) while 32 consecutive bins
+    // still cover all banks (the coalesced read-out conflict-free).
+    static constexpr int kbit(int i) {
+        const int e = i + 4, st = (LOGN - e - 1) / 4;  // stage whose stride S satisfies S <= 2^e < 16 S
+        return 4 * st + e - (LOGN - 4 * st - 4);
+    }
+    static constexpr unsigned swz_vec(int b) {  // XOR vector of bin bit b >= 5 (0: none)
+        unsigned used = 0;
+        for (int i = 0; i < 5; ++i)
+            if (kbit(i) < 5) used |= 1u << kbit(i);
+        for (int i = 0, free_bit = 0; i < 5; ++i) {
+            if (kbit(i) < 5) continue;
+            while (used & (1u << free_bit)) ++free_bit;
+            used |= 1u << free_bit;
+            if (kbit(i) == b) return 1u << free_bit;
+        }
+        return 0;
+    }
+};
+
+template <int LOGN>
+OWRX_DEV int wf_ip_row_addr(int k) {
+    unsigned x = 0;
+#pragma unroll
+    for (int b = 5; b < LOGN; ++b)
+        if (WfIp<LOGN>::swz_vec(b)) x ^= ((k >> b) & 1) ? WfIp<LOGN>::swz_vec(b) : 0u;
+    return k ^ (int)x;
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__(WfIp<LOGN>::NT)
+wf_fft_ip(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+          const float* __restrict__ window, const float2* __restrict__ tw, float* __restrict__ partial) {
+    using K = WfIp<LOGN>;
+    constexpr int N = K::N, NT = K::NT, P16 = K::P16, RL = K::RL, NS = K::NS;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int tid0 = threadIdx.x;
+    const WfGroup g = groups[blockIdx.x];
+    WF_STAMP(0);
+    // frame samples and window taps through buffer descriptors (one VGPR of lane offset), the
+    // first frame requested before the twiddle tables (vmcnt is in order)
+    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
+    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
+    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
+        0x00020000);
+    const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
+                                                      (int)(sizeof(float) * N), 0x00020000);
+    auto load_x = [&](int f, c2* v) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            // two dword loads paired into one dwordx2 (this hipcc's vector-returning
+            // raw_buffer_load_b64 / _b128 builtins load one dword and splat it)
+            const int vo = tid0 * 8 + f * hop * 8;
+            v[r] = c2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
+                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0))};
+        }
+    };
+    c2 nx[16];
+    load_x(0, nx);
+    // twiddle bases: stage 0's W_N^tid stays in a register (each thread uses only its own); the
+    // later stages' tables (N/256 + N/4096 + ... entries) go to LDS, written in frame 0 before the
+    // stage-1 barrier so no load latency is waited for before the first DFT
+    const c2 tw0 = c2_of(tw[tid0]);
+    constexpr int NTAB1 = K::tab(NS) - K::tab(1);  // entries of stages >= 1
+    float2 tw1 = float2{0.0f, 0.0f};
+    int tab_i = 0;
+    if (NTAB1 > 0 && tid0 < NTAB1) {
+        int s = 1, n = tid0;
+        while (s < NS && n >= K::stride(s)) n -= K::stride(s++);
+        tab_i = K::TW0 + K::tab(s) + n;
+        tw1 = tw[n << (4 * s)];
+    }
+    float acc[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
+#pragma unroll 1
+    for (int f = 0; f < nfr; ++f) {
+        int tid = threadIdx.x;  // opaque: keeps the stage addresses inside the frame loop
+        asm volatile("" : "+v"(tid));
+        const int st0 = 1 + 6 * f;
+        WF_STAMP(st0);
+        c2 a[16];
+        {
+            float wv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, tid0 * 4, r * NT * 4, 0));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = nx[r] * wv[r];
+        }
+        WF_STAMP(st0 + 1);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int S = K::stride(s);
+            const int n = tid & (S - 1);
+            const int base = (tid / S) * (16 * S) + n;  // sub-transform start + n
+            if (s > 0) {
+                __syncthreads();  // the previous stage's stores
+#pragma unroll
+                for (int m = 0; m < 16; ++m) a[m] = c2_of(sm[wf_pad(base + m * S)]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            dft_r<16>(a);
+            if (n) twiddle_r<16>(a, s == 0 ? tw0 : c2_of(sm[K::TW0 + K::tab(s) + n]));  // W_(16 S)^(n q)
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) sm[wf_pad(base + q * S)] = f2_of(a[q]);
+            if (s == 0 && f == 0 && NTAB1 > 0 && tid0 < NTAB1) sm[tab_i] = tw1;
+            if (s == 0 && f + 1 < nfr) load_x(f + 1, nx);
+            WF_STAMP(st0 + 2 + s);
+        }
+        __syncthreads();
+        // last stage: 16 consecutive samples per thread
+        if constexpr (RL > 1) {
+#pragma unroll
+            for (int j = 0; j < 16 / RL; ++j) {
+                c2 c[RL];
+#pragma unroll
+                for (int n = 0; n < RL; ++n) c[n] = c2_of(sm[wf_pad(16 * tid + RL * j + n)]);
+                dft_r<RL>(c);
+#pragma unroll
+                for (int q = 0; q < RL; ++q)
+                    acc[j * RL + q] = fmaf(c[q].y, c[q].y, fmaf(c[q].x, c[q].x, acc[j * RL + q]));
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) a[m] = c2_of(sm[wf_pad(16 * tid + m)]);
+            dft_r<16>(a);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[q] = fmaf(a[q].y, a[q].y, fmaf(a[q].x, a[q].x, acc[q]));
+        }
+        WF_STAMP(st0 + 5);
+        __syncthreads();  // LDS reused by the next frame (and by the row below)
+    }
+    // bins: position p = 16 tid + RL j holds, after stage s, digit q_s = (p / S_s) % 16 of the
+    // bin (weight 16^s); the last stage's output q has weight 16^(number of earlier stages)
+    float* rowl = reinterpret_cast<float*>(sm);
+    constexpr int NE = RL > 1 ? P16 : P16 - 1;  // stages before the last
+    constexpr int WL = 1 << (4 * NE);
+#pragma unroll
+    for (int j = 0; j < (RL > 1 ? 16 / RL : 1); ++j) {
+        const int p = 16 * tid0 + (RL > 1 ? RL : 16) * j;
+        int k0 = 0;
+#pragma unroll
+        for (int s = 0; s < NE; ++s) k0 += ((p / K::stride(s)) & 15) << (4 * s);
+        constexpr int Q = RL > 1 ? RL : 16;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) rowl[wf_ip_row_addr<LOGN>(k0 + q * WL)] = acc[j * Q + q];
+    }
+    __syncthreads();
+    float* out = partial + (int64_t)blockIdx.x * N;
+    for (int i = tid0; i < N; i += NT) out[i] = rowl[wf_ip_row_addr<LOGN>(i)];
+    WF_STAMP(13);
 }
 
 // ---- wf_fft_rx<LOGN, R>: the same product with radix-R passes, N/R threads -----------------
@@ -712,6 +922,31 @@ static hipError_t launch_fft_r32(const float2* blk, int64_t blk_start, const WfG
     return hipGetLastError();
 }
 
+template <int LOGN>
+static hipError_t launch_fft_ip(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                int ngroups, const float* window, const float2* tw,
+                                float* partial, hipStream_t st) {
+    using K = WfIp<LOGN>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_ip<LOGN>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(wf_fft_ip<LOGN>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start,
+                       groups, window, tw, partial);
+    return hipGetLastError();
+}
+
+static bool wf_in_place() {  // OWRX_WF_KERNEL=ip: the in-place DIF kernel (A/B)
+    static const bool v = [] {
+        const char* s = getenv("OWRX_WF_KERNEL");
+        return s && strcmp(s, "ip") == 0;
+    }();
+    return v;
+}
+
 static bool wf_radix32() {  // OWRX_WF_KERNEL=r32: the radix-32 kernel (A/B)
     static const bool v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
@@ -772,6 +1007,18 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
+// 1024 <= N <= 16384: the Stockham radix-16 kernel, or an A/B alternative
+// (OWRX_WF_KERNEL=ip | r32 | radix4; DESIGN.md records the measurements)
+template <int LOGN>
+static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                 int ngroups, const float* window, const float2* tw, float* partial,
+                                 hipStream_t st) {
+    if (wf_radix32()) return launch_fft_r32<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+    if (wf_in_place()) return launch_fft_ip<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+    if (wf_radix4_only()) return launch_fft_t<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+    return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+}
+
 // scratch: ngroups * N cf32, used for N > 16384 (groups hold one frame each there)
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, const float* window, const float2* tw, float* partial,
@@ -779,36 +1026,11 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
     switch (logn) {
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 10:
-            if (wf_radix32())
-                return launch_fft_r32<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            if (!wf_radix4_only())
-                return launch_fft_r16<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            return launch_fft_t<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 11:
-            if (wf_radix32())
-                return launch_fft_r32<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            if (!wf_radix4_only())
-                return launch_fft_r16<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            return launch_fft_t<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 12:
-            if (wf_radix32())
-                return launch_fft_r32<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            if (!wf_radix4_only())
-                return launch_fft_r16<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            return launch_fft_t<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 13:
-            if (wf_radix32())
-                return launch_fft_r32<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            if (!wf_radix4_only())
-                return launch_fft_r16<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            return launch_fft_t<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 14:
-            if (wf_radix32())
-                return launch_fft_r32<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            if (!wf_radix4_only())
-                return launch_fft_r16<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-            return launch_fft_t<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 10: return launch_fft_sel<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 11: return launch_fft_sel<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 12: return launch_fft_sel<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 13: return launch_fft_sel<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 14: return launch_fft_sel<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 15: return launch_fft4_t<7, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
                                             scratch, st);
         case 16: return launch_fft4_t<8, 8>(blk, blk_start, groups, ngroups, window, tw, partial,

@@ -186,6 +186,24 @@ def test_waterfall_float_rows(amd, N, fs):
     assert np.max(err) < 2e-3, np.max(err)   # dB; fp32 FFT vs double
 
 
+@pytest.mark.parametrize("variant", ["ip", "r32", "radix4"])
+def test_waterfall_kernel_variants(variant):
+    """The A/B waterfall kernels (OWRX_WF_KERNEL: in-place DIF, radix 32, radix 4) give the
+    oracle's rows at N = 1024 .. 16384 (<= 2e-3 dB, as the production kernel); each runs in a
+    child process since the selection is read once per process."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, OWRX_WF_KERNEL=variant)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "wf_variant_rows.py")], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    errs = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(errs) == 5 and all(e is not None and e < 2e-3 for e in errs.values()), errs
+
+
 def test_waterfall_adpcm_rows_and_block_invariance(amd):
     fs, N = 2400000, 4096
     avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)

@@ -14,18 +14,26 @@ from openwebrx_amd.engine import Engine  # noqa: E402
 
 fs, blk = 10000000, 1 << 22
 sizes = [int(s) for s in sys.argv[1:]] or [8192, 16384]
-x = (torch.randn(blk, dtype=torch.complex64, device="cuda") * 0.1).contiguous()
+# a contiguous recording of 4 blocks: owrx_process_device reads the stream history before the
+# pointer it is handed (include/owrx_amd.h), so blocks start at offsets >= 1 block
+x = (torch.randn(4 * blk, dtype=torch.complex64, device="cuda") * 0.1).contiguous()
+
+
+def ptr(i):
+    return x.data_ptr() + 8 * blk * (1 + i % 3)
+
+
 for n in sizes:
     avg, hop = params.fft_parameters(fs, n, 9, 0.3)
     eng = Engine(fs, max_block=blk)
     wf = eng.waterfall(n, hop, avg, adpcm=False)
-    for _ in range(3):
-        eng.process_device(x.data_ptr(), blk)
+    for i in range(3):
+        eng.process_device(ptr(i), blk)
     eng.sync()
     wf.read_rows()
     t0 = time.time()
     for i in range(30):
-        eng.process_device(x.data_ptr(), blk)
+        eng.process_device(ptr(i), blk)
         if i % 8 == 7:
             eng.sync()
             wf.read_rows()
