@@ -160,6 +160,8 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     period = block / fs
     nblocks = max(1, int(seconds / period))
     lat, joins, leaves = [], [], []
+    tp = ts = tr = 0.0  # host seconds in push (block build + launches), sync, output reads
+    st0 = eng.stats()
     t0 = time.perf_counter()
     for i in range(nblocks):
         wait = t0 + i * period - time.perf_counter()
@@ -167,6 +169,8 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             time.sleep(wait)
         a = time.perf_counter()
         eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
+        b = time.perf_counter()
+        tp += b - a
         if churn and i % 2 == 1 and chains:
             c0 = time.perf_counter()
             chains.pop(i % len(chains)).close()
@@ -175,11 +179,20 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             c2 = time.perf_counter()
             leaves.append(c1 - c0)
             joins.append(c2 - c1)
+        c = time.perf_counter()
         eng.sync()
+        d = time.perf_counter()
         eng.read_chains(chains)
         wf.read()
-        lat.append(time.perf_counter() - a)
+        e = time.perf_counter()
+        ts += d - c
+        tr += e - d
+        lat.append(e - a)
     st = eng.stats()
+    host = {"push_ms": round(1e3 * tp / nblocks, 3), "sync_ms": round(1e3 * ts / nblocks, 3),
+            "read_ms": round(1e3 * tr / nblocks, 3)}
+    for k in ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots", "host_ms_wait_rows"):
+        host[k] = round((st[k] - st0[k]) / nblocks, 3)
     eng.close()
     extra = {}
     if joins:
@@ -193,6 +206,7 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             "max_block_latency_ms": round(1e3 * max(lat), 3),
             "mean_block_latency_ms": round(1e3 * sum(lat) / len(lat), 3),
             "overruns": int(st["overruns"]),
+            "host_per_block": host,
             "keeps_up": bool(st["overruns"] == 0 and max(lat) < period),
             "path": "host cf32 -> owrx_push_iq (PCIe) -> engine, sync + drain per block"}
 
@@ -222,7 +236,8 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
         _log("  setup %.2f s, keeps_up %s, max block latency %.2f ms"
              % (r["setup_s"], r["keeps_up"], r["max_block_latency_ms"]))
         levels.append({k: r[k] for k in ("chains", "keeps_up", "max_block_latency_ms",
-                                         "mean_block_latency_ms", "overruns", "setup_s")})
+                                         "mean_block_latency_ms", "overruns", "setup_s",
+                                         "host_per_block")})
         if not r["keeps_up"]:
             break
         best = C

@@ -20,6 +20,7 @@
 #include <chrono>
 #include <cmath>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -420,6 +421,11 @@ struct owrx_engine {
     // R: waterfall row encoding + copies.  Four streams = the four hardware queues HIP gives a
     // process (GPU_MAX_HW_QUEUES), so no two of them serialise on a shared queue.
     hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sR = nullptr;
+    // unmasked twins of B and C: past kWideSerialChains chains the serial kernels are
+    // throughput-bound on their few CUs and spread over the chip instead (serial_wide)
+    hipStream_t sBw = nullptr, sCw = nullptr;
+    bool serial_wide = false;
+    std::vector<int> sel_buckets[3][2][4];  // per-block scratch of the serial lane lists
     double samp_rate = 0;
     int64_t max_block = 0;
     int cus_a = 0;  // CUs of stream A (DDC launch shape)
@@ -440,7 +446,9 @@ struct owrx_engine {
     hipEvent_t evIn = nullptr;  // end of the last block's stream-A work (input reusable)
     bool in_pending = false;
     std::map<int, std::unique_ptr<Waterfall>> wfs;
-    std::map<int, std::unique_ptr<Chain>> chains;
+    // hashed: the per-block loops and the batched reads look every chain up (a tree of 65 536
+    // chains costs ~16 cache misses per lookup)
+    std::unordered_map<int, std::unique_ptr<Chain>> chains;
     std::vector<std::unique_ptr<ChainGroup>> groups;
     int next_handle = 1;
     // post staging (all chains), per block parity
@@ -965,6 +973,18 @@ static double now_ms() {
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Chains per block above which the serial kernels (post_serial_front, chain_nr, chain_adpcm) run
+// on unmasked streams: one lane per chain, so 1 024 chains are 16 waves = one per SIMD of
+// stream B's / C's 4 CUs; beyond that those CUs time-slice while the rest of the chip waits.
+// OWRX_WIDE_SERIAL_CHAINS overrides (A/B; a huge value keeps the masked streams).
+static int wide_serial_chains() {
+    static const int v = [] {
+        const char* s = getenv("OWRX_WIDE_SERIAL_CHAINS");
+        return s ? atoi(s) : 1024;
+    }();
+    return v;
+}
+
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const double t_enter = now_ms();
     // the previous block's stream-A work must be done before its input / descriptors are
@@ -1131,10 +1151,12 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             p.deemph_beta = 1.0f - p.deemph_alpha;
             if (q.nr_enabled && c->d_nr_state && q.output != OWRX_OUT_IQ) {
                 if (c->nr_reset) {  // a fresh NoiseFilter (ClientAudioChain._updateConverter)
-                    HIPCHK(hipMemsetAsync(c->d_nr_state, 0, sizeof(NrState), e->sB));
-                    HIPCHK(hipMemsetAsync(c->d_nr_in, 0, sizeof(float) * kNrHop, e->sB));
-                    HIPCHK(hipMemsetAsync(c->d_nr_pow, 0, sizeof(float) * 2 * (kNrN / 2 + 1), e->sB));
-                    HIPCHK(hipMemsetAsync(c->d_nr_ola, 0, sizeof(float) * kNrHop, e->sB));
+                    // on the serial stream in use (a switch orders the other one behind it)
+                    hipStream_t sb = e->serial_wide ? e->sBw : e->sB;
+                    HIPCHK(hipMemsetAsync(c->d_nr_state, 0, sizeof(NrState), sb));
+                    HIPCHK(hipMemsetAsync(c->d_nr_in, 0, sizeof(float) * kNrHop, sb));
+                    HIPCHK(hipMemsetAsync(c->d_nr_pow, 0, sizeof(float) * 2 * (kNrN / 2 + 1), sb));
+                    HIPCHK(hipMemsetAsync(c->d_nr_ola, 0, sizeof(float) * kNrHop, sb));
                     c->nr_reset = false;
                 }
                 p.nr_enabled = 1;
@@ -1240,7 +1262,24 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         for (int lg = 0; lg < 32; ++lg)
             if (sf_sizes & (1u << lg)) HIPCHK(launch_chain_sfft(lg, S.d_posts, np, S.d_counts, e->sA));
         HIPCHK(hipEventRecord(S.evA, e->sA));
-        HIPCHK(hipStreamWaitEvent(e->sB, S.evA, 0));
+        // serial streams for this block: the CU-masked pair, or past kWideSerialChains chains
+        // (more waves than their CUs hold) the unmasked pair; on a switch the new pair first
+        // waits for the old pair's last block, so every chain's state stays in block order
+        const bool wide = np > wide_serial_chains();
+        hipStream_t sB = wide ? e->sBw : e->sB, sC = wide ? e->sCw : e->sC;
+        if (wide != e->serial_wide) {
+            hipEvent_t fb, fc;
+            HIPCHK(hipEventCreateWithFlags(&fb, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&fc, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(fb, e->serial_wide ? e->sBw : e->sB));
+            HIPCHK(hipEventRecord(fc, e->serial_wide ? e->sCw : e->sC));
+            HIPCHK(hipStreamWaitEvent(sB, fb, 0));
+            HIPCHK(hipStreamWaitEvent(sC, fc, 0));
+            HIPCHK(hipEventDestroy(fb));  // released once the waits are satisfied
+            HIPCHK(hipEventDestroy(fc));
+            e->serial_wide = wide;
+        }
+        HIPCHK(hipStreamWaitEvent(sB, S.evA, 0));
         // one post_serial_front launch per output format present (S16 / ADPCM / F32); within
         // a format the chains are ordered by demodulator and every demodulator's run is padded
         // to whole 64-lane workgroups (-1 = idle lane), so each wave has a uniform demodulator
@@ -1248,40 +1287,44 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         // instead of converting; the two ADPCM lists are adjacent (one chain_adpcm launch)
         int nsel[3][2] = {}, off[3][2] = {};
         int nfill = 0;
-        for (int o = 0; o < 3; ++o)
-            for (int nr = 0; nr < 2; ++nr) {
-                off[o][nr] = nfill;
-                for (int dm = 0; dm < 4; ++dm) {
-                    int run = 0;
-                    for (int i = 0; i < np; ++i)
-                        if (e->posts[i].output == o && e->posts[i].demod == dm &&
-                            (e->posts[i].nr_enabled != 0) == (nr != 0)) {
-                            S.h_sel[nfill++] = i;
-                            run++;
-                        }
-                    while (run % 64) {
-                        S.h_sel[nfill++] = -1;
-                        run++;
-                    }
-                }
-                nsel[o][nr] = nfill - off[o][nr];
+        {
+            // one pass: bucket the posts by (output, NoiseFilter, demodulator), in index order
+            std::vector<int>(&bk)[3][2][4] = e->sel_buckets;
+            for (auto& a : bk)
+                for (auto& b : a)
+                    for (auto& v : b) v.clear();
+            for (int i = 0; i < np; ++i) {
+                const ChainPost& p = e->posts[i];
+                if (p.output >= 0 && p.output < 3 && p.demod >= 0 && p.demod < 4)
+                    bk[p.output][p.nr_enabled != 0][p.demod].push_back(i);
             }
-        HIPCHK(kcopy(S.d_sel, S.h_sel, sizeof(int) * nfill, e->sB));
+            for (int o = 0; o < 3; ++o)
+                for (int nr = 0; nr < 2; ++nr) {
+                    off[o][nr] = nfill;
+                    for (int dm = 0; dm < 4; ++dm) {
+                        const std::vector<int>& v = bk[o][nr][dm];
+                        for (int i : v) S.h_sel[nfill++] = i;
+                        for (size_t run = v.size(); run % 64; ++run) S.h_sel[nfill++] = -1;
+                    }
+                    nsel[o][nr] = nfill - off[o][nr];
+                }
+        }
+        HIPCHK(kcopy(S.d_sel, S.h_sel, sizeof(int) * nfill, sB));
         const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
         for (int o = 0; o < 3; ++o)
             for (int nr = 0; nr < 2; ++nr)
                 HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o][nr],
-                                          nsel[o][nr], o, dbg, nr, e->sB));
-        if (any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, e->sB));
-        HIPCHK(hipEventRecord(S.evF, e->sB));
+                                          nsel[o][nr], o, dbg, nr, sB));
+        if (any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, sB));
+        HIPCHK(hipEventRecord(S.evF, sB));
         // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host
-        HIPCHK(hipStreamWaitEvent(e->sC, S.evF, 0));
+        HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
         HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + off[1][0],
-                                  nsel[1][0] + nsel[1][1], e->sC));
-        if (timed) HIPCHK(hipEventRecord(S.b1, e->sC));
+                                  nsel[1][0] + nsel[1][1], sC));
+        if (timed) HIPCHK(hipEventRecord(S.b1, sC));
         // the copies to host go on stream R (behind this block's encoder), so stream C runs
         // encoders back to back: its kernel is the pipeline's longest serial stage
-        HIPCHK(hipEventRecord(S.evC, e->sC));
+        HIPCHK(hipEventRecord(S.evC, sC));
         HIPCHK(hipStreamWaitEvent(e->sR, S.evC, 0));
         hipLaunchKernelGGL(gather_outputs, dim3(np), dim3(256), 0, e->sR, S.d_posts, S.d_counts,
                            S.d_out, S.h_out, S.d_sm, S.h_sm, (int)e->sm_stride, S.h_counts);
@@ -1356,6 +1399,10 @@ static hipError_t create_streams(owrx_engine* e) {
     int ncu = 0;
     hipError_t err = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device);
     if (err != hipSuccess) return err;
+    for (hipStream_t* st : {&e->sBw, &e->sCw}) {
+        err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+        if (err != hipSuccess) return err;
+    }
     // R (8 CUs) holds the output gathers and the waterfall row encoders: one stream per row
     // slot, so the rows of consecutive blocks (independent: FftAdpcm restarts every row)
     // encode concurrently instead of queueing behind each other
@@ -1457,7 +1504,7 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
 int owrx_engine_destroy(owrx_engine* e) {
     if (!e) return OWRX_EINVAL;
     hipSetDevice(e->device);
-    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR})
+    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamSynchronize(st);
     for (auto& r : e->rslots)
         if (r.stream) hipStreamSynchronize(r.stream);
@@ -1492,7 +1539,7 @@ int owrx_engine_destroy(owrx_engine* e) {
         if (r.evC) hipEventDestroy(r.evC);
         if (r.stream) hipStreamDestroy(r.stream);
     }
-    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR})
+    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamDestroy(st);
     delete e;
     return OWRX_OK;
@@ -1925,8 +1972,7 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     RC_FAIL(e, drain_all(e));
-    HIPCHK(hipStreamSynchronize(e->sB));
-    HIPCHK(hipStreamSynchronize(e->sC));
+    for (hipStream_t st : {e->sB, e->sC, e->sBw, e->sCw}) HIPCHK(hipStreamSynchronize(st));
     ChainGroup* g = it->second->group;
     // swap-remove: the last member takes the slot (and its filter spectra move with it)
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());

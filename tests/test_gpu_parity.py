@@ -204,6 +204,27 @@ def test_waterfall_kernel_variants(variant):
     assert len(errs) == 5 and all(e is not None and e < 2e-3 for e in errs.values()), errs
 
 
+def test_wide_serial_streams_same_audio():
+    """Past OWRX_WIDE_SERIAL_CHAINS chains the serial kernels move from the CU-masked streams to
+    unmasked ones (engine.hip process_block); a stream whose chain count crosses the threshold
+    up and down (3 -> 8 -> 3 chains, threshold 4) gives every chain the same audio and s-meter
+    bytes as with the masked streams only (threshold out of reach)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = []
+    for thr in ("1000000000", "4"):
+        env = dict(os.environ, OWRX_WIDE_SERIAL_CHAINS=thr)
+        r = subprocess.run([sys.executable, os.path.join(here, "serial_wide_run.py")], env=env,
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert len(res[0]) == 8 and all(v[2] > 1000 for v in res[0].values()), res[0]
+    assert res[0] == res[1]
+
+
 def test_waterfall_adpcm_rows_and_block_invariance(amd):
     fs, N = 2400000, 4096
     avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
