@@ -269,8 +269,13 @@ fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs,
             }
         }
     };
+    // the prologue issues the two groups in the loop's order (ua0's loads the older): the
+    // wait-count pass merges the loop header's entry and back-edge states, and with ua1's
+    // loads scheduled first here it made every block wait for the next block's operands too
     load(ua0, wa0, 0);
+    __builtin_amdgcn_sched_barrier(0);
     load(ua1, wa1, 1);
+    __builtin_amdgcn_sched_barrier(0);
     for (int kb = 0; kb < nkb; kb += 3) {
         load(ua2, wa2, kb + 2);
         __builtin_amdgcn_sched_barrier(0);  // issue the loads before this block's MFMAs
