@@ -17,7 +17,7 @@ def main(ROOT, REF):
     import openwebrx_amd.pycsdr as shim
     shim.install()
     sys.path.append(REF)
-    from csdr.chain.analog import NFm, Am, Ssb, WFm, SAm
+    from csdr.chain.analog import NFm, Am, Ssb, WFm, SAm, RawSAm
     from csdr.chain.demodulator import SecondaryDemodulator, SecondarySelectorChain, ServiceDemodulator
     from owrx.service.chain import ServiceDemodulatorChain
     from csdr.module import ThreadModule
@@ -98,7 +98,7 @@ def main(ROOT, REF):
                   "length", "decimation", "hang_length", "flush_length", "report_interval",
                   "level", "size", "every_n_samples", "avg_number", "add_db", "fft_size",
                   "max_amplitude", "sample_rate", "tau", "prefilter", "threshold", "sync",
-                  "initial_gain", "max_gain", "update_period", "sample_period"):
+                  "initial_gain", "max_gain", "update_period", "sample_period", "gain"):
             if hasattr(mod, k):
                 v = getattr(mod, k)
                 d[k] = v if isinstance(v, (int, float, bool, type(None))) else str(v)
@@ -194,6 +194,11 @@ def main(ROOT, REF):
     chain.setDemodulator(SAm())
     chain.setBandpass(-4700, 4700)
     record("sam", chain, wide)
+    # raw synchronous AM, HD audio (csdr/chain/analog.py:156-167): the Selector runs at the
+    # client's hd rate (48 kHz here, owrx/dsp.py:150-166) into Afc(50, 8) -> RealPart ->
+    # DcBlock -> Gain(100)
+    chain.setDemodulator(RawSAm(48000))
+    record("rawsam", chain, wide)
     _graph.finish(wide)
 
     # background services (owrx/service/__init__.py): ServiceDemodulatorChain on a service

@@ -36,6 +36,8 @@ def _make(d):
         return M.Limit(d["max_amplitude"])
     if c == "Afc":
         return M.Afc(d["update_period"], d["sample_period"])
+    if c == "Gain":
+        return M.Gain(Format[d["format"]], d["gain"])
     if c == "NfmDeemphasis":
         return M.NfmDeemphasis(d["sample_rate"])
     if c == "WfmDeemphasis":

@@ -166,18 +166,20 @@ def test_service_demodulator_chain_replay(step):
 
 
 @pytest.mark.gpu
-def test_sam_chain_replay():
-    """SAm (csdr/chain/analog.py:141-154) on the reference's ClientDemodulatorChain
-    (tests/golden/dsp_graph.json "sam"): the fused Selector writes its output into the buffer
-    the standalone GPU Afc reads (OWRX_OUT_SEL); Afc -> RealPart -> DcBlock -> Agc(Slow, initial
-    gain 200) run as GPU modules.  The Selector output equals the oracle's squelch stage and
+@pytest.mark.parametrize("step", ["sam", "rawsam"])
+def test_sam_chain_replay(step):
+    """SAm / RawSAm (csdr/chain/analog.py:141-167) on the reference's ClientDemodulatorChain
+    (tests/golden/dsp_graph.json "sam", "rawsam"): the fused Selector (12 kHz; RawSAm at the
+    48 kHz hd rate) writes its output into the buffer the standalone GPU Afc reads
+    (OWRX_OUT_SEL); Afc -> RealPart -> DcBlock -> Agc(Slow, initial gain 200) / Gain(100) run as
+    GPU modules.  The Selector output equals the oracle's squelch stage and
     the Agc output the oracle's afc -> realpart -> dcblock -> agc of it, <=1e-5 rel-RMS; end to
     end the bound adds the oracle's own sensitivity to the Selector difference (Afc parity
     unpinned: csdr's Afc is not in the reference)."""
     import oracle
     from openwebrx_amd import _lib
     from openwebrx_amd.pycsdr import _graph
-    s = dsp_replay.steps()["sam"]
+    s = dsp_replay.steps()[step]
     fs = 10000000
     n = 8 * (1 << 20)
     rng = np.random.default_rng(5)
@@ -188,7 +190,8 @@ def test_sam_chain_replay():
     wide, mods, outs, power = dsp_replay.build(s)
     cls = [d["class"] for _, d, _ in s["graph"]]
     sel = _collect(outs[cls.index("Squelch")])
-    agc = _collect(outs[cls.index("Agc")])
+    last = "Agc" if "Agc" in cls else "Gain"
+    agc = _collect(outs[cls.index(last)])
     for i in range(0, iq.size, 100003):
         wide.write(iq[i:i + 100003].tobytes())
     drv = _graph._drivers.get(id(wide))
@@ -215,9 +218,12 @@ def test_sam_chain_replay():
     assert rel_rms(tap, ref) < 1e-5
     got = np.frombuffer(b"".join(agc[2]), np.float32)
     d = {dd["class"]: dd for _, dd, _ in s["graph"]}
-    ap = oracle.agc_params(_lib.AGC_SLOW, d["Agc"]["initial_gain"])
-    chain = lambda z: oracle.agc(oracle.dcblock(oracle.realpart(
-        oracle.afc(z, d["Afc"]["update_period"], d["Afc"]["sample_period"]))), ap)
+    def chain(z):
+        y = oracle.dcblock(oracle.realpart(
+            oracle.afc(z, d["Afc"]["update_period"], d["Afc"]["sample_period"])))
+        if last == "Agc":
+            return oracle.agc(y, oracle.agc_params(_lib.AGC_SLOW, d["Agc"]["initial_gain"]))
+        return oracle.gain(y, d["Gain"]["gain"])
     assert got.size == tap.size, (got.size, tap.size)
     assert rel_rms(got, chain(tap)) < 1e-5        # the module chain on the engine's output
     # end to end from the oracle's squelch stage: Afc's frequency loop integrates the Selector's

@@ -107,7 +107,20 @@ def test_sam_keeps_the_selector_fused_and_runs_afc_on_the_gpu():
     assert (afc["update_period"], afc["sample_period"]) == (10, 4)
 
 
-@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio", "sam"])
+def test_rawsam_runs_the_selector_at_the_hd_rate():
+    """RawSAm (csdr/chain/analog.py:156-167) is HdAudio: ClientDemodulatorChain runs its
+    Selector at the hd output rate (48 kHz, owrx/dsp.py:150-166); still fused, its output
+    (OWRX_OUT_SEL) feeding Afc(50, 8) -> RealPart -> DcBlock -> Gain(100) on the GPU."""
+    s = dsp_replay.steps()["rawsam"]
+    assert s["fused"] and s["params"]["output"] == 4 and s["params"]["decimation"] == 208
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    assert cls.index("Squelch") < cls.index("Afc") < cls.index("RealPart") < cls.index("Gain")
+    g = {d["class"]: d for _, d, _ in s["graph"]}
+    assert (g["Afc"]["update_period"], g["Afc"]["sample_period"]) == (50, 8)
+    assert g["Gain"]["gain"] == 100.0
+
+
+@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio", "sam", "rawsam"])
 def test_replayed_graph_plans_like_the_reference(step):
     """The shim-built replay of each recorded graph is planned exactly as the reference's."""
     from openwebrx_amd.pycsdr import _graph
