@@ -235,6 +235,32 @@ def plan_segment(head):
     bp = take(M.Bandpass)
     sq = take(M.Squelch)
     selector_last = mods[i - 1]
+    sel_end = i
+
+    def _selector_output():
+        """Selector output read by something the engine does not fuse (an IQ-input decoder:
+        ServiceDemodulatorChain with Selector(withSquelch=False), owrx/service/chain.py:7-23;
+        SAm's Afc; a demodulator without Agc): the engine emits the cf32 Selector output itself
+        and whatever reads it runs as standalone modules."""
+        if selector_last.writer is None or selector_last is fir:
+            return None
+        p = dict(shift_rate=shift.rate, decimation=fir.decimation, transition=fir.transition,
+                 cutoff=fir.cutoff, frac_rate=frac.rate if frac is not None else 1.0,
+                 bandpass=0, bp_low=0.0, bp_high=0.0, bp_transition=0.0,
+                 sq_length=750, sq_decimation=5, sq_hang=0, sq_flush=0, sq_report=0,
+                 sq_level=0.0, demod=_lib.DEMOD_SSB, agc_profile=0, agc_initial_gain=-1.0,
+                 agc_max_gain=-1.0, audio_rate=12000, output=_lib.OUT_SEL, power_writer=None,
+                 tap_selector=None, tap_audio=None, secondary_fft=None, secondary_modules=[],
+                 secondary_writer=None)
+        if bp is not None and bp.low_cut is not None and bp.high_cut is not None:
+            p.update(bandpass=1, bp_low=bp.low_cut, bp_high=bp.high_cut,
+                     bp_transition=bp.transition)
+        if sq is not None:
+            p.update(sq_length=sq.length, sq_decimation=sq.decimation, sq_hang=sq.hang_length,
+                     sq_flush=sq.flush_length, sq_report=sq.report_interval, sq_level=sq.level,
+                     power_writer=sq.power_writer)
+        return ("chain", p, mods[:sel_end])
+
     fm = take(M.FmDemod)
     wfm = None
     if fm is not None:
@@ -253,35 +279,17 @@ def plan_segment(head):
             wfm = dict(if_rate=fdf.rate * wde.sample_rate, deemph_tau=wde.tau)
     elif take(M.AmDemod) is not None:
         if take(M.DcBlock) is None:
-            return None
+            return _selector_output()
         demod, audio_rate = _lib.DEMOD_AM, 12000
     elif take(M.RealPart) is not None:
         demod, audio_rate = _lib.DEMOD_SSB, 12000
-    elif selector_last.writer is not None and selector_last is not fir:
-        # Selector output read by something the engine does not fuse (an IQ-input decoder:
-        # ServiceDemodulatorChain with Selector(withSquelch=False), owrx/service/chain.py:7-23):
-        # the engine emits the cf32 Selector output itself
-        p = dict(shift_rate=shift.rate, decimation=fir.decimation, transition=fir.transition,
-                 cutoff=fir.cutoff, frac_rate=frac.rate if frac is not None else 1.0,
-                 bandpass=0, bp_low=0.0, bp_high=0.0, bp_transition=0.0,
-                 sq_length=750, sq_decimation=5, sq_hang=0, sq_flush=0, sq_report=0,
-                 sq_level=0.0, demod=_lib.DEMOD_SSB, agc_profile=0, agc_initial_gain=-1.0,
-                 agc_max_gain=-1.0, audio_rate=12000, output=_lib.OUT_SEL, power_writer=None,
-                 tap_selector=None, tap_audio=None, secondary_fft=None, secondary_modules=[],
-                 secondary_writer=None)
-        if bp is not None and bp.low_cut is not None and bp.high_cut is not None:
-            p.update(bandpass=1, bp_low=bp.low_cut, bp_high=bp.high_cut,
-                     bp_transition=bp.transition)
-        if sq is not None:
-            p.update(sq_length=sq.length, sq_decimation=sq.decimation, sq_hang=sq.hang_length,
-                     sq_flush=sq.flush_length, sq_report=sq.report_interval, sq_level=sq.level,
-                     power_writer=sq.power_writer)
-        return ("chain", p, mods[:i])
     else:
-        return None
+        return _selector_output()
     agc = take(M.Agc) if wfm is None else None
     if agc is None and wfm is None:
-        return None
+        # a demodulator without Agc (RawAm: AmDemod -> DcBlock -> Gain(100),
+        # csdr/chain/analog.py:23-31): the Selector stays fused, the rest runs as GPU modules
+        return _selector_output()
     demod_last = mods[i - 1]  # writes audioBuffer (ClientDemodulatorChain._connect, dsp.py:86-92)
     nr = take(M.NoiseFilter)
     output = _lib.OUT_F32

@@ -17,7 +17,7 @@ def main(ROOT, REF):
     import openwebrx_amd.pycsdr as shim
     shim.install()
     sys.path.append(REF)
-    from csdr.chain.analog import NFm, Am, Ssb, WFm, SAm, RawSAm
+    from csdr.chain.analog import NFm, Am, Ssb, WFm, SAm, RawSAm, RawAm, SsbDigital
     from csdr.chain.demodulator import SecondaryDemodulator, SecondarySelectorChain, ServiceDemodulator
     from owrx.service.chain import ServiceDemodulatorChain
     from csdr.module import ThreadModule
@@ -199,6 +199,14 @@ def main(ROOT, REF):
     # DcBlock -> Gain(100)
     chain.setDemodulator(RawSAm(48000))
     record("rawsam", chain, wide)
+    # raw AM, HD audio (csdr/chain/analog.py:23-31): AmDemod -> DcBlock -> Gain(100), no Agc
+    chain.setDemodulator(RawAm(48000))
+    record("rawam", chain, wide)
+    # SsbDigital (FixedAudioRateChain + HdAudio, csdr/chain/analog.py:169-181): RealPart ->
+    # Agc(Slow) with the Selector at its fixed 48 kHz audio rate
+    chain.setDemodulator(SsbDigital(48000))
+    chain.setBandpass(150, 3000)
+    record("ssbdigital", chain, wide)
     _graph.finish(wide)
 
     # background services (owrx/service/__init__.py): ServiceDemodulatorChain on a service

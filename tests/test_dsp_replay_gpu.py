@@ -166,13 +166,13 @@ def test_service_demodulator_chain_replay(step):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("step", ["sam", "rawsam"])
+@pytest.mark.parametrize("step", ["sam", "rawsam", "rawam"])
 def test_sam_chain_replay(step):
-    """SAm / RawSAm (csdr/chain/analog.py:141-167) on the reference's ClientDemodulatorChain
-    (tests/golden/dsp_graph.json "sam", "rawsam"): the fused Selector (12 kHz; RawSAm at the
-    48 kHz hd rate) writes its output into the buffer the standalone GPU Afc reads
-    (OWRX_OUT_SEL); Afc -> RealPart -> DcBlock -> Agc(Slow, initial gain 200) / Gain(100) run as
-    GPU modules.  The Selector output equals the oracle's squelch stage and
+    """SAm / RawSAm / RawAm (csdr/chain/analog.py:23-31, 141-167) on the reference's
+    ClientDemodulatorChain (tests/golden/dsp_graph.json "sam", "rawsam", "rawam"): the fused
+    Selector (12 kHz; the Raw* chains at the 48 kHz hd rate) writes its output into the buffer
+    the standalone GPU modules read (OWRX_OUT_SEL); Afc -> RealPart -> DcBlock -> Agc(Slow,
+    initial gain 200) / Gain(100), or AmDemod -> DcBlock -> Gain(100), run as GPU modules.  The Selector output equals the oracle's squelch stage and
     the Agc output the oracle's afc -> realpart -> dcblock -> agc of it, <=1e-5 rel-RMS; end to
     end the bound adds the oracle's own sensitivity to the Selector difference (Afc parity
     unpinned: csdr's Afc is not in the reference)."""
@@ -219,6 +219,8 @@ def test_sam_chain_replay(step):
     got = np.frombuffer(b"".join(agc[2]), np.float32)
     d = {dd["class"]: dd for _, dd, _ in s["graph"]}
     def chain(z):
+        if "AmDemod" in d:  # RawAm: AmDemod -> DcBlock -> Gain(100)
+            return oracle.gain(oracle.dcblock(oracle.amdemod(z)), d["Gain"]["gain"])
         y = oracle.dcblock(oracle.realpart(
             oracle.afc(z, d["Afc"]["update_period"], d["Afc"]["sample_period"])))
         if last == "Agc":

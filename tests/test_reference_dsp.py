@@ -120,7 +120,23 @@ def test_rawsam_runs_the_selector_at_the_hd_rate():
     assert g["Gain"]["gain"] == 100.0
 
 
-@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio", "sam", "rawsam"])
+def test_rawam_and_ssbdigital_plan():
+    """RawAm (csdr/chain/analog.py:23-31: AmDemod -> DcBlock -> Gain(100), no Agc) keeps the
+    Selector fused (OWRX_OUT_SEL) and runs its demodulator as GPU modules; SsbDigital
+    (FixedAudioRateChain + HdAudio, :169-181) fuses whole as RealPart + Agc(Slow) with the
+    Selector at its fixed 48 kHz rate (D = 208)."""
+    s = dsp_replay.steps()["rawam"]
+    assert s["fused"] and s["params"]["output"] == 4 and s["params"]["decimation"] == 208
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    assert cls.index("Squelch") < cls.index("AmDemod") < cls.index("DcBlock") < cls.index("Gain")
+    s = dsp_replay.steps()["ssbdigital"]
+    assert s["fused"] and s["kind"] == "chain"
+    assert s["params"]["demod"] == 2 and s["params"]["decimation"] == 208
+    assert s["params"]["agc_profile"] == 1 and s["params"]["output"] == 1  # SLOW, ADPCM
+
+
+@pytest.mark.parametrize("step", sorted(MODES) + ["service_iq", "service_audio", "sam", "rawsam",
+                                  "rawam", "ssbdigital"])
 def test_replayed_graph_plans_like_the_reference(step):
     """The shim-built replay of each recorded graph is planned exactly as the reference's."""
     from openwebrx_amd.pycsdr import _graph
