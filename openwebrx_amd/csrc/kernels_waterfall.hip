@@ -459,6 +459,147 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     WF_STAMP(13);
 }
 
+// ---- wf_fft_wl: N = 16384 as 16 x 1024 with wave-local sub-transforms (production, C2/C3) --
+// Same product as wf_fft_r16.  Only the first radix-16 pass is a workgroup step: thread t
+// (1024 threads) takes x[t + 1024 r] from HBM (times the window), DFT16 over r, twiddles by
+// W_N^(t k1) and stores Y[k1][t] into region k1 of LDS; one barrier.  Region k1 is then one
+// independent 1024-point DFT (X[k1 + 16 k2] = sum_t Y[k1][t] W_1024^(t k2)), done by wave k1
+// alone: t = l + 64 r (DFT16 over r, twiddle W_1024^(l j1)), l = s + 4 m (DFT16 over m, twiddle
+// W_64^(s j2a)), DFT4 over s, with k2 = j1 + 16 j2a + 256 j2b.  Its two exchanges go through the
+// wave's own region, ordered by the in-order LDS queue of one wave (no workgroup barrier), so
+// sixteen waves interleave one's LDS traffic with another's butterflies instead of the whole
+// workgroup alternating VALU and LDS phases between barriers.  One more barrier per frame
+// before the next frame's first-pass stores reuse the regions.  All twiddles are powers of
+// W_N^t, t < 1024 (an LDS table behind the regions).
+struct WfWl {
+    static constexpr int LOGN = 14, N = 1 << LOGN, NT = 1024;
+    static constexpr int PT = 68;                  // exchange 1 row pitch: T[j1][l], 64 + 4
+    static constexpr int PJ = 17;                  // exchange 2: U[s][j2a][j1] at s PU + j2a PJ + j1
+    static constexpr int PU = 16 * PJ;
+    static constexpr int REG = 16 * PT;            // region of one wave (>= 1024, >= 4 PU)
+    static constexpr int TW0 = 16 * REG;
+    static constexpr size_t kLds = sizeof(float2) * (TW0 + NT);
+    static_assert(REG >= 1024 && REG >= 4 * PU, "region");
+};
+
+OWRX_DEV void wl_wave_fence() {  // order one wave's LDS accesses across lanes (in-order queue)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(WfWl::NT)
+wf_fft_wl(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+          const float* __restrict__ window, const float2* __restrict__ tw,
+          float* __restrict__ partial) {
+    using K = WfWl;
+    constexpr int N = K::N, NT = K::NT;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int tid0 = threadIdx.x;
+    const WfGroup g = groups[blockIdx.x];
+    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
+    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
+    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
+        0x00020000);
+    const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
+                                                      (int)(sizeof(float) * N), 0x00020000);
+    auto load_x = [&](int f, c2* v) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int vo = tid0 * 8 + f * hop * 8;
+            v[r] = c2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
+                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0))};
+        }
+    };
+    c2 nx[16];
+    load_x(0, nx);
+    sm[K::TW0 + tid0] = tw[tid0];  // W_N^t, t < 1024
+    const int wave = tid0 >> 6, lane = tid0 & 63;
+    float acc[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
+    __syncthreads();
+#pragma unroll 1
+    for (int f = 0; f < nfr; ++f) {
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        c2 a[16];
+        {   // pass 0 (workgroup): windowed samples, DFT16 over r, twiddle W_N^(t k1), Y[k1][t]
+            float wv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, tid0 * 4, r * NT * 4, 0));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = nx[r] * wv[r];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        dft_r<16>(a);
+        if (tid) twiddle_r<16>(a, c2_of(sm[K::TW0 + tid]));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) sm[k1 * K::REG + tid] = f2_of(a[k1]);
+        if (f + 1 < nfr) load_x(f + 1, nx);
+        __syncthreads();
+        // wave-local 1024-point DFT of region `wave`
+        float2* R = sm + wave * K::REG;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = c2_of(R[ln + 64 * r]);
+        __builtin_amdgcn_sched_barrier(0);
+        dft_r<16>(a);
+        if (ln) twiddle_r<16>(a, c2_of(sm[K::TW0 + 16 * ln]));  // W_1024^(l j1)
+        __builtin_amdgcn_sched_barrier(0);
+        wl_wave_fence();  // every lane's reads of Y before the region is rewritten
+#pragma unroll
+        for (int j1 = 0; j1 < 16; ++j1) R[j1 * K::PT + ln] = f2_of(a[j1]);
+        wl_wave_fence();
+        const int j1 = ln & 15, s = ln >> 4;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) a[m] = c2_of(R[j1 * K::PT + s + 4 * m]);
+        __builtin_amdgcn_sched_barrier(0);
+        dft_r<16>(a);
+        if (s) twiddle_r<16>(a, c2_of(sm[K::TW0 + 256 * s]));  // W_64^(s j2a)
+        __builtin_amdgcn_sched_barrier(0);
+        wl_wave_fence();
+#pragma unroll
+        for (int j2a = 0; j2a < 16; ++j2a) R[s * K::PU + j2a * K::PJ + j1] = f2_of(a[j2a]);
+        wl_wave_fence();
+        // lane (j1, gq = s): DFT4 over s of (j1, j2a = 4 gq + u), u < 4
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j2a = 4 * s + u;
+            c2 c[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) c[q] = c2_of(R[q * K::PU + j2a * K::PJ + j1]);
+            dft4(c[0], c[1], c[2], c[3]);
+#pragma unroll
+            for (int j2b = 0; j2b < 4; ++j2b)
+                acc[4 * u + j2b] = fmaf(c[j2b].y, c[j2b].y, fmaf(c[j2b].x, c[j2b].x, acc[4 * u + j2b]));
+        }
+        __syncthreads();  // regions reused by the next frame's first pass
+    }
+    // bin of acc[4 u + j2b]: k = wave + 16 j1 + 256 (4 gq + u) + 4096 j2b; the row goes out
+    // through LDS in bin order (k + k/16 + k/1024 spreads one store's lanes over the banks) so
+    // that the partial row is written with coalesced stores
+    float* rowl = reinterpret_cast<float*>(sm);
+    auto raddr = [](int k) { return k + (k >> 4) + (k >> 10); };
+    {
+        const int j1 = lane & 15, gq = lane >> 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j2b = 0; j2b < 4; ++j2b)
+                rowl[raddr(wave + 16 * j1 + 256 * (4 * gq + u) + 4096 * j2b)] = acc[4 * u + j2b];
+    }
+    __syncthreads();
+    float* out = partial + (int64_t)blockIdx.x * N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = rowl[raddr(tid0 + r * NT)];
+}
+
 // ---- wf_fft_ip<LOGN>: in-place decimation-in-frequency (A/B: OWRX_WF_KERNEL=ip) ------------
 // Same product as wf_fft_r16 (|X|^2 of the group's windowed frames summed per bin), with the
 // passes done in place: stage s reads 16 samples of one length-L_s sub-transform (stride
@@ -939,6 +1080,30 @@ static hipError_t launch_fft_ip(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
+static hipError_t launch_fft_wl(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                int ngroups, const float* window, const float2* tw,
+                                float* partial, hipStream_t st) {
+    using K = WfWl;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_wl,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(wf_fft_wl, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start, groups,
+                       window, tw, partial);
+    return hipGetLastError();
+}
+
+static bool wf_wave_local() {  // OWRX_WF_KERNEL=wl: wave-local sub-transforms (N = 16384)
+    static const bool v = [] {
+        const char* s = getenv("OWRX_WF_KERNEL");
+        return s && strcmp(s, "wl") == 0;
+    }();
+    return v;
+}
+
 static bool wf_in_place() {  // OWRX_WF_KERNEL=ip: the in-place DIF kernel (A/B)
     static const bool v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
@@ -1016,6 +1181,8 @@ static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfG
     if (wf_radix32()) return launch_fft_r32<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
     if (wf_in_place()) return launch_fft_ip<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
     if (wf_radix4_only()) return launch_fft_t<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+    if constexpr (LOGN == 14)
+        if (wf_wave_local()) return launch_fft_wl(blk, blk_start, groups, ngroups, window, tw, partial, st);
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
 
