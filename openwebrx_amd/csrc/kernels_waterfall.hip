@@ -488,6 +488,36 @@ OWRX_DEV void wl_wave_fence() {  // order one wave's LDS accesses across lanes (
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// v_permlane32_swap: lanes 32..63 of p <-> lanes 0..31 of q; v_permlane16_swap: the odd rows
+// of p <-> the even rows of q (rows of 16 lanes), both components.  (Scalar temporaries: this
+// hipcc folds __builtin_bit_cast of a vector element into the wrong element.)
+template <bool S32>
+OWRX_DEV void wl_swap1(float& a, float& b) {
+    const unsigned ua = __float_as_uint(a), ub = __float_as_uint(b);
+    unsigned r0, r1;
+    if constexpr (S32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
+        r0 = r[0];
+        r1 = r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane16_swap(ua, ub, false, false);
+        r0 = r[0];
+        r1 = r[1];
+    }
+    a = __uint_as_float(r0);
+    b = __uint_as_float(r1);
+}
+template <bool S32>
+OWRX_DEV void wl_swap(c2& p, c2& q) {
+    float px = p.x, py = p.y, qx = q.x, qy = q.y;
+    wl_swap1<S32>(px, qx);
+    wl_swap1<S32>(py, qy);
+    p = c2{px, py};
+    q = c2{qx, qy};
+}
+
+// XL: the last radix-4 stage across the wave's rows with lane swaps instead of an LDS exchange
+template <bool XL>
 __global__ void __launch_bounds__(WfWl::NT)
 wf_fft_wl(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
           const float* __restrict__ window, const float2* __restrict__ tw,
@@ -563,21 +593,41 @@ wf_fft_wl(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __re
         dft_r<16>(a);
         if (s) twiddle_r<16>(a, c2_of(sm[K::TW0 + 256 * s]));  // W_64^(s j2a)
         __builtin_amdgcn_sched_barrier(0);
-        wl_wave_fence();
+        if constexpr (!XL) {
+            wl_wave_fence();
 #pragma unroll
-        for (int j2a = 0; j2a < 16; ++j2a) R[s * K::PU + j2a * K::PJ + j1] = f2_of(a[j2a]);
-        wl_wave_fence();
-        // lane (j1, gq = s): DFT4 over s of (j1, j2a = 4 gq + u), u < 4
+            for (int j2a = 0; j2a < 16; ++j2a) R[s * K::PU + j2a * K::PJ + j1] = f2_of(a[j2a]);
+            wl_wave_fence();
+            // lane (j1, gq = s): DFT4 over s of (j1, j2a = 4 gq + u), u < 4
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j2a = 4 * s + u;
-            c2 c[4];
+            for (int u = 0; u < 4; ++u) {
+                const int j2a = 4 * s + u;
+                c2 c[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) c[q] = c2_of(R[q * K::PU + j2a * K::PJ + j1]);
-            dft4(c[0], c[1], c[2], c[3]);
+                for (int q = 0; q < 4; ++q) c[q] = c2_of(R[q * K::PU + j2a * K::PJ + j1]);
+                dft4(c[0], c[1], c[2], c[3]);
 #pragma unroll
-            for (int j2b = 0; j2b < 4; ++j2b)
-                acc[4 * u + j2b] = fmaf(c[j2b].y, c[j2b].y, fmaf(c[j2b].x, c[j2b].x, acc[4 * u + j2b]));
+                for (int j2b = 0; j2b < 4; ++j2b)
+                    acc[4 * u + j2b] = fmaf(c[j2b].y, c[j2b].y, fmaf(c[j2b].x, c[j2b].x, acc[4 * u + j2b]));
+            }
+        } else {
+            // DFT4 over s = the lane's row (16 lanes) without LDS: registers j2a = 2i, 2i + 1
+            // meet in v_permlane32_swap (rows r, r + 2: s bit 1), then the b0 = 1 half of the
+            // odd rows takes W4 = -i, then v_permlane16_swap (rows r, r + 1: s bit 0).  Lane
+            // (j1, row) ends with register 2i + row / 2, outputs j2b = row % 2 (F0) and
+            // row % 2 + 2 (F1).
+            const bool odd = s & 1;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                c2 P = a[2 * i], Q = a[2 * i + 1];
+                wl_swap<true>(P, Q);
+                c2 X = P + Q, Y = P - Q;
+                if (odd) Y = c2{Y.y, -Y.x};
+                wl_swap<false>(X, Y);
+                const c2 F0 = X + Y, F1 = X - Y;
+                acc[2 * i] = fmaf(F0.y, F0.y, fmaf(F0.x, F0.x, acc[2 * i]));
+                acc[2 * i + 1] = fmaf(F1.y, F1.y, fmaf(F1.x, F1.x, acc[2 * i + 1]));
+            }
         }
         __syncthreads();  // regions reused by the next frame's first pass
     }
@@ -588,11 +638,20 @@ wf_fft_wl(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __re
     auto raddr = [](int k) { return k + (k >> 4) + (k >> 10); };
     {
         const int j1 = lane & 15, gq = lane >> 4;
+        if constexpr (!XL) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int j2b = 0; j2b < 4; ++j2b)
-                rowl[raddr(wave + 16 * j1 + 256 * (4 * gq + u) + 4096 * j2b)] = acc[4 * u + j2b];
+                for (int j2b = 0; j2b < 4; ++j2b)
+                    rowl[raddr(wave + 16 * j1 + 256 * (4 * gq + u) + 4096 * j2b)] = acc[4 * u + j2b];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    rowl[raddr(wave + 16 * j1 + 256 * (2 * i + (gq >> 1)) + 4096 * ((gq & 1) + 2 * h))] =
+                        acc[2 * i + h];
+        }
     }
     __syncthreads();
     float* out = partial + (int64_t)blockIdx.x * N;
@@ -1082,24 +1141,35 @@ static hipError_t launch_fft_ip(const float2* blk, int64_t blk_start, const WfGr
 
 static hipError_t launch_fft_wl(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                 int ngroups, const float* window, const float2* tw,
-                                float* partial, hipStream_t st) {
+                                float* partial, bool xl, hipStream_t st) {
     using K = WfWl;
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_wl,
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_wl<false>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)wf_fft_wl<true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(wf_fft_wl, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start, groups,
+    if (xl)
+        hipLaunchKernelGGL(wf_fft_wl<true>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start,
+                           groups, window, tw, partial);
+    else
+        hipLaunchKernelGGL(wf_fft_wl<false>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start, groups,
                        window, tw, partial);
     return hipGetLastError();
 }
 
-static bool wf_wave_local() {  // OWRX_WF_KERNEL=wl: wave-local sub-transforms (N = 16384)
-    static const bool v = [] {
+// OWRX_WF_KERNEL=wl: wave-local sub-transforms (N = 16384); wlx: and the last stage by lane
+// swaps (1: wl, 2: wlx, 0: neither)
+static int wf_wave_local() {
+    static const int v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
-        return s && strcmp(s, "wl") == 0;
+        if (s && strcmp(s, "wl") == 0) return 1;
+        if (s && strcmp(s, "wlx") == 0) return 2;
+        return 0;
     }();
     return v;
 }
@@ -1182,7 +1252,9 @@ static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfG
     if (wf_in_place()) return launch_fft_ip<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
     if (wf_radix4_only()) return launch_fft_t<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
     if constexpr (LOGN == 14)
-        if (wf_wave_local()) return launch_fft_wl(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        if (wf_wave_local())
+            return launch_fft_wl(blk, blk_start, groups, ngroups, window, tw, partial,
+                                 wf_wave_local() == 2, st);
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
 
