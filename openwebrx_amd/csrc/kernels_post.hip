@@ -16,6 +16,8 @@
 //   concurrently with the next blocks' stream-A work.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "../../include/owrx_amd.h"
@@ -870,6 +872,7 @@ constexpr int kAdGroups = kAdChunk / 8;
 
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 
+template <bool T2>  // T2: the byte-addressed successor table (adpcm_encode_tab2; A/B)
 __global__ void __launch_bounds__(128)
 chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
             const int* __restrict__ sel, int nsel) {
@@ -877,7 +880,8 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     __shared__ uint4 ring[2][kAdGroups][64];  // [slot][group][lane]: 8 int16 samples
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    adpcm_tab_fill(NS, threadIdx.x, 128);
+    if constexpr (T2) adpcm_tab2_fill(NS, threadIdx.x, 128);
+    else adpcm_tab_fill(NS, threadIdx.x, 128);
     const SerLane sl = ser_lane(sel, nsel);
     const int c = sl.c;
     const ChainPost* Pp = posts + c;
@@ -914,7 +918,14 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     // ---- wave 0: the encoder
     ChainStateS* sp = Pp->sstate;
     const ChainStateS st0 = *sp;
-    AdpcmTab ad = adpcm_tab_state(st0.adpcm);
+    auto ad = [&] {
+        if constexpr (T2) return adpcm_tab2_state(st0.adpcm);
+        else return adpcm_tab_state(st0.adpcm);
+    }();
+    auto encode = [&](int x) {
+        if constexpr (T2) return adpcm_encode_tab2(ad, x, NS);
+        else return adpcm_encode_tab(ad, x, NS);
+    };
     const int pend = st0.has_left;  // 1: bytes start at odd samples of this block
     int left = st0.left_code;       // the started byte's low nibble (pend == 1)
     int64_t K = st0.adpcm_bytes + pend;  // index of the next byte to start
@@ -951,7 +962,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
-                    w |= (uint32_t)adpcm_encode_tab(ad, x, NS) << (4 * t);
+                    w |= (uint32_t)encode(x) << (4 * t);
                 }
                 const uint32_t bytes4 = pend ? ((w << 4) | (uint32_t)left) : w;
                 if (pend) left = (int)(w >> 28);
@@ -973,7 +984,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
                     if (kmod == 0) frame();
                     if (++kmod == kAdpcmSyncPeriod) kmod = 0;
                 }
-                const int code = adpcm_encode_tab(ad, x, NS);
+                const int code = encode(x);
                 if (start) {
                     nib = code;
                 } else {
@@ -1051,8 +1062,18 @@ hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
-    hipLaunchKernelGGL(chain_adpcm, dim3((nsel + 63) / 64), dim3(128), 0, st, posts, counts, sel,
-                       nsel);
+    // the byte-addressed successor table (default: 564-567 vs 573-574 us per C3 block, same box,
+    // profiles/r02ab_ab_adpcm_tab2_c3.txt); OWRX_AD_TAB=1: the index-row table (A/B)
+    static const bool t2 = [] {
+        const char* v = getenv("OWRX_AD_TAB");
+        return !(v && strcmp(v, "1") == 0);
+    }();
+    if (t2)
+        hipLaunchKernelGGL(chain_adpcm<true>, dim3((nsel + 63) / 64), dim3(128), 0, st, posts, counts,
+                           sel, nsel);
+    else
+        hipLaunchKernelGGL(chain_adpcm<false>, dim3((nsel + 63) / 64), dim3(128), 0, st, posts,
+                           counts, sel, nsel);
     return hipGetLastError();
 }
 
