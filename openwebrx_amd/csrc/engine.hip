@@ -443,7 +443,9 @@ struct owrx_engine {
     int win_idx = 0;
     float* h_in = nullptr;  // pinned staging for push_iq, two blocks (per block parity)
     int16_t* d_cs16 = nullptr;  // device staging of cs16 ingest (allocated on first use)
-    hipEvent_t evIn = nullptr;  // end of the last block's stream-A work (input reusable)
+    // end of a block's stream-A work (its input and parity-indexed host descriptors reusable),
+    // per block parity; in_pending: the event of the last block is recorded and not waited for
+    hipEvent_t evIn[2] = {nullptr, nullptr};
     bool in_pending = false;
     std::map<int, std::unique_ptr<Waterfall>> wfs;
     // hashed: the per-block loops and the batched reads look every chain up (a tree of 65 536
@@ -987,10 +989,18 @@ static int wide_serial_chains() {
 
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const double t_enter = now_ms();
-    // the previous block's stream-A work must be done before its input / descriptors are
-    // reused; waiting here (not at the end of that block) lets the caller's host work overlap it
-    if (e->in_pending) {
-        HIPCHK(hipEventSynchronize(e->evIn));
+    // Block k's host descriptors and push staging are indexed by block parity, so they need
+    // block k - 2's stream-A work done: the previous call waited for it before returning.  The
+    // wait for block k - 1 (whose input the caller may reuse once this call returns: the
+    // owrx_process_device contract) comes at the end, after block k is built and enqueued, so
+    // stream A runs block k - 1 while the host builds block k (OWRX_IN_WAIT=start: the wait
+    // before the build, the previous order, for A/B).
+    static const bool wait_first = [] {
+        const char* v = getenv("OWRX_IN_WAIT");
+        return v && strcmp(v, "start") == 0;
+    }();
+    if (wait_first && e->in_pending) {
+        HIPCHK(hipEventSynchronize(e->evIn[(e->block_index + 1) & 1]));
         e->stats.host_ms_wait_input += now_ms() - t_enter;
         e->in_pending = false;
     }
@@ -1340,7 +1350,12 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         HIPCHK(hipEventRecord(S.a3, e->sA));
         S.timed = true;
     }
-    HIPCHK(hipEventRecord(e->evIn, e->sA));
+    HIPCHK(hipEventRecord(e->evIn[bp], e->sA));
+    if (!wait_first && e->in_pending) {  // block k - 1 (see the top)
+        const double t = now_ms();
+        HIPCHK(hipEventSynchronize(e->evIn[bp ^ 1]));
+        e->stats.host_ms_wait_input += now_ms() - t;
+    }
     e->in_pending = true;
     e->pos = blk_end;
     e->stats.samples_in += n;
@@ -1495,8 +1510,8 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
         if (dalloc(&e->d_win[i], (size_t)(e->history + max_block)) != hipSuccess)
             return fail("window");
     if (halloc(&e->h_in, 4 * (size_t)max_block) != hipSuccess) return fail("pinned input");
-    if (hipEventCreateWithFlags(&e->evIn, hipEventDisableTiming) != hipSuccess)
-        return fail("event");
+    for (hipEvent_t& ev : e->evIn)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail("event");
     *out = e;
     return OWRX_OK;
 }
@@ -1528,7 +1543,8 @@ int owrx_engine_destroy(owrx_engine* e) {
     dfree(e->d_win[1]);
     dfree(e->d_cs16);
     hfree(e->h_in);
-    if (e->evIn) hipEventDestroy(e->evIn);
+    for (hipEvent_t ev : e->evIn)
+        if (ev) hipEventDestroy(ev);
     for (auto& s : e->slots) {
         free_slot_staging(s);
         for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1, s.m0, s.m1})

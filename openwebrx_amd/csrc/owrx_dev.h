@@ -276,38 +276,47 @@ OWRX_DEV int adpcm_encode_tab(AdpcmTab& s, int sample, const uint32_t* __restric
     return mag | (sgn & 8);
 }
 
-// Byte-addressed variant (chain_adpcm A/B, OWRX_AD_TAB=2): NS2[index * 8 + magnitude] = next
-// step | (next index * 32) << 16, so the next record's LDS byte address is the current record's
-// high half plus 4 * magnitude -- one select after the last magnitude compare instead of
-// assembling the magnitude and scaling it; each magnitude bit's remainder is selected from a
-// subtraction done beside the compare.  Bit-identical to adpcm_encode.
+// Byte-addressed variant (chain_adpcm default; OWRX_AD_TAB=1 selects adpcm_encode_tab):
+// NS2[index * 16 + sign * 8 + magnitude] = next step | (next index * 64) << 16 (the entry does
+// not depend on the sign: each row is stored twice), so the next record's LDS byte address is
+// the current record's high half + 32 * sign + 4 * magnitude -- one select after the last
+// magnitude compare -- and the 4-bit code is that address's bits 2..5.  Each magnitude bit's
+// remainder is selected from a subtraction done beside the compare.  Bit-identical to
+// adpcm_encode.
+constexpr int kAdpcmTab2Entries = 89 * 16;
+
 OWRX_DEV void adpcm_tab2_fill(uint32_t* NS2, int tid, int nthreads) {
-    for (int e = tid; e < kAdpcmTabEntries; e += nthreads) {
-        const int i = e >> 3, m = e & 7;
+    for (int e = tid; e < kAdpcmTab2Entries; e += nthreads) {
+        const int i = e >> 4, m = e & 7;
         int ni = i + kAdpcmIndex[m];
         ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
-        NS2[e] = (uint32_t)kAdpcmStep[ni] | ((uint32_t)(ni * 32) << 16);
+        NS2[e] = (uint32_t)kAdpcmStep[ni] | ((uint32_t)(ni * 64) << 16);
     }
 }
 
 struct AdpcmTab2 {
-    uint32_t rec;  // step | (index * 32) << 16
+    uint32_t rec;  // step | (index * 64) << 16
     int pred;
-    OWRX_DEV int index() const { return (int)(rec >> 21); }
+    OWRX_DEV int index() const { return (int)(rec >> 22); }
 };
 
 OWRX_DEV AdpcmTab2 adpcm_tab2_state(AdpcmState s) {
-    return AdpcmTab2{(uint32_t)kAdpcmStep[s.index] | ((uint32_t)(s.index * 32) << 16), s.pred};
+    return AdpcmTab2{(uint32_t)kAdpcmStep[s.index] | ((uint32_t)(s.index * 64) << 16), s.pred};
 }
 
 OWRX_DEV int adpcm_encode_tab2(AdpcmTab2& s, int sample, const uint32_t* __restrict__ NS2) {
-    const uint32_t rec = s.rec;
-    const int step = (int)(rec & 0xffffu);
-    const int rb = (int)(rec >> 16);
-    const int h = step >> 1, q = step >> 2, s3 = step >> 3;
+    // everything that needs only the predictor first, then a scheduling fence, so that it is
+    // issued while this sample's record is still on its way from LDS (the record's first use
+    // carries the wait)
     const int d = sample - s.pred;
     const int sgn = d >> 31;
+    const int sg32 = sgn & 32;
     const int a0 = max(d, -d);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t rec = s.rec;
+    const int step = (int)(rec & 0xffffu);
+    const int h = step >> 1, q = step >> 2, s3 = step >> 3;
+    const int rb = (int)(rec >> 16) + sg32;
     const bool m4 = a0 >= step;
     const int a1 = m4 ? a0 - step : a0;
     const bool m2 = a1 >= h;
@@ -316,10 +325,12 @@ OWRX_DEV int adpcm_encode_tab2(AdpcmTab2& s, int sample, const uint32_t* __restr
     const int base = rb + (m4 ? 16 : 0) + (m2 ? 8 : 0);
     const int addr = m1 ? base + 4 : base;
     s.rec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(NS2) + addr);
+    // the predictor update after the lookup is issued (it fills the lookup's latency)
+    __builtin_amdgcn_sched_barrier(0);
     const int dq = s3 + (m4 ? step : 0) + (m2 ? h : 0) + (m1 ? q : 0);
     const int p = s.pred + ((dq ^ sgn) - sgn);
     s.pred = min(max(p, -32768), 32767);
-    return ((addr - rb) >> 2) | (sgn & 8);  // the magnitude bits are the address offset
+    return (addr >> 2) & 15;  // magnitude bits and the sign (32 bytes = code bit 3)
 }
 
 }  // namespace owrx
