@@ -993,11 +993,12 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     // block k - 2's stream-A work done: the previous call waited for it before returning.  The
     // wait for block k - 1 (whose input the caller may reuse once this call returns: the
     // owrx_process_device contract) comes at the end, after block k is built and enqueued, so
-    // stream A runs block k - 1 while the host builds block k (OWRX_IN_WAIT=start: the wait
-    // before the build, the previous order, for A/B).
+    // stream A runs block k - 1 while the host builds block k.  That order is the A/B option
+    // OWRX_IN_WAIT=end (+1-2 % at C3); the default waits before the build, the order every
+    // round-1/2 parity run used.
     static const bool wait_first = [] {
         const char* v = getenv("OWRX_IN_WAIT");
-        return v && strcmp(v, "start") == 0;
+        return !(v && strcmp(v, "end") == 0);
     }();
     if (wait_first && e->in_pending) {
         HIPCHK(hipEventSynchronize(e->evIn[(e->block_index + 1) & 1]));
