@@ -296,6 +296,18 @@ def _collect(buf):
     return r, t, out
 
 
+def _stop_collector(col, timeout=5.0):
+    """Let a collector read what its buffer holds, then stop it: Reader.stop() makes read()
+    return None at once, dropping unread bytes (the reference's semantics), so stopping a
+    collector that is still behind would truncate what it saw."""
+    r, t, _ = col
+    deadline = time.time() + timeout
+    while r.available() > 0 and time.time() < deadline:
+        time.sleep(0.005)
+    r.stop()
+    t.join(timeout)
+
+
 @pytest.mark.gpu
 def test_pycsdr_graph_equals_engine():
     """Wideband Buffer -> two ClientDemodulatorChain-shaped graphs + an FftChain graph, fed in
@@ -343,8 +355,7 @@ def test_pycsdr_graph_equals_engine():
         time.sleep(0.01)
     _graph.finish(wide)
     for col in outs + smeters + [wcol, sfcol]:
-        col[0].stop()
-        col[1].join(5)
+        _stop_collector(col)
 
     eng = Engine(1.0, max_block=_graph.BLOCK)
     ref_ch = [eng.chain(params.chain_params(fs, o, m, output=_lib.OUT_ADPCM))
@@ -513,8 +524,7 @@ def test_pycsdr_sharded_engines_equal_single(monkeypatch):
         nengines = len(drv.engines)
         res = []
         for col in [c for pair in cols for c in pair] + [wcol]:
-            col[0].stop()
-            col[1].join(5)
+            _stop_collector(col)
             res.append(b"".join(col[2]))
         return nengines, res
 
@@ -584,8 +594,7 @@ def test_engine_metrics_count_blocks_and_audio():
     _graph.finish(wide)
     for pair in cols:
         for col in pair:
-            col[0].stop()
-            col[1].join(5)
+            _stop_collector(col)
     assert flat["gpu.engines"] >= 1 and flat["gpu.segments"] >= 1
     assert flat["gpu.blocks"] >= 3 and flat["gpu.samples_in"] >= 3 * _graph.BLOCK
     assert flat["gpu.audio_bytes"] > 0 and flat["gpu.failed"] == 0
