@@ -876,7 +876,7 @@ template <bool T2>  // T2: the byte-addressed successor table (adpcm_encode_tab2
 __global__ void __launch_bounds__(128)
 chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
             const int* __restrict__ sel, int nsel) {
-    __shared__ __align__(16) uint32_t NS[kAdpcmTabEntries];
+    __shared__ __align__(16) uint32_t NS[T2 ? kAdpcmTab2Entries : kAdpcmTabEntries];
     __shared__ uint4 ring[2][kAdGroups][64];  // [slot][group][lane]: 8 int16 samples
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
