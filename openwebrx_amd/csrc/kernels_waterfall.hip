@@ -2,13 +2,15 @@
 // owrx/fft.py:36-59): Fft(size=N, every_n_samples=hop) -> LogAveragePower(add_db, N, avg)
 // -> FftSwap -> FftAdpcm.
 //
-// wf_fft_r16 (1024 <= N <= 16384, production): one workgroup (N/16 threads) per group of
+// wf_fft_l32 (N = 16384, production for C2/C3/C5): 32 x 32 x 16 with two LDS exchanges, 512
+//   threads of 32 points, one workgroup per group of consecutive frames (see its comment).
+// wf_fft_r16 (1024 <= N <= 8192; N = 16384 with OWRX_WF_KERNEL=r16): one workgroup (N/16 threads) per group of
 //   consecutive frames of one waterfall row.  Each frame: cf32 samples * Hamming window in
 //   registers (16 per thread, the next frame prefetched during the passes), radix-16 register
 //   DFTs with Stockham exchanges through LDS (N complex + 1-in-16 padding: 136 KiB at
 //   N = 16384, one workgroup per CU), twiddle bases from LDS tables; |X|^2 summed in registers
-//   over the group's frames and written once per group.  A/B alternatives: wf_fft_ip (in-place
-//   DIF, one barrier per stage), wf_fft_rx<.., 32> (radix 32), wf_fft_power (radix 4).
+//   over the group's frames and written once per group.  wf_fft_power (radix 4): N = 256, 512.
+//   Variants that lost their same-box A/B live in tools/micro/wf_variants.hip.
 // wf_fft4_cols / wf_fft4_rows (N = 32768, 65536): four-step FFT through a cf32 scratch frame.
 // wf_finalize: sums each row's group partials in a fixed order onto the carried accumulator
 //   (rows span blocks), 10*log10 + add_db correction, fftshift, quantise (short)(dB*100).
@@ -311,9 +313,17 @@ __device__ unsigned long long g_wf_stamp[1024][16];
     do {                                                                                      \
         if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < 16) g_wf_stamp[blockIdx.x][i] = clock64(); \
     } while (0)
+#define WF_RSTAMP(i)                                                                          \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < 16)                                \
+            g_wf_stamp[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();                     \
+    } while (0)
 #else
 #define WF_STAMP(i) \
     do {            \
+    } while (0)
+#define WF_RSTAMP(i) \
+    do {             \
     } while (0)
 #endif
 
@@ -459,276 +469,162 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     WF_STAMP(13);
 }
 
-// ---- wf_fft_wl: N = 16384 as 16 x 1024 with wave-local sub-transforms (production, C2/C3) --
-// Same product as wf_fft_r16.  Only the first radix-16 pass is a workgroup step: thread t
-// (1024 threads) takes x[t + 1024 r] from HBM (times the window), DFT16 over r, twiddles by
-// W_N^(t k1) and stores Y[k1][t] into region k1 of LDS; one barrier.  Region k1 is then one
-// independent 1024-point DFT (X[k1 + 16 k2] = sum_t Y[k1][t] W_1024^(t k2)), done by wave k1
-// alone: t = l + 64 r (DFT16 over r, twiddle W_1024^(l j1)), l = s + 4 m (DFT16 over m, twiddle
-// W_64^(s j2a)), DFT4 over s, with k2 = j1 + 16 j2a + 256 j2b.  Its two exchanges go through the
-// wave's own region, ordered by the in-order LDS queue of one wave (no workgroup barrier), so
-// sixteen waves interleave one's LDS traffic with another's butterflies instead of the whole
-// workgroup alternating VALU and LDS phases between barriers.  One more barrier per frame
-// before the next frame's first-pass stores reuse the regions.  All twiddles are powers of
-// W_N^t, t < 1024 (an LDS table behind the regions).
-struct WfWl {
-    static constexpr int LOGN = 14, N = 1 << LOGN, NT = 1024;
-    static constexpr int PT = 68;                  // exchange 1 row pitch: T[j1][l], 64 + 4
-    static constexpr int PJ = 17;                  // exchange 2: U[s][j2a][j1] at s PU + j2a PJ + j1
-    static constexpr int PU = 16 * PJ;
-    static constexpr int REG = 16 * PT;            // region of one wave (>= 1024, >= 4 PU)
-    static constexpr int TW0 = 16 * REG;
-    static constexpr size_t kLds = sizeof(float2) * (TW0 + NT);
-    static_assert(REG >= 1024 && REG >= 4 * PU, "region");
-};
+// ---- plain-FP32 complex helpers (wf_fft_l32) ------------------------------------------------
+// A packed FP32 instruction issues in twice the cycles of a scalar one on CDNA4's 32-lane SIMDs,
+// so these are scalar float2 butterflies (FMA-contracted complex products, 4 VALU each).
 
-OWRX_DEV void wl_wave_fence() {  // order one wave's LDS accesses across lanes (in-order queue)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// W_16^m = exp(-2 pi i m / 16), m a compile-time constant after unrolling
+OWRX_DEV float2 w16c(int m) {
+    constexpr float c[16] = {1.0f, 0.92387953251128676f, 0.70710678118654752f, 0.38268343236508977f,
+                             0.0f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128676f,
+                             -1.0f, -0.92387953251128676f, -0.70710678118654752f, -0.38268343236508977f,
+                             0.0f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128676f};
+    return make_float2(c[m & 15], -c[(m + 12) & 15]);  // sin(2 pi m / 16) = cos(2 pi (m - 4) / 16)
 }
 
-// v_permlane32_swap: lanes 32..63 of p <-> lanes 0..31 of q; v_permlane16_swap: the odd rows
-// of p <-> the even rows of q (rows of 16 lanes), both components.  (Scalar temporaries: this
-// hipcc folds __builtin_bit_cast of a vector element into the wrong element.)
-template <bool S32>
-OWRX_DEV void wl_swap1(float& a, float& b) {
-    const unsigned ua = __float_as_uint(a), ub = __float_as_uint(b);
-    unsigned r0, r1;
-    if constexpr (S32) {
-        const auto r = __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
-        r0 = r[0];
-        r1 = r[1];
+OWRX_DEV float2 f2add(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+OWRX_DEV float2 f2sub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+OWRX_DEV float2 f2mi(float2 a) { return make_float2(a.y, -a.x); }  // -i a
+// complex product, FMA form (4 VALU instructions)
+OWRX_DEV float2 f2mul(float2 a, float2 w) {
+    return make_float2(fmaf(a.x, w.x, -(a.y * w.y)), fmaf(a.x, w.y, a.y * w.x));
+}
+
+OWRX_DEV void f2dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = f2add(a0, a2), t1 = f2sub(a0, a2), t2 = f2add(a1, a3), d = f2mi(f2sub(a1, a3));
+    a0 = f2add(t0, t2);
+    a2 = f2sub(t0, t2);
+    a1 = f2add(t1, d);
+    a3 = f2sub(t1, d);
+}
+
+// in-register forward DFT of size R in natural order (R = 2, 4, 8, 16)
+template <int R>
+OWRX_DEV void f2dft(float2* a) {
+    if constexpr (R == 2) {
+        const float2 t = a[1];
+        a[1] = f2sub(a[0], t);
+        a[0] = f2add(a[0], t);
+    } else if constexpr (R == 4) {
+        f2dft4(a[0], a[1], a[2], a[3]);
+    } else if constexpr (R == 8) {
+        float2 b0[4] = {a[0], a[2], a[4], a[6]}, b1[4] = {a[1], a[3], a[5], a[7]};
+        f2dft4(b0[0], b0[1], b0[2], b0[3]);
+        f2dft4(b1[0], b1[1], b1[2], b1[3]);
+        const float h = 0.70710678118654752f;
+        b1[1] = make_float2(h * (b1[1].x + b1[1].y), h * (b1[1].y - b1[1].x));    // W8^1
+        b1[2] = f2mi(b1[2]);                                                      // W8^2
+        b1[3] = make_float2(h * (b1[3].y - b1[3].x), -h * (b1[3].x + b1[3].y));   // W8^3
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            a[k] = f2add(b0[k], b1[k]);
+            a[k + 4] = f2sub(b0[k], b1[k]);
+        }
     } else {
-        const auto r = __builtin_amdgcn_permlane16_swap(ua, ub, false, false);
-        r0 = r[0];
-        r1 = r[1];
+        static_assert(R == 16, "radix");
+        // n = 4 n1 + n2, k = k1 + 4 k2: DFT4 over n1, twiddle W16^(n2 k1), DFT4 over n2
+#pragma unroll
+        for (int n2 = 0; n2 < 4; ++n2) f2dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
+        const float c1 = 0.92387953251128676f, s1 = 0.38268343236508977f, h = 0.70710678118654752f;
+        a[5] = f2mul(a[5], make_float2(c1, -s1));                                      // W^1
+        a[9] = make_float2(h * (a[9].x + a[9].y), h * (a[9].y - a[9].x));              // W^2
+        a[13] = f2mul(a[13], make_float2(s1, -c1));                                    // W^3
+        a[6] = make_float2(h * (a[6].x + a[6].y), h * (a[6].y - a[6].x));              // W^2
+        a[10] = f2mi(a[10]);                                                           // W^4
+        a[14] = make_float2(h * (a[14].y - a[14].x), -h * (a[14].x + a[14].y));        // W^6
+        a[7] = f2mul(a[7], make_float2(s1, -c1));                                      // W^3
+        a[11] = make_float2(h * (a[11].y - a[11].x), -h * (a[11].x + a[11].y));        // W^6
+        a[15] = f2mul(a[15], make_float2(-c1, s1));                                    // W^9
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1) f2dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
+        float2 t[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i] = a[i];
+#pragma unroll
+        for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) a[k1 + 4 * k2] = t[4 * k1 + k2];
     }
-    a = __uint_as_float(r0);
-    b = __uint_as_float(r1);
-}
-template <bool S32>
-OWRX_DEV void wl_swap(c2& p, c2& q) {
-    float px = p.x, py = p.y, qx = q.x, qy = q.y;
-    wl_swap1<S32>(px, qx);
-    wl_swap1<S32>(py, qy);
-    p = c2{px, py};
-    q = c2{qx, qy};
 }
 
-// XL: the last radix-4 stage across the wave's rows with lane swaps instead of an LDS exchange
-template <bool XL>
-__global__ void __launch_bounds__(WfWl::NT)
-wf_fft_wl(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
-          const float* __restrict__ window, const float2* __restrict__ tw,
-          float* __restrict__ partial) {
-    using K = WfWl;
+// W_32^m = exp(-2 pi i m / 32), m a compile-time constant after unrolling
+OWRX_DEV float2 w32c(int m) {
+    constexpr float c[32] = {
+        1.0f, 0.98078528040323043f, 0.92387953251128676f, 0.83146961230254524f,
+        0.70710678118654752f, 0.55557023301960218f, 0.38268343236508977f, 0.19509032201612827f,
+        0.0f, -0.19509032201612827f, -0.38268343236508977f, -0.55557023301960218f,
+        -0.70710678118654752f, -0.83146961230254524f, -0.92387953251128676f, -0.98078528040323043f,
+        -1.0f, -0.98078528040323043f, -0.92387953251128676f, -0.83146961230254524f,
+        -0.70710678118654752f, -0.55557023301960218f, -0.38268343236508977f, -0.19509032201612827f,
+        0.0f, 0.19509032201612827f, 0.38268343236508977f, 0.55557023301960218f,
+        0.70710678118654752f, 0.83146961230254524f, 0.92387953251128676f, 0.98078528040323043f};
+    return make_float2(c[m & 31], -c[(m + 24) & 31]);
+}
+
+// a * W_32^m for a compile-time m: the eighth turns as adds and a multiply, -i as a swap
+OWRX_DEV float2 f2mul32(float2 a, int m) {
+    const float h = 0.70710678118654752f;
+    switch (m & 31) {
+        case 0: return a;
+        case 4: return make_float2(h * (a.x + a.y), h * (a.y - a.x));
+        case 8: return f2mi(a);
+        case 12: return make_float2(h * (a.y - a.x), -h * (a.x + a.y));
+        case 16: return make_float2(-a.x, -a.y);
+        case 20: return make_float2(-h * (a.x + a.y), h * (a.x - a.y));
+        case 24: return make_float2(-a.y, a.x);
+        case 28: return make_float2(h * (a.x - a.y), h * (a.x + a.y));
+        default: return f2mul(a, w32c(m));
+    }
+}
+
+// in-register forward DFT-32 in place: n = 4 n1 + n2 (n1 < 8, n2 < 4), k = k1 + 8 k2; X[k] is
+// left at a[4 k1 + k2] (l32_at(k)), so no register array is copied
+OWRX_DEV constexpr int l32_at(int k) { return 4 * (k & 7) + (k >> 3); }
+OWRX_DEV void f2dft32(float2* a) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+        float2 v[8];
+#pragma unroll
+        for (int n1 = 0; n1 < 8; ++n1) v[n1] = a[4 * n1 + n2];
+        f2dft<8>(v);
+#pragma unroll
+        for (int k1 = 0; k1 < 8; ++k1) a[4 * k1 + n2] = k1 && n2 ? f2mul32(v[k1], n2 * k1) : v[k1];
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < 8; ++k1) f2dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
+}
+
+// ---- wf_fft_l32: N = 16384 as 32 x 32 x 16, two LDS exchanges ------------------------------
+// 512 threads of 32 points (two waves per SIMD, up to 256 VGPRs each), one workgroup per CU.
+// LDS stores are the scarcest resource of the exchange (~85 B/clk/CU for any store width), so
+// radix 32 cuts them from three 128 KiB exchanges per frame to two:
+//  P1 (Ns = 1):    x[t + 512 r] * window -> DFT32 -> image[32 t + k]
+//  P2 (Ns = 32):   image[t + 512 r] * W_1024^(r k), k = t & 31 (LDS table [31][32]) -> DFT32
+//                  -> image[(t >> 5) 1024 + k + 32 r]
+//  P3 (Ns = 1024): two radix-16 butterflies j = t + 512 b: image[j + 1024 r] * W_N^(r j), the
+//                  bases W_N^(r t) in registers for the whole group (W_N^(r j) = W_N^(r t) W_32^(r b))
+//                  -> DFT16 -> |X|^2 of bins j + 1024 r, summed in registers over the group.
+// The image is XOR-swizzled (e ^ ((e >> 5) & 15)): the stride-32 stores of P1 and every read
+// are bank-conflict-free.  The next frame's samples are loaded in P1 (in flight across P2 and
+// P3) and the window taps in P3, so a frame starts on data already in registers.
+struct WfL32 {
+    static constexpr int LOGN = 14, N = 1 << LOGN, NT = 512;
+    static constexpr int TW2 = N;  // [31][32]: W_1024^(r k), r = 1..31
+    static constexpr size_t kLds = sizeof(float2) * (N + 31 * 32);
+};
+OWRX_DEV int wf_swz32(int e) { return e ^ ((e >> 5) & 15); }
+
+__global__ void __launch_bounds__(WfL32::NT)
+wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+           const float* __restrict__ window, const float2* __restrict__ tw,
+           float* __restrict__ partial) {
+    using K = WfL32;
     constexpr int N = K::N, NT = K::NT;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    const int tid0 = threadIdx.x;
-    const WfGroup g = groups[blockIdx.x];
-    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
-    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
-    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
-    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
-        0x00020000);
-    const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
-                                                      (int)(sizeof(float) * N), 0x00020000);
-    auto load_x = [&](int f, c2* v) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int vo = tid0 * 8 + f * hop * 8;
-            v[r] = c2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
-                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0))};
-        }
-    };
-    c2 nx[16];
-    load_x(0, nx);
-    sm[K::TW0 + tid0] = tw[tid0];  // W_N^t, t < 1024
-    const int wave = tid0 >> 6, lane = tid0 & 63;
-    float acc[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
-    __syncthreads();
-#pragma unroll 1
-    for (int f = 0; f < nfr; ++f) {
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        c2 a[16];
-        {   // pass 0 (workgroup): windowed samples, DFT16 over r, twiddle W_N^(t k1), Y[k1][t]
-            float wv[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, tid0 * 4, r * NT * 4, 0));
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a[r] = nx[r] * wv[r];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        dft_r<16>(a);
-        if (tid) twiddle_r<16>(a, c2_of(sm[K::TW0 + tid]));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) sm[k1 * K::REG + tid] = f2_of(a[k1]);
-        if (f + 1 < nfr) load_x(f + 1, nx);
-        __syncthreads();
-        // wave-local 1024-point DFT of region `wave`
-        float2* R = sm + wave * K::REG;
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-#pragma unroll
-        for (int r = 0; r < 16; ++r) a[r] = c2_of(R[ln + 64 * r]);
-        __builtin_amdgcn_sched_barrier(0);
-        dft_r<16>(a);
-        if (ln) twiddle_r<16>(a, c2_of(sm[K::TW0 + 16 * ln]));  // W_1024^(l j1)
-        __builtin_amdgcn_sched_barrier(0);
-        wl_wave_fence();  // every lane's reads of Y before the region is rewritten
-#pragma unroll
-        for (int j1 = 0; j1 < 16; ++j1) R[j1 * K::PT + ln] = f2_of(a[j1]);
-        wl_wave_fence();
-        const int j1 = ln & 15, s = ln >> 4;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) a[m] = c2_of(R[j1 * K::PT + s + 4 * m]);
-        __builtin_amdgcn_sched_barrier(0);
-        dft_r<16>(a);
-        if (s) twiddle_r<16>(a, c2_of(sm[K::TW0 + 256 * s]));  // W_64^(s j2a)
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!XL) {
-            wl_wave_fence();
-#pragma unroll
-            for (int j2a = 0; j2a < 16; ++j2a) R[s * K::PU + j2a * K::PJ + j1] = f2_of(a[j2a]);
-            wl_wave_fence();
-            // lane (j1, gq = s): DFT4 over s of (j1, j2a = 4 gq + u), u < 4
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j2a = 4 * s + u;
-                c2 c[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) c[q] = c2_of(R[q * K::PU + j2a * K::PJ + j1]);
-                dft4(c[0], c[1], c[2], c[3]);
-#pragma unroll
-                for (int j2b = 0; j2b < 4; ++j2b)
-                    acc[4 * u + j2b] = fmaf(c[j2b].y, c[j2b].y, fmaf(c[j2b].x, c[j2b].x, acc[4 * u + j2b]));
-            }
-        } else {
-            // DFT4 over s = the lane's row (16 lanes) without LDS: registers j2a = 2i, 2i + 1
-            // meet in v_permlane32_swap (rows r, r + 2: s bit 1), then the b0 = 1 half of the
-            // odd rows takes W4 = -i, then v_permlane16_swap (rows r, r + 1: s bit 0).  Lane
-            // (j1, row) ends with register 2i + row / 2, outputs j2b = row % 2 (F0) and
-            // row % 2 + 2 (F1).
-            const bool odd = s & 1;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                c2 P = a[2 * i], Q = a[2 * i + 1];
-                wl_swap<true>(P, Q);
-                c2 X = P + Q, Y = P - Q;
-                if (odd) Y = c2{Y.y, -Y.x};
-                wl_swap<false>(X, Y);
-                const c2 F0 = X + Y, F1 = X - Y;
-                acc[2 * i] = fmaf(F0.y, F0.y, fmaf(F0.x, F0.x, acc[2 * i]));
-                acc[2 * i + 1] = fmaf(F1.y, F1.y, fmaf(F1.x, F1.x, acc[2 * i + 1]));
-            }
-        }
-        __syncthreads();  // regions reused by the next frame's first pass
-    }
-    // bin of acc[4 u + j2b]: k = wave + 16 j1 + 256 (4 gq + u) + 4096 j2b; the row goes out
-    // through LDS in bin order (k + k/16 + k/1024 spreads one store's lanes over the banks) so
-    // that the partial row is written with coalesced stores
-    float* rowl = reinterpret_cast<float*>(sm);
-    auto raddr = [](int k) { return k + (k >> 4) + (k >> 10); };
-    {
-        const int j1 = lane & 15, gq = lane >> 4;
-        if constexpr (!XL) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-#pragma unroll
-                for (int j2b = 0; j2b < 4; ++j2b)
-                    rowl[raddr(wave + 16 * j1 + 256 * (4 * gq + u) + 4096 * j2b)] = acc[4 * u + j2b];
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    rowl[raddr(wave + 16 * j1 + 256 * (2 * i + (gq >> 1)) + 4096 * ((gq & 1) + 2 * h))] =
-                        acc[2 * i + h];
-        }
-    }
-    __syncthreads();
-    float* out = partial + (int64_t)blockIdx.x * N;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) out[tid0 + r * NT] = rowl[raddr(tid0 + r * NT)];
-}
-
-// ---- wf_fft_ip<LOGN>: in-place decimation-in-frequency (A/B: OWRX_WF_KERNEL=ip) ------------
-// Same product as wf_fft_r16 (|X|^2 of the group's windowed frames summed per bin), with the
-// passes done in place: stage s reads 16 samples of one length-L_s sub-transform (stride
-// S_s = L_s / 16), takes the DFT16, twiddles output q by W_(L_s)^(n q) and writes it back to the
-// addresses it read.  No thread overwrites another's inputs, so a stage needs one barrier (its
-// reads after the previous stage's stores) instead of two, and each wave's stores follow its
-// own DFT without waiting for every wave's reads.  The last stage (radix RL, or the last
-// radix-16 stage when N is a power of 16) reads 16 consecutive samples per thread and leaves the
-// bins in digit-reversed positions; the bin index is recomputed when the partial row goes out
-// (through LDS, coalesced).  With the 1-in-16 padding every stage's reads and stores are free of
-// LDS bank conflicts.  Twiddle bases W_(L_s)^n come from per-stage LDS tables.
-template <int LOGN>
-struct WfIp {
-    static constexpr int N = 1 << LOGN;
-    static constexpr int NT = N / 16;
-    static constexpr int P16 = LOGN / 4;                      // radix-16 stages
-    static constexpr int RL = 1 << (LOGN - 4 * P16);          // last radix (1: none)
-    static constexpr int NS = RL > 1 ? P16 : P16 - 1;         // stages that twiddle and store
-    static constexpr int stride(int s) { return N >> (4 * (s + 1)); }  // S_s
-    static constexpr int tab(int s) {                         // table offset of stage s
-        int o = 0;
-        for (int i = 0; i < s; ++i) o += stride(i);
-        return o;
-    }
-    static constexpr int TW0 = N + N / 16;
-    static constexpr size_t kLds = sizeof(float2) * (TW0 + tab(NS));
-    // The partial row goes through LDS by bin: thread t's bins differ from its neighbours' in
-    // five bin bits (lane bit i moves position bit i + 4, i.e. digit bit kbit(i) of the bin).
-    // The row is stored at k ^ swz(k), swz built from the bits above 4 only, so that those five
-    // bits land on five different bank bits (stores conflict-free) while 32 consecutive bins
-    // still cover all banks (the coalesced read-out conflict-free).
-    static constexpr int kbit(int i) {
-        const int e = i + 4, st = (LOGN - e - 1) / 4;  // stage whose stride S satisfies S <= 2^e < 16 S
-        return 4 * st + e - (LOGN - 4 * st - 4);
-    }
-    static constexpr unsigned swz_vec(int b) {  // XOR vector of bin bit b >= 5 (0: none)
-        unsigned used = 0;
-        for (int i = 0; i < 5; ++i)
-            if (kbit(i) < 5) used |= 1u << kbit(i);
-        for (int i = 0, free_bit = 0; i < 5; ++i) {
-            if (kbit(i) < 5) continue;
-            while (used & (1u << free_bit)) ++free_bit;
-            used |= 1u << free_bit;
-            if (kbit(i) == b) return 1u << free_bit;
-        }
-        return 0;
-    }
-};
-
-template <int LOGN>
-OWRX_DEV int wf_ip_row_addr(int k) {
-    unsigned x = 0;
-#pragma unroll
-    for (int b = 5; b < LOGN; ++b)
-        if (WfIp<LOGN>::swz_vec(b)) x ^= ((k >> b) & 1) ? WfIp<LOGN>::swz_vec(b) : 0u;
-    return k ^ (int)x;
-}
-
-template <int LOGN>
-__global__ void __launch_bounds__(WfIp<LOGN>::NT)
-wf_fft_ip(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
-          const float* __restrict__ window, const float2* __restrict__ tw, float* __restrict__ partial) {
-    using K = WfIp<LOGN>;
-    constexpr int N = K::N, NT = K::NT, P16 = K::P16, RL = K::RL, NS = K::NS;
-    extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    const int tid0 = threadIdx.x;
-    const WfGroup g = groups[blockIdx.x];
+    const int t0 = threadIdx.x;
+    WF_RSTAMP(14);
     WF_STAMP(0);
-    // frame samples and window taps through buffer descriptors (one VGPR of lane offset), the
-    // first frame requested before the twiddle tables (vmcnt is in order)
+    const WfGroup g = groups[blockIdx.x];
     const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
     const int hop = __builtin_amdgcn_readfirstlane(g.hop);
     const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
@@ -737,214 +633,116 @@ wf_fft_ip(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __re
         0x00020000);
     const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
                                                       (int)(sizeof(float) * N), 0x00020000);
-    auto load_x = [&](int f, c2* v) {
+    auto load_x = [&](int f, float2* v) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            // two dword loads paired into one dwordx2 (this hipcc's vector-returning
-            // raw_buffer_load_b64 / _b128 builtins load one dword and splat it)
-            const int vo = tid0 * 8 + f * hop * 8;
-            v[r] = c2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
-                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0))};
+        for (int r = 0; r < 32; ++r) {
+            const int vo = t0 * 8 + f * hop * 8;
+            v[r] = make_float2(
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0)));
         }
     };
-    c2 nx[16];
-    load_x(0, nx);
-    // twiddle bases: stage 0's W_N^tid stays in a register (each thread uses only its own); the
-    // later stages' tables (N/256 + N/4096 + ... entries) go to LDS, written in frame 0 before the
-    // stage-1 barrier so no load latency is waited for before the first DFT
-    const c2 tw0 = c2_of(tw[tid0]);
-    constexpr int NTAB1 = K::tab(NS) - K::tab(1);  // entries of stages >= 1
-    float2 tw1 = float2{0.0f, 0.0f};
-    int tab_i = 0;
-    if (NTAB1 > 0 && tid0 < NTAB1) {
-        int s = 1, n = tid0;
-        while (s < NS && n >= K::stride(s)) n -= K::stride(s++);
-        tab_i = K::TW0 + K::tab(s) + n;
-        tw1 = tw[n << (4 * s)];
-    }
-    float acc[16];
+    auto load_w = [&](float* v) {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
+        for (int r = 0; r < 32; ++r)
+            v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, t0 * 4, r * NT * 4, 0));
+    };
+    // L2-resident tables first (vmcnt retires in order: the frame's HBM loads queue behind them)
+    float2 tp[4];  // W_N^(2^i t), i < 4: P3's bases W_N^(r t) are products of at most four
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tp[i] = tw[(t0 << i) & (N - 1)];
+    float2 t2v[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int e = t0 + NT * i;  // 992 entries: (r - 1) * 32 + k
+        t2v[i] = e < 31 * 32 ? tw[(((e >> 5) + 1) * (e & 31)) << 4] : make_float2(0.f, 0.f);
+    }
+    float2 nx[32];
+    load_x(0, nx);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        if (t0 + NT * i < 31 * 32) sm[K::TW2 + t0 + NT * i] = t2v[i];
+    float acc[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
+    const int sw = wf_swz32(t0);  // swz(t + 512 m) = swz(t) + 512 m
 #pragma unroll 1
     for (int f = 0; f < nfr; ++f) {
-        int tid = threadIdx.x;  // opaque: keeps the stage addresses inside the frame loop
-        asm volatile("" : "+v"(tid));
-        const int st0 = 1 + 6 * f;
-        WF_STAMP(st0);
-        c2 a[16];
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        const int sb = 1 + 6 * f;
+        if (f < 2) WF_STAMP(sb);
+        float2 a[32];
         {
-            float wv[16];
+            float wv[32];
+            load_w(wv);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) a[r] = make_float2(nx[r].x * wv[r], nx[r].y * wv[r]);
+        }
+        if (f + 1 < nfr) load_x(f + 1, nx);
+        f2dft32(a);
+        if (f < 2) WF_STAMP(sb + 1);
+        __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
+#pragma unroll
+        for (int k = 0; k < 32; ++k) sm[32 * t + (k ^ (t & 15))] = a[l32_at(k)];
+        if (f < 2) WF_STAMP(sb + 2);
+        __syncthreads();
+        // P2
+        {
+            const int ts = wf_swz32(t);
+#pragma unroll
+            for (int r = 0; r < 32; ++r) a[r] = sm[ts + NT * r];
+            const int k = t & 31;
+            const float2* T = sm + K::TW2 + k;
+#pragma unroll
+            for (int r = 1; r < 32; ++r) {
+                a[r] = f2mul(a[r], T[(r - 1) * 32]);
+                if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 8 twiddles live
+            }
+            f2dft32(a);
+            __syncthreads();  // every P2 read before any P2 store
+            const int base = (t >> 5) * 1024 + k;
+#pragma unroll
+            for (int r = 0; r < 32; ++r) sm[wf_swz32(base + 32 * r)] = a[l32_at(r)];
+        }
+        if (f < 2) WF_STAMP(sb + 3);
+        __syncthreads();
+        // P3
+#pragma unroll
+        for (int m = 0; m < 32; ++m) a[m] = sm[sw + NT * m];
+        if (f < 2) WF_STAMP(sb + 4);
+        float2 tb[16];  // W_N^(r t) from the exact powers of two, at most three products each
+        tb[1] = tp[0];
+        tb[2] = tp[1];
+        tb[4] = tp[2];
+        tb[8] = tp[3];
+        tb[3] = f2mul(tp[0], tp[1]);
+        tb[5] = f2mul(tp[0], tp[2]);
+        tb[6] = f2mul(tp[1], tp[2]);
+        tb[7] = f2mul(tb[3], tp[2]);
+#pragma unroll
+        for (int r = 9; r < 16; ++r) tb[r] = f2mul(tb[r - 8], tp[3]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            float2 c[16];
+            c[0] = a[b];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) {
+                const float2 w = b ? f2mul32(tb[r], r) : tb[r];
+                c[r] = f2mul(a[b + 2 * r], w);
+            }
+            f2dft<16>(c);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, tid0 * 4, r * NT * 4, 0));
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a[r] = nx[r] * wv[r];
+                acc[b + 2 * r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b + 2 * r]));
         }
-        WF_STAMP(st0 + 1);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            const int S = K::stride(s);
-            const int n = tid & (S - 1);
-            const int base = (tid / S) * (16 * S) + n;  // sub-transform start + n
-            if (s > 0) {
-                __syncthreads();  // the previous stage's stores
-#pragma unroll
-                for (int m = 0; m < 16; ++m) a[m] = c2_of(sm[wf_pad(base + m * S)]);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            dft_r<16>(a);
-            if (n) twiddle_r<16>(a, s == 0 ? tw0 : c2_of(sm[K::TW0 + K::tab(s) + n]));  // W_(16 S)^(n q)
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) sm[wf_pad(base + q * S)] = f2_of(a[q]);
-            if (s == 0 && f == 0 && NTAB1 > 0 && tid0 < NTAB1) sm[tab_i] = tw1;
-            if (s == 0 && f + 1 < nfr) load_x(f + 1, nx);
-            WF_STAMP(st0 + 2 + s);
-        }
-        __syncthreads();
-        // last stage: 16 consecutive samples per thread
-        if constexpr (RL > 1) {
-#pragma unroll
-            for (int j = 0; j < 16 / RL; ++j) {
-                c2 c[RL];
-#pragma unroll
-                for (int n = 0; n < RL; ++n) c[n] = c2_of(sm[wf_pad(16 * tid + RL * j + n)]);
-                dft_r<RL>(c);
-#pragma unroll
-                for (int q = 0; q < RL; ++q)
-                    acc[j * RL + q] = fmaf(c[q].y, c[q].y, fmaf(c[q].x, c[q].x, acc[j * RL + q]));
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < 16; ++m) a[m] = c2_of(sm[wf_pad(16 * tid + m)]);
-            dft_r<16>(a);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) acc[q] = fmaf(a[q].y, a[q].y, fmaf(a[q].x, a[q].x, acc[q]));
-        }
-        WF_STAMP(st0 + 5);
-        __syncthreads();  // LDS reused by the next frame (and by the row below)
+        if (f < 2) WF_STAMP(sb + 5);
     }
-    // bins: position p = 16 tid + RL j holds, after stage s, digit q_s = (p / S_s) % 16 of the
-    // bin (weight 16^s); the last stage's output q has weight 16^(number of earlier stages)
-    float* rowl = reinterpret_cast<float*>(sm);
-    constexpr int NE = RL > 1 ? P16 : P16 - 1;  // stages before the last
-    constexpr int WL = 1 << (4 * NE);
-#pragma unroll
-    for (int j = 0; j < (RL > 1 ? 16 / RL : 1); ++j) {
-        const int p = 16 * tid0 + (RL > 1 ? RL : 16) * j;
-        int k0 = 0;
-#pragma unroll
-        for (int s = 0; s < NE; ++s) k0 += ((p / K::stride(s)) & 15) << (4 * s);
-        constexpr int Q = RL > 1 ? RL : 16;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) rowl[wf_ip_row_addr<LOGN>(k0 + q * WL)] = acc[j * Q + q];
-    }
-    __syncthreads();
     float* out = partial + (int64_t)blockIdx.x * N;
-    for (int i = tid0; i < N; i += NT) out[i] = rowl[wf_ip_row_addr<LOGN>(i)];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
     WF_STAMP(13);
-}
-
-// ---- wf_fft_rx<LOGN, R>: the same product with radix-R passes, N/R threads -----------------
-// R = 32: 512 threads of 32 points at N = 16384, two LDS round trips per frame (radix 32, 32,
-// then a last radix 16) instead of three; |X|^2 summed in fp32 per bin (one register per bin).
-// The LDS image is padded one element in R.  Selected by OWRX_WF_KERNEL=r32 (A/B).
-template <int LOGN, int R>
-struct WfRx {
-    static constexpr int LOGR = R == 16 ? 4 : 5;
-    static constexpr int N = 1 << LOGN;
-    static constexpr int NT = N / R;
-    static constexpr int PR = LOGN / LOGR;                      // radix-R passes
-    static constexpr int RL = 1 << (LOGN - LOGR * PR);          // last radix (1: none)
-    static constexpr int BL = RL > 1 ? N / RL / NT : 1;         // butterflies / thread, last
-    static constexpr int NACC = RL > 1 ? BL * RL : R;           // bins per thread
-    static constexpr size_t kLds = sizeof(float2) * (N + N / R);
-    OWRX_DEV static int pad(int i) { return i + (i >> LOGR); }
-};
-
-template <int LOGN, int R>
-__global__ void __launch_bounds__((WfRx<LOGN, R>::NT))
-wf_fft_rx(const float2* __restrict__ blk, int64_t blk_start,
-          const WfGroup* __restrict__ groups, const float* __restrict__ window,
-          const float2* __restrict__ tw, float* __restrict__ partial) {
-    using K = WfRx<LOGN, R>;
-    constexpr int N = K::N, NT = K::NT, PR = K::PR, RL = K::RL, BL = K::BL;
-    extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    const int tid0 = threadIdx.x;
-    const WfGroup g = groups[blockIdx.x];
-    float acc[K::NACC];  // sum |X|^2 per bin
-#pragma unroll
-    for (int m = 0; m < K::NACC; ++m) acc[m] = 0.0f;
-    c2 nx[R];  // the next frame's samples, loaded while this frame's LDS passes run
-#pragma unroll
-    for (int r = 0; r < R; ++r) nx[r] = c2_of(blk[g.start - blk_start + tid0 + r * NT]);
-#pragma unroll 1
-    for (int f = 0; f < g.nframes; ++f) {
-        int tid = threadIdx.x;
-        asm volatile("" : "+v"(tid));  // keeps each pass's address arithmetic in the loop
-        c2 a[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) a[r] = nx[r] * window[tid + r * NT];
-        int ns = 1;
-#pragma unroll
-        for (int pass = 0; pass < PR; ++pass) {
-            if (pass > 0) {
-                __syncthreads();  // the previous pass's stores
-#pragma unroll
-                for (int r = 0; r < R; ++r) a[r] = c2_of(sm[K::pad(tid + r * NT)]);
-                const int k = tid & (ns - 1);
-                if (k) twiddle_r<R>(a, c2_of(tw[k * (N / (ns * R))]));  // W_(R Ns)^k
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            dft_r<R>(a);
-            __builtin_amdgcn_sched_barrier(0);
-            const bool last = (pass == PR - 1) && RL == 1;
-            if (last) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] = fmaf(a[r].x, a[r].x, fmaf(a[r].y, a[r].y, acc[r]));
-            } else {
-                if (pass > 0) __syncthreads();  // every load of this pass before any store
-                const int k = tid & (ns - 1);
-                const int d = ((tid / ns) * ns * R) + k;
-#pragma unroll
-                for (int r = 0; r < R; ++r) sm[K::pad(d + r * ns)] = f2_of(a[r]);
-                if (pass == 0 && f + 1 < g.nframes) {
-                    const float2* xn = blk + (g.start + (int64_t)(f + 1) * g.hop - blk_start);
-#pragma unroll
-                    for (int r = 0; r < R; ++r) nx[r] = c2_of(xn[tid + r * NT]);
-                }
-            }
-            ns *= R;
-        }
-        if constexpr (RL > 1) {
-            // last pass: radix RL, Ns = N / RL, butterflies j = tid + b NT, outputs j + r N/RL
-            __syncthreads();
-#pragma unroll
-            for (int b = 0; b < BL; ++b) {
-                const int j = tid + b * NT;
-                c2 c[RL];
-#pragma unroll
-                for (int r = 0; r < RL; ++r) c[r] = c2_of(sm[K::pad(j + r * (N / RL))]);
-                if (j) twiddle_r<RL>(c, c2_of(tw[j]));  // W_N^(r j)
-                dft_r<RL>(c);
-#pragma unroll
-                for (int r = 0; r < RL; ++r)
-                    acc[b * RL + r] = fmaf(c[r].x, c[r].x, fmaf(c[r].y, c[r].y, acc[b * RL + r]));
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        __syncthreads();  // LDS reused by the next frame
-    }
-    float* out = partial + (int64_t)blockIdx.x * N;
-    if constexpr (RL > 1) {
-#pragma unroll
-        for (int b = 0; b < BL; ++b)
-#pragma unroll
-            for (int r = 0; r < RL; ++r) out[tid0 + b * NT + r * (N / RL)] = acc[b * RL + r];
-    } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r) out[tid0 + r * NT] = acc[r];
-    }
+    WF_RSTAMP(15);
 }
 
 // ---- FFT sizes above one CU's LDS (32768, 65536): four-step, two launches ------------------
@@ -1105,100 +903,6 @@ static hipError_t launch_fft_r16(const float2* blk, int64_t blk_start, const WfG
 }
 
 template <int LOGN>
-static hipError_t launch_fft_r32(const float2* blk, int64_t blk_start, const WfGroup* groups,
-                                 int ngroups, const float* window, const float2* tw,
-                                 float* partial, hipStream_t st) {
-    using K = WfRx<LOGN, 32>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_rx<LOGN, 32>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)K::kLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    hipLaunchKernelGGL((wf_fft_rx<LOGN, 32>), dim3(ngroups), dim3(K::NT), K::kLds, st, blk,
-                       blk_start, groups, window, tw, partial);
-    return hipGetLastError();
-}
-
-template <int LOGN>
-static hipError_t launch_fft_ip(const float2* blk, int64_t blk_start, const WfGroup* groups,
-                                int ngroups, const float* window, const float2* tw,
-                                float* partial, hipStream_t st) {
-    using K = WfIp<LOGN>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_ip<LOGN>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    hipLaunchKernelGGL(wf_fft_ip<LOGN>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start,
-                       groups, window, tw, partial);
-    return hipGetLastError();
-}
-
-static hipError_t launch_fft_wl(const float2* blk, int64_t blk_start, const WfGroup* groups,
-                                int ngroups, const float* window, const float2* tw,
-                                float* partial, bool xl, hipStream_t st) {
-    using K = WfWl;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_wl<false>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)wf_fft_wl<true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)K::kLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    if (xl)
-        hipLaunchKernelGGL(wf_fft_wl<true>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start,
-                           groups, window, tw, partial);
-    else
-        hipLaunchKernelGGL(wf_fft_wl<false>, dim3(ngroups), dim3(K::NT), K::kLds, st, blk, blk_start, groups,
-                       window, tw, partial);
-    return hipGetLastError();
-}
-
-// OWRX_WF_KERNEL=wl: wave-local sub-transforms (N = 16384); wlx: and the last stage by lane
-// swaps (1: wl, 2: wlx, 0: neither)
-static int wf_wave_local() {
-    static const int v = [] {
-        const char* s = getenv("OWRX_WF_KERNEL");
-        if (s && strcmp(s, "wl") == 0) return 1;
-        if (s && strcmp(s, "wlx") == 0) return 2;
-        return 0;
-    }();
-    return v;
-}
-
-static bool wf_in_place() {  // OWRX_WF_KERNEL=ip: the in-place DIF kernel (A/B)
-    static const bool v = [] {
-        const char* s = getenv("OWRX_WF_KERNEL");
-        return s && strcmp(s, "ip") == 0;
-    }();
-    return v;
-}
-
-static bool wf_radix32() {  // OWRX_WF_KERNEL=r32: the radix-32 kernel (A/B)
-    static const bool v = [] {
-        const char* s = getenv("OWRX_WF_KERNEL");
-        return s && strcmp(s, "r32") == 0;
-    }();
-    return v;
-}
-
-static bool wf_radix4_only() {  // OWRX_WF_KERNEL=radix4: the radix-4 LDS kernel (A/B)
-    static const bool v = [] {
-        const char* s = getenv("OWRX_WF_KERNEL");
-        return s && strcmp(s, "radix4") == 0;
-    }();
-    return v;
-}
-
-template <int LOGN>
 static hipError_t launch_fft_t(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                int ngroups, const float* window, const float2* tw,
                                float* partial, hipStream_t st) {
@@ -1242,23 +946,42 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
-// 1024 <= N <= 16384: the Stockham radix-16 kernel, or an A/B alternative
-// (OWRX_WF_KERNEL=ip | r32 | radix4; DESIGN.md records the measurements)
+// N = 16384: the radix-32 two-exchange kernel (OWRX_WF_KERNEL=r16 keeps the radix-16 one, A/B);
+// 1024 <= N <= 8192: radix 16
+static bool wf_force_r16() {
+    static const bool v = [] {
+        const char* s = getenv("OWRX_WF_KERNEL");
+        return s && strcmp(s, "r16") == 0;
+    }();
+    return v;
+}
+
+static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                 int ngroups, const float* window, const float2* tw,
+                                 float* partial, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_l32,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)WfL32::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(wf_fft_l32, dim3(ngroups), dim3(WfL32::NT), WfL32::kLds, st, blk, blk_start,
+                       groups, window, tw, partial);
+    return hipGetLastError();
+}
+
 template <int LOGN>
 static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw, float* partial,
                                  hipStream_t st) {
-    if (wf_radix32()) return launch_fft_r32<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-    if (wf_in_place()) return launch_fft_ip<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-    if (wf_radix4_only()) return launch_fft_t<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
     if constexpr (LOGN == 14)
-        if (wf_wave_local())
-            return launch_fft_wl(blk, blk_start, groups, ngroups, window, tw, partial,
-                                 wf_wave_local() == 2, st);
+        if (!wf_force_r16()) return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, st);
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
 
-// scratch: ngroups * N cf32, used for N > 16384 (groups hold one frame each there)
+
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, const float* window, const float2* tw, float* partial,
                          float2* scratch, hipStream_t st) {
