@@ -268,7 +268,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--block", type=int, default=1 << 22)
+    ap.add_argument("--block", type=int, default=1 << 20,
+                    help="IQ samples per step (SURVEY.md 8d: 2^20-sample blocks)")
+    ap.add_argument("--wf-batch", type=int, default=-1,
+                    help="waterfall frames per FFT launch (owrx_waterfall_set_batch; -1: four per "
+                         "stream-A CU, 0: every block's frames in that block)")
     ap.add_argument("--chains", type=int, default=None,
                     help="chains per GPU (default: the config's)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
@@ -323,12 +327,21 @@ def main():
              for o, m in mine]
 
     block = args.block
-    eng = Engine(fs, max_block=block, device=local)
+    # waterfall batching (rank 0 of a one-GPU run): the engine keeps enough history for the
+    # batch's frames, and the FFT runs once per batch instead of once per block
+    wf_batch = 0
+    if world == 1 and not args.no_waterfall:
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        wf_batch = 4 * max(1, cus - 16) if args.wf_batch < 0 else args.wf_batch
+    history = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
+    eng = Engine(fs, max_block=block, device=local, history=history)
     eng.set_ddc_mode(args.ddc)
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:
         wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
+        if wf_batch > 1:
+            wf.set_batch(wf_batch)
     chains = [eng.chain(p) for p in plist]
 
     # engine priming before the W warmup steps: the first ~10 blocks of a fresh engine include
@@ -437,6 +450,12 @@ def main():
     wf_ms = d["gpu_ms_waterfall"]
     post_ms = d["gpu_ms_post"]
     wf_launches = d["waterfall_launches"]
+    # waterfall roofline (HBM-bound, 8 B of cf32 per input sample read once):
+    # algorithmic bytes of the frames the timed FFT launches advanced over / their HIP-event time
+    wf_fft_ms = d["gpu_ms_waterfall_fft"]
+    wf_bytes = 8.0 * d["waterfall_timed_samples"]
+    wf_gbs = wf_bytes / (wf_fft_ms / 1e3) / 1e9 if wf_fft_ms > 0 else None
+    wf_traffic, wf_traffic_src = pmc_traffic("wf_fft_l32", args.config)
 
     traffic, traffic_src = pmc_traffic("fc_mac<" if fast else "ddc_lds<", args.config)
     rt = None
@@ -510,6 +529,31 @@ def main():
                         "so the HBM fraction is given beside it.  traffic = HBM bytes per launch "
                         "from separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE "
                         "passes of this config: " + traffic_src,
+                "waterfall": None if wf_gbs is None else {
+                    "bound": "hbm",
+                    "kernel": "wf_fft_l32 + wf_finalize (FftChain: Hamming FFT, |X|^2 summed over "
+                              "avg frames, 10 log10, FftSwap, quantise)",
+                    "achieved": round(wf_gbs, 1),
+                    "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s",
+                    "frac": round(wf_gbs / HBM_PEAK_GBS, 4),
+                    "traffic": wf_traffic,
+                    "frames_per_launch": round(d["waterfall_frames"] / max(1, wf_launches), 1),
+                    "launches": wf_launches,
+                    "ms_per_launch": round(wf_fft_ms / max(1, wf_launches), 4),
+                    "note": "achieved = 8 B x the stream samples the timed launches' frames advanced "
+                            "over (frames x hop) / the HIP-event time of those launches (FFT + "
+                            "finalize) on stream A; traffic from rocprofv3 PMC passes: "
+                            + wf_traffic_src,
+                },
+            },
+            "waterfall_batch": {
+                "min_frames": wf_batch,
+                "engine_history_samples": hist,
+                "row_latency_s": round(wf_batch * hop / fs, 3) if wf_batch > 1 else 0.0,
+                "note": "owrx_waterfall_set_batch: the FFT launches once the batch's frames are "
+                        "ready (rows reach the reader up to row_latency_s of stream later than "
+                        "with per-block launches; rows bit-identical for any block cut)",
             },
             "ddc": {
                 "form": "fast convolution" if fast else "direct",

@@ -67,6 +67,13 @@ int owrx_device_count(void);                   /* visible HIP devices, or OWRX_E
  * Replaces the wideband pycsdr Buffer(COMPLEX_FLOAT) fed by TcpSource
  * (owrx/source/__init__.py:307-330) and the per-module native threads. */
 int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_engine** out);
+/* As owrx_engine_create, keeping `history` samples of the stream before each block readable
+ * (<= 0: the minimum, 2^18: the longest FIR and the FFT overlap).  A longer history lets a
+ * waterfall batch the frames of several blocks into one chip-filling launch
+ * (owrx_waterfall_set_batch).  The push path keeps it in one device ring (the last `history`
+ * samples are copied to the ring's start once per lap, not per block). */
+int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64_t history,
+                          owrx_engine** out);
 int owrx_engine_destroy(owrx_engine* e);
 /* samples that must precede a block handed to owrx_process_device (filter/FFT history) */
 int64_t owrx_engine_history(owrx_engine* e);
@@ -102,6 +109,14 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
 /* FftChain._setBlockSize / setFftAverages / setCompression (fft.py:51-55, 11-16, 87-96) */
 int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_number,
                        int adpcm);
+/* Launch granularity of the waterfall FFT (an engine-side choice; the rows, bit for bit, and
+ * their order do not depend on it).  Complete frame groups are launched when at least
+ * `min_frames` are ready, or when the oldest pending frame starts `max_lag` or more samples
+ * before the end of the newest block, or before it would leave the engine history, and on
+ * owrx_sync.  min_frames <= 1 (the default): every block's frames in that block.  max_lag <= 0:
+ * as far as the history allows.  Rows then reach the reader up to max_lag samples later than
+ * with per-block launches (the throughput / latency trade of Fft(every_n_samples) batching). */
+int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t max_lag);
 int owrx_waterfall_destroy(owrx_engine* e, int handle);
 /* bytes of one output row: (fft_size+10)/2 with ADPCM, 4*fft_size without */
 int64_t owrx_waterfall_row_bytes(owrx_engine* e, int handle);
@@ -221,6 +236,11 @@ typedef struct {
     double  host_ms_wait_input;/*   the previous block's stream-A work (input / descriptors) */
     double  host_ms_wait_slots;/*   block k - 4's chain outputs (the pipeline depth) */
     double  host_ms_wait_rows; /*   the oldest waterfall row slot */
+    int64_t waterfall_frames;  /* FFT frames launched */
+    int64_t waterfall_samples; /* stream samples those frames advanced over (frames x hop) */
+    double  gpu_ms_waterfall_fft; /* HIP-event time of the waterfall FFT + finalize launches
+                                     alone (timing enabled), for the HBM roofline */
+    int64_t waterfall_timed_samples; /* stream samples of the frames those timed launches did */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* 1 => record HIP events around each kernel group on the engine's streams */

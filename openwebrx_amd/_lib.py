@@ -94,6 +94,10 @@ class Stats(ctypes.Structure):
         ("host_ms_wait_input", ctypes.c_double),
         ("host_ms_wait_slots", ctypes.c_double),
         ("host_ms_wait_rows", ctypes.c_double),
+        ("waterfall_frames", ctypes.c_int64),
+        ("waterfall_samples", ctypes.c_int64),
+        ("gpu_ms_waterfall_fft", ctypes.c_double),
+        ("waterfall_timed_samples", ctypes.c_int64),
     ]
 
 
@@ -111,6 +115,7 @@ PROTOTYPES = {
     "owrx_last_error": (ctypes.c_char_p, []),
     "owrx_device_count": (_i32, []),
     "owrx_engine_create": (_i32, [_i32, _f64, _i64, ctypes.POINTER(_vp)]),
+    "owrx_engine_create_ex": (_i32, [_i32, _f64, _i64, _i64, ctypes.POINTER(_vp)]),
     "owrx_engine_destroy": (_i32, [_vp]),
     "owrx_engine_history": (_i64, [_vp]),
     "owrx_engine_max_block": (_i64, [_vp]),
@@ -122,6 +127,7 @@ PROTOTYPES = {
     "owrx_sync": (_i32, [_vp]),
     "owrx_waterfall_create": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32, _pi32]),
     "owrx_waterfall_set": (_i32, [_vp, _i32, _i32, _i32, _i32]),
+    "owrx_waterfall_set_batch": (_i32, [_vp, _i32, _i32, _i64]),
     "owrx_waterfall_destroy": (_i32, [_vp, _i32]),
     "owrx_waterfall_row_bytes": (_i64, [_vp, _i32]),
     "owrx_waterfall_read": (_i64, [_vp, _i32, _vp, _i64]),

@@ -46,6 +46,7 @@ void set_last_error(const char* fmt, ...) {
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, const float* window, const float2* tw, float* partial,
                          float2* scratch, hipStream_t st);
+bool wf_uses_l32(int logn);  // kernels_waterfall.hip: the N = 16384 kernel in use
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st);
@@ -166,6 +167,9 @@ struct Waterfall {
     bool pending = false;
     int64_t next_start = 0;  // absolute index of the next frame
     int row_frame = 0;       // frames of the current row already scheduled
+    int fpg = 1;             // frames per group (fixed per configuration: rows are bit-stable)
+    int batch_min = 0;       // owrx_waterfall_set_batch: launch once this many frames are ready
+    int64_t batch_lag = 0;   //   ... or the oldest pending frame is this far behind (0: history)
     bool carry_valid = false;
     int carry_idx = 0;
     int64_t rows = 0;
@@ -315,8 +319,10 @@ struct Slot {  // one block's outputs in flight on streams B / C
     hipEvent_t m0 = nullptr, m1 = nullptr;  // around the fast-convolution DDC's GEMM (fc_mac)
     bool timed_mac = false;
     hipEvent_t b0 = nullptr, b1 = nullptr;
+    hipEvent_t w0 = nullptr, w1 = nullptr;  // around the waterfall FFT + finalize launches
     bool timed = false;
     bool timed_wf = false;
+    bool timed_wff = false;
 };
 
 struct RowSlot {  // one block's waterfall rows being encoded / copied on stream R
@@ -438,9 +444,13 @@ struct owrx_engine {
     bool timing = false;
     int ddc_mode = OWRX_DDC_FAST;
     std::recursive_mutex mu;
-    // push-path window (ping-pong): [history | block]
-    float2* d_win[2] = {nullptr, nullptr};
-    int win_idx = 0;
+    // push-path ring: blocks are appended at wp with `history` samples before them; when the
+    // next block does not fit, the last `history` samples move to the start (once per lap)
+    float2* d_ring = nullptr;
+    int64_t ring_cap = 0, wp = 0;
+    // the newest block's window (the waterfall flush at owrx_sync launches pending frames on it)
+    const float2* last_blk = nullptr;
+    int64_t last_start = 0, last_end = 0;
     float* h_in = nullptr;  // pinned staging for push_iq, two blocks (per block parity)
     int16_t* d_cs16 = nullptr;  // device staging of cs16 ingest (allocated on first use)
     // end of a block's stream-A work (its input and parity-indexed host descriptors reusable),
@@ -609,6 +619,12 @@ static int drain_slot(owrx_engine* e, int si) {
         if (hipEventElapsedTime(&ms, s.a0, s.a1) == hipSuccess) e->stats.gpu_ms_waterfall += ms;
         s.timed_wf = false;
     }
+    if (s.timed_wff) {
+        float ms = 0;
+        HIPCHK(hipEventSynchronize(s.w1));
+        if (hipEventElapsedTime(&ms, s.w0, s.w1) == hipSuccess) e->stats.gpu_ms_waterfall_fft += ms;
+        s.timed_wff = false;
+    }
     return OWRX_OK;
 }
 
@@ -668,8 +684,10 @@ static int drain_all(owrx_engine* e) {
 }
 
 static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
-    // capacities derived from the current hop/avg; re-run when they change
-    const int64_t frames = e->max_block / std::max(1, w->hop) + 2 * kWfMaxFramesPerGroup + 2;
+    // capacities derived from the current hop/avg; re-run when they change.  A batched launch
+    // (owrx_waterfall_set_batch) holds at most the frames of the history window plus a block.
+    const int64_t span = w->batch_min > 1 ? e->history + e->max_block : e->max_block;
+    const int64_t frames = span / std::max(1, w->hop) + 2 * kWfMaxFramesPerGroup + 2;
     const int groups = (int)(frames + 2);  // a group may hold a single frame at row ends
     const int rows = (int)(frames / std::max(1, w->avg) + 3);
     if (groups > w->partial_groups || rows > w->rows_cap) RCCHK(drain_all(e));
@@ -871,38 +889,52 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
 // block processing
 // ------------------------------------------------------------------------------------------
 
-// Schedules and launches one FftChain's work for the block on stream A; completed rows are
-// staged in slot `si` (their ADPCM / copy is enqueued by the caller on stream C).
-// Frames summed by one FFT workgroup: enough that a full block's frames occupy stream A's CUs
-// about once (the partial |X|^2 rows written per block shrink by the same factor).  Depends
-// only on the engine geometry and hop, and groups start at fixed frame offsets of a row, so
-// the summation order -- hence every row, bit for bit -- does not depend on how the stream is
-// cut into blocks.  The four-step FFT (N > kWfLdsMaxN) takes one frame per group.
+// Frames summed by one FFT workgroup (one partial |X|^2 row per group).  Fixed per waterfall
+// configuration (engine geometry, hop, batching) and groups start at fixed frame offsets of a
+// row, so the summation order -- hence every row, bit for bit -- does not depend on how the
+// stream is cut into blocks or launches.  `frames` is the launch size expected: a block's
+// frames, or the batch.
+//  - wf_fft_l32 (N = 16384): 2, or 4 for launches of >= 3 frames per CU (micro-benchmark, C3
+//    geometry: 366 frames F=2 21.3 us vs F=1 24.6 / F=3 27.6; 960 frames F=4 41.4 us vs F=2
+//    45.5; profiles/r03a_wf_micro_*.txt);
+//  - wf_fft_r16: enough that a launch's frames occupy stream A's CUs about once;
+//  - the four-step FFT (N > kWfLdsMaxN): one frame per group.
 static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
     if (w->N > kWfLdsMaxN) return 1;
     const int64_t hop = std::max(1, w->hop);
-    const int64_t per_block = e->max_block / hop;
-    static const int wgs_per_cu = [] {  // OWRX_WF_GROUPS_PER_CU: A/B of the group count
-        const char* s = getenv("OWRX_WF_GROUPS_PER_CU");
-        return s ? std::max(1, atoi(s)) : 1;
-    }();
-    const int64_t slots = (int64_t)std::max(1, e->cus_a) * wgs_per_cu;
-    int64_t fpg = (per_block + slots - 1) / slots;
-    fpg = std::min<int64_t>(fpg, (e->history - w->N) / hop);
+    const int64_t frames = std::max<int64_t>(w->batch_min, e->max_block / hop);
+    const int64_t cus = std::max(1, e->cus_a);
+    if (wf_uses_l32(w->logn)) return frames >= 3 * cus ? 4 : 2;
+    int64_t fpg = (frames + cus - 1) / cus;
+    fpg = std::min(fpg, (e->history - w->N) / hop);
     return (int)std::max<int64_t>(1, std::min<int64_t>(fpg, kWfMaxFramesPerGroup));
 }
 
+// Schedules and launches one FftChain's ready frames on stream A (when the batching rule says
+// so, or `force`); completed rows are staged in row slot `ri` (their ADPCM / copy is enqueued
+// by the caller on that slot's stream).
 static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, int64_t blk_start,
-                             int64_t blk_end, int ri, int* completed) {
+                             int64_t blk_end, int ri, bool force, int* completed, bool timed,
+                             Slot* S) {
     *completed = 0;
     w->groups.clear();
     w->rowdesc.clear();
+    if (w->next_start + w->N > blk_end) return OWRX_OK;  // no frame complete
+    if (w->batch_min > 1 && !force) {
+        // launch once enough frames are ready, or the oldest pending one is max_lag behind, or
+        // it would leave the window of the next block (which starts at blk_end - history)
+        const int64_t ready = (blk_end - w->N - w->next_start) / std::max(1, w->hop) + 1;
+        const int64_t lag = blk_end - w->next_start;
+        const int64_t max_lag = w->batch_lag > 0 ? w->batch_lag : e->history;
+        const bool leaving = w->next_start < blk_end + w->hop - e->history;
+        if (ready < w->batch_min && lag < max_lag && !leaving) return OWRX_OK;
+    }
     int cur_row_first_group = 0;
     bool row_open = false;
     const int adpcm_now = w->adpcm;
     const int avg_now = w->avg;
     while (true) {
-        const int gf = std::min(wf_frames_per_group(e, w), w->avg - w->row_frame);
+        const int gf = std::min(w->fpg, w->avg - w->row_frame);
         const int64_t last = w->next_start + (int64_t)(gf - 1) * w->hop;
         if (last + w->N > blk_end) break;
         if ((int)w->groups.size() >= w->partial_groups) break;
@@ -929,6 +961,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
                 w->hop = w->new_hop;
                 w->avg = w->new_avg;
                 w->adpcm = w->new_adpcm;
+                w->fpg = wf_frames_per_group(e, w);
                 w->pending = false;
                 break;
             }
@@ -947,11 +980,20 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         w->rowdesc.push_back(r);
     }
     if (w->groups.empty()) return OWRX_OK;
+    int64_t nfr = 0;
+    for (const WfGroup& g : w->groups) nfr += g.nframes;
+    e->stats.waterfall_frames += nfr;
+    e->stats.waterfall_samples += nfr * w->hop;
     const int bp = (int)(e->block_index & 1);
     memcpy(w->h_groups[bp], w->groups.data(), sizeof(WfGroup) * w->groups.size());
     memcpy(w->h_rows[bp], w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size());
     HIPCHK(kcopy(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(), e->sA));
     HIPCHK(kcopy(w->d_rows, w->h_rows[bp], sizeof(WfRow) * w->rowdesc.size(), e->sA));
+    const bool tm = timed && S && !S->timed_wff;  // the first waterfall of a timed block
+    if (tm) {
+        HIPCHK(hipEventRecord(S->w0, e->sA));
+        e->stats.waterfall_timed_samples += nfr * w->hop;
+    }
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(),
                          w->d_window, w->d_tw, w->d_partial, w->d_y4, e->sA));
     const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
@@ -959,6 +1001,10 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     HIPCHK(launch_wf_finalize(w->d_partial, w->d_rows, (int)w->rowdesc.size(), w->d_carry[cin],
                               w->d_carry[cout], w->N, corr, adpcm_now, w->d_s16[ri],
                               w->d_f32[ri], e->sA));
+    if (tm) {
+        HIPCHK(hipEventRecord(S->w1, e->sA));
+        S->timed_wff = true;
+    }
     if (row_open) {
         w->carry_idx = cout;
         w->carry_valid = true;
@@ -974,6 +1020,48 @@ static double now_ms() {
     return std::chrono::duration<double, std::milli>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+
+// Every waterfall's ready frames (batching rule, or all of them with `force`) on stream A, then
+// the completed rows' FftAdpcm + copy on a row slot's stream.
+static int run_waterfalls(owrx_engine* e, const float2* blk, int64_t blk_start, int64_t blk_end,
+                          bool force, bool timed, Slot* S) {
+    bool any_rows = false;
+    if (!e->wfs.empty()) {
+        const double t = now_ms();
+        RCCHK(drain_rows(e, true, kRowSlots - 1));  // frees the slot about to be reused
+        e->stats.host_ms_wait_rows += now_ms() - t;
+        const int ri = (int)(e->row_head % kRowSlots);
+        RowSlot& R = e->rslots[ri];
+        for (auto& kv : e->wfs) {
+            Waterfall* w = kv.second.get();
+            int done = 0;
+            RCCHK(process_waterfall(e, w, blk, blk_start, blk_end, ri, force, &done, timed, S));
+            any_rows |= done > 0;
+        }
+        if (any_rows) {
+            HIPCHK(hipEventRecord(R.evWf, e->sA));
+            HIPCHK(hipStreamWaitEvent(R.stream, R.evWf, 0));
+            for (auto& kv : e->wfs) {
+                Waterfall* w = kv.second.get();
+                const int nr = w->pend_rows[ri];
+                if (nr <= 0) continue;
+                const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
+                if (w->pend_adpcm[ri]) {
+                    HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
+                                           R.stream));
+                    HIPCHK(kcopy(w->h_bytes[ri], w->d_bytes[ri], rb * nr, R.stream));
+                } else {
+                    HIPCHK(kcopy(w->h_bytes[ri], w->d_f32[ri], rb * nr, R.stream));
+                }
+            }
+            HIPCHK(hipEventRecord(R.evC, R.stream));
+            R.pending = true;
+            e->row_head++;
+        }
+    }
+    return OWRX_OK;
+}
+
 
 // Chains per block above which the serial kernels (post_serial_front, chain_nr, chain_adpcm) run
 // on unmasked streams: one lane per chain, so 1 024 chains are 16 waves = one per SIMD of
@@ -1020,40 +1108,10 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     if (timed) HIPCHK(hipEventRecord(S.a0, e->sA));
 
     // ---- waterfalls (stream A); row encoding + copy on the row slot's own stream
-    bool any_rows = false;
-    if (!e->wfs.empty()) {
-        const double t = now_ms();
-        RCCHK(drain_rows(e, true, kRowSlots - 1));  // frees the slot about to be reused
-        e->stats.host_ms_wait_rows += now_ms() - t;
-        const int ri = (int)(e->row_head % kRowSlots);
-        RowSlot& R = e->rslots[ri];
-        for (auto& kv : e->wfs) {
-            Waterfall* w = kv.second.get();
-            int done = 0;
-            RCCHK(process_waterfall(e, w, blk, blk_start, blk_end, ri, &done));
-            any_rows |= done > 0;
-        }
-        if (any_rows) {
-            HIPCHK(hipEventRecord(R.evWf, e->sA));
-            HIPCHK(hipStreamWaitEvent(R.stream, R.evWf, 0));
-            for (auto& kv : e->wfs) {
-                Waterfall* w = kv.second.get();
-                const int nr = w->pend_rows[ri];
-                if (nr <= 0) continue;
-                const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
-                if (w->pend_adpcm[ri]) {
-                    HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
-                                           R.stream));
-                    HIPCHK(kcopy(w->h_bytes[ri], w->d_bytes[ri], rb * nr, R.stream));
-                } else {
-                    HIPCHK(kcopy(w->h_bytes[ri], w->d_f32[ri], rb * nr, R.stream));
-                }
-            }
-            HIPCHK(hipEventRecord(R.evC, R.stream));
-            R.pending = true;
-            e->row_head++;
-        }
-    }
+    RCCHK(run_waterfalls(e, blk, blk_start, blk_end, false, timed, &S));
+    e->last_blk = blk;
+    e->last_start = blk_start;
+    e->last_end = blk_end;
     // ---- chains: DDC per group (A); post_parallel + post_serial_front (B); ADPCM + copies (C)
     e->posts.clear();
     S.post_ids.clear();
@@ -1464,6 +1522,11 @@ static hipError_t create_streams(owrx_engine* e) {
 }
 
 int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_engine** out) {
+    return owrx_engine_create_ex(device, samp_rate, max_block, 0, out);
+}
+
+int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64_t history,
+                          owrx_engine** out) {
     if (!out || samp_rate <= 0 || max_block <= 0) {
         set_last_error("owrx_engine_create: bad arguments");
         return OWRX_EINVAL;
@@ -1478,6 +1541,7 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
     e->device = device;
     e->samp_rate = samp_rate;
     e->max_block = max_block;
+    e->history = std::max<int64_t>(kDefaultHistory, (history + 255) & ~(int64_t)255);
     memset(&e->stats, 0, sizeof(e->stats));
     auto fail = [&](const char* what) {
         set_last_error("owrx_engine_create: %s", what);
@@ -1504,12 +1568,17 @@ int owrx_engine_create(int device, double samp_rate, int64_t max_block, owrx_eng
             hipEventCreateWithFlags(&s.b0, hipEventDisableSystemFence) != hipSuccess ||
             hipEventCreateWithFlags(&s.b1, hipEventDisableSystemFence) != hipSuccess ||
             hipEventCreateWithFlags(&s.m0, hipEventDisableSystemFence) != hipSuccess ||
-            hipEventCreateWithFlags(&s.m1, hipEventDisableSystemFence) != hipSuccess)
+            hipEventCreateWithFlags(&s.m1, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.w0, hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.w1, hipEventDisableSystemFence) != hipSuccess)
             return fail("event");
     }
-    for (int i = 0; i < 2; ++i)
-        if (dalloc(&e->d_win[i], (size_t)(e->history + max_block)) != hipSuccess)
-            return fail("window");
+    // push-path ring: a lap holds >= 4 blocks past the history, so the per-lap move of the
+    // history to the start never overlaps its source, and no block still read on stream A
+    e->ring_cap = 2 * e->history + 4 * max_block;
+    if (dalloc(&e->d_ring, (size_t)e->ring_cap) != hipSuccess) return fail("ring");
+    if (hipMemset(e->d_ring, 0, sizeof(float2) * e->history) != hipSuccess) return fail("ring");
+    e->wp = e->history;
     if (halloc(&e->h_in, 4 * (size_t)max_block) != hipSuccess) return fail("pinned input");
     for (hipEvent_t& ev : e->evIn)
         if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail("event");
@@ -1540,15 +1609,15 @@ int owrx_engine_destroy(owrx_engine* e) {
         hfree(g->h_chains[0]);
         hfree(g->h_chains[1]);
     }
-    dfree(e->d_win[0]);
-    dfree(e->d_win[1]);
+    dfree(e->d_ring);
     dfree(e->d_cs16);
     hfree(e->h_in);
     for (hipEvent_t ev : e->evIn)
         if (ev) hipEventDestroy(ev);
     for (auto& s : e->slots) {
         free_slot_staging(s);
-        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1, s.m0, s.m1})
+        for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1, s.m0, s.m1,
+                              s.w0, s.w1})
             if (ev) hipEventDestroy(ev);
     }
     for (auto& r : e->rslots) {
@@ -1577,29 +1646,36 @@ int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t n) {
     return OWRX_OK;
 }
 
+// Room for a block of n at the ring's write position: when it does not fit, the last `history`
+// samples move to the ring's start on stream A (behind every kernel that read them).
+static int ring_room(owrx_engine* e, int64_t n, bool* wrapped) {
+    *wrapped = false;
+    if (e->wp + n <= e->ring_cap) return OWRX_OK;
+    HIPCHK(hipMemcpyAsync(e->d_ring, e->d_ring + (e->wp - e->history), sizeof(float2) * e->history,
+                          hipMemcpyDeviceToDevice, e->sA));
+    e->wp = e->history;
+    *wrapped = true;
+    return OWRX_OK;
+}
+
 int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity) {
     ENGINE_GUARD(e);
     if (!dev_ptr || !capacity) return OWRX_EINVAL;
-    *dev_ptr = (float*)(e->d_win[e->win_idx] + e->history);
+    bool wrapped = false;
+    RC_FAIL(e, ring_room(e, e->max_block, &wrapped));
+    // the caller writes on a stream of its own: the move must be done first
+    if (wrapped) RC_FAIL(e, hipStreamSynchronize(e->sA) == hipSuccess ? OWRX_OK : OWRX_EIO);
+    *dev_ptr = (float*)(e->d_ring + e->wp);
     *capacity = e->max_block;
     return OWRX_OK;
 }
 
 int owrx_commit(owrx_engine* e, int64_t n) {
     ENGINE_GUARD(e);
-    if (n < 0 || n > e->max_block) return OWRX_EINVAL;
+    if (n < 0 || n > e->max_block || e->wp + n > e->ring_cap) return OWRX_EINVAL;
     if (n == 0) return OWRX_OK;
-    float2* w = e->d_win[e->win_idx];
-    RC_FAIL(e, process_block(e, w + e->history, n));
-    // carry the last `history` samples into the other window
-    float2* o = e->d_win[1 - e->win_idx];
-    if (hipMemcpyAsync(o, w + n, sizeof(float2) * e->history, hipMemcpyDeviceToDevice, e->sA) !=
-        hipSuccess) {
-        e->failed = true;
-        set_last_error("window carry copy failed");
-        return OWRX_EIO;
-    }
-    e->win_idx = 1 - e->win_idx;
+    RC_FAIL(e, process_block(e, e->d_ring + e->wp, n));
+    e->wp += n;
     return OWRX_OK;
 }
 
@@ -1613,7 +1689,9 @@ int owrx_push_iq(owrx_engine* e, const float* iq, int64_t n) {
         // block's stream-A work, which process_block waited for at the start of the last block
         float* hb = e->h_in + 2 * (e->block_index & 1) * e->max_block;
         memcpy(hb, iq + 2 * done, sizeof(float2) * m);
-        float2* dst = e->d_win[e->win_idx] + e->history;
+        bool wrapped = false;
+        RC_FAIL(e, ring_room(e, m, &wrapped));  // ordered with the copy below on stream A
+        float2* dst = e->d_ring + e->wp;
         if (hipMemcpyAsync(dst, hb, sizeof(float2) * m, hipMemcpyHostToDevice, e->sA) !=
             hipSuccess) {
             e->failed = true;
@@ -1642,7 +1720,9 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq, int64_t n, float gain) 
         // same staging discipline as owrx_push_iq (half the bytes per sample)
         int16_t* hb = reinterpret_cast<int16_t*>(e->h_in + 2 * (e->block_index & 1) * e->max_block);
         memcpy(hb, iq + 2 * done, 4 * (size_t)m);
-        float* dst = reinterpret_cast<float*>(e->d_win[e->win_idx] + e->history);
+        bool wrapped = false;
+        RC_FAIL(e, ring_room(e, m, &wrapped));
+        float* dst = reinterpret_cast<float*>(e->d_ring + e->wp);
         if (hipMemcpyAsync(e->d_cs16, hb, 4 * (size_t)m, hipMemcpyHostToDevice, e->sA) !=
             hipSuccess) {
             e->failed = true;
@@ -1666,6 +1746,9 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq, int64_t n, float gain) 
 
 int owrx_sync(owrx_engine* e) {
     ENGINE_GUARD(e);
+    // batched waterfalls: launch what is pending on the newest block's window (still valid:
+    // owrx_process_device's contract, or the ring)
+    if (e->last_blk) RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr));
     RC_FAIL(e, drain_all(e));
     return OWRX_OK;
 }
@@ -1696,6 +1779,7 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
     w->adpcm = adpcm ? 1 : 0;
     w->add_db = add_db;
     w->next_start = e->pos;
+    w->fpg = wf_frames_per_group(e, w.get());
     std::vector<float> win = hamming_window(fft_size);
     std::vector<float> tw = fft_twiddles(fft_size);
     HIPCHK(dalloc(&w->d_window, (size_t)fft_size));
@@ -1730,11 +1814,40 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
         w->hop = w->new_hop;
         w->avg = w->new_avg;
         w->adpcm = w->new_adpcm;
+        w->fpg = wf_frames_per_group(e, w);
         w->pending = false;
     } else {
         w->pending = true;
     }
     RC_FAIL(e, wf_alloc_buffers(e, w));  // sized for the larger of old/new settings
+    return OWRX_OK;
+}
+
+int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t max_lag) {
+    ENGINE_GUARD(e);
+    auto it = e->wfs.find(handle);
+    if (it == e->wfs.end() || max_lag < 0) return OWRX_EINVAL;
+    Waterfall* w = it->second.get();
+    // pending frames first (they were grouped under the old rule), at a row boundary only: the
+    // group size may change with the batch, and rows must not mix two group sizes
+    if (e->last_blk) RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr));
+    RC_FAIL(e, drain_all(e));
+    if (w->row_frame != 0 || w->carry_valid) {
+        set_last_error("owrx_waterfall_set_batch: only between rows (set it before the stream starts)");
+        return OWRX_EINVAL;
+    }
+    const int old_min = w->batch_min, old_fpg = w->fpg;
+    w->batch_min = std::max(0, min_frames);
+    w->batch_lag = max_lag;
+    w->fpg = wf_frames_per_group(e, w);
+    // a deferred group must still fit the next block's window when its first frame leaves
+    if (w->batch_min > 1 && e->history < 2 * ((int64_t)w->fpg + 1) * w->hop + 2 * (int64_t)w->N) {
+        w->batch_min = old_min;
+        w->fpg = old_fpg;
+        set_last_error("owrx_waterfall_set_batch: engine history too short to batch (owrx_engine_create_ex)");
+        return OWRX_EINVAL;
+    }
+    RC_FAIL(e, wf_alloc_buffers(e, w));
     return OWRX_OK;
 }
 
@@ -2233,7 +2346,11 @@ int owrx_get_stats(owrx_engine* e, owrx_stats* s) {
     if (!s) return OWRX_EINVAL;
     *s = e->stats;
     int64_t dropped = 0;
-    for (auto& kv : e->chains) dropped += kv.second->audio.dropped;
+    for (auto& kv : e->chains) {
+        const Chain& c = *kv.second;
+        dropped += c.audio.dropped + c.smeter.dropped + c.sfft.dropped + c.tap_sel.dropped +
+                   c.tap_audio.dropped;
+    }
     for (auto& kv : e->wfs) dropped += kv.second->ring.dropped;
     s->overruns += dropped;
     return OWRX_OK;

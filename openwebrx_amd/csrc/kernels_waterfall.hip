@@ -956,6 +956,8 @@ static bool wf_force_r16() {
     return v;
 }
 
+bool wf_uses_l32(int logn) { return logn == 14 && !wf_force_r16(); }
+
 static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw,
                                  float* partial, hipStream_t st) {

@@ -37,10 +37,15 @@ def device_count():
 
 
 class Engine:
-    def __init__(self, samp_rate, max_block=1 << 20, device=0):
+    def __init__(self, samp_rate, max_block=1 << 20, device=0, history=None):
+        """history: samples of the stream kept readable before each block (None: the minimum,
+        2^18).  A waterfall batches frames across blocks (Waterfall.set_batch) only as far as
+        the history reaches; owrx_process_device callers must provide that much before each
+        block pointer."""
         h = ctypes.c_void_p()
-        check(lib.owrx_engine_create(device, float(samp_rate), int(max_block), ctypes.byref(h)),
-              "owrx_engine_create")
+        check(lib.owrx_engine_create_ex(device, float(samp_rate), int(max_block),
+                                        int(history or 0), ctypes.byref(h)),
+              "owrx_engine_create_ex")
         self._h = h
         self.samp_rate = samp_rate
         self.device = device
@@ -153,6 +158,13 @@ class Waterfall:
         check(lib.owrx_waterfall_set(self.engine.handle, self.id, int(every_n_samples),
                                      int(avg_number), 1 if adpcm else 0), "owrx_waterfall_set")
         self.adpcm = adpcm
+
+    def set_batch(self, min_frames, max_lag=0):
+        """Launch the FFT once `min_frames` frames are ready (or the oldest pending frame is
+        `max_lag` samples behind the newest block, or at sync): chip-filling launches at the
+        cost of row latency.  Call before streaming."""
+        check(lib.owrx_waterfall_set_batch(self.engine.handle, self.id, int(min_frames),
+                                           int(max_lag)), "owrx_waterfall_set_batch")
 
     def row_bytes(self):
         return check(lib.owrx_waterfall_row_bytes(self.engine.handle, self.id), "row_bytes")

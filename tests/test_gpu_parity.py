@@ -186,6 +186,70 @@ def test_waterfall_float_rows(amd, N, fs):
     assert np.max(err) < 2e-3, np.max(err)   # dB; fp32 FFT vs double
 
 
+def _wf_batched(amd, iq, fs, N, hop, avg, block, min_frames, history, ingest=False):
+    eng = amd.Engine(fs, max_block=block, history=history)
+    wf = eng.waterfall(N, hop, avg, adpcm=False)
+    wf.set_batch(min_frames)
+    for i in range(0, iq.size, block):
+        piece = iq[i:i + block]
+        if ingest:  # owrx_ingest_buffer / owrx_commit: the caller writes the ring slot
+            import ctypes
+            hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+            ptr, cap = eng.ingest_buffer()
+            assert cap >= piece.size
+            piece = np.ascontiguousarray(piece)
+            assert hip.hipMemcpy(ctypes.c_void_p(ptr), ctypes.c_void_p(piece.ctypes.data),
+                                 ctypes.c_size_t(8 * piece.size), 1) == 0  # host to device
+            eng.commit(piece.size)
+        else:
+            eng.push(piece)
+    st = eng.stats()
+    eng.sync()
+    rows = wf.read_rows()
+    st2 = eng.stats()
+    eng.close()
+    return rows, st, st2
+
+
+def test_waterfall_batched_launches(amd):
+    """owrx_waterfall_set_batch: frames of several blocks in one launch (rows out at the batch
+    or at sync).  The rows match the oracle as per-block launches do, are bit-identical for any
+    cut of the stream into blocks (the group size depends on the batch, not the blocks), the
+    engine launched far fewer FFTs than it processed blocks, and the push-path ring wrapped
+    (history 2^21 < the stream) without losing a sample."""
+    fs, N = 10000000, 16384
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+    avg = 6
+    from openwebrx_amd import synth
+    n = hop * avg * 7 + N
+    iq, _ = synth.make_iq(fs, n, ["nfm", "am", "usb"])
+    a, st, st2 = _wf_batched(amd, iq, fs, N, hop, avg, 1 << 16, 40, 1 << 21)
+    b, _, _ = _wf_batched(amd, iq, fs, N, hop, avg, 99991, 40, 1 << 21)
+    ref = np.stack([oracle.fftswap(r) for r in oracle.waterfall_rows(iq, N, hop, avg)])
+    assert a.shape == ref.shape and b.shape == ref.shape
+    assert np.max(np.abs(a - ref)) < 2e-3
+    assert np.array_equal(a, b)
+    blocks = (n + (1 << 16) - 1) >> 16
+    # 42 frames: one launch once >= 40 are ready (the rest, if any, at sync); per-block: 7
+    assert st["blocks"] == blocks and st["waterfall_launches"] == 1, st
+    assert 1 <= st2["waterfall_launches"] <= 2, st2
+    assert st2["waterfall_frames"] >= avg * ref.shape[0]
+    assert st2["waterfall_samples"] == st2["waterfall_frames"] * hop
+
+
+def test_engine_ring_ingest_commit(amd):
+    """The caller-written ring slot (owrx_ingest_buffer / owrx_commit, e.g. an RCCL broadcast)
+    gives the same rows as owrx_push_iq through the ring's wraps."""
+    fs, N = 2400000, 4096
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+    from openwebrx_amd import synth
+    n = hop * avg * 3 + N
+    iq, _ = synth.make_iq(fs, n, ["nfm"])
+    a, _, _ = _wf_batched(amd, iq, fs, N, hop, avg, 1 << 16, 0, 0)
+    b, _, _ = _wf_batched(amd, iq, fs, N, hop, avg, 1 << 16, 0, 0, ingest=True)
+    assert a.shape[0] == 3 and np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("variant", ["r16"])
 def test_waterfall_kernel_variants(variant):
     """The A/B waterfall kernel (OWRX_WF_KERNEL=r16: the radix-16 kernel at N = 16384 instead of
