@@ -241,10 +241,12 @@ typedef struct {
     double  gpu_ms_waterfall_fft; /* HIP-event time of the waterfall FFT + finalize launches
                                      alone (timing enabled), for the HBM roofline */
     int64_t waterfall_timed_samples; /* stream samples of the frames those timed launches did */
+    int64_t timed_blocks;      /* blocks whose kernel groups were timed (owrx_set_timing) */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
-/* 1 => record HIP events around each kernel group on the engine's streams */
-int owrx_set_timing(owrx_engine* e, int enable);
+/* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th
+ * block (the gpu_ms_* statistics average over those blocks); 0 => off */
+int owrx_set_timing(owrx_engine* e, int every_n_blocks);
 /* Form of the fused Shift + FirDecimate (csdr/chain/selector.py:11-35, :95, :132-140) every
  * chain group runs from the next block on.  Both compute y[k] = sum_t h[t] x[kD+t] e^{j phase}
  * exactly (fp32 rounding apart):

@@ -98,6 +98,7 @@ class Stats(ctypes.Structure):
         ("waterfall_samples", ctypes.c_int64),
         ("gpu_ms_waterfall_fft", ctypes.c_double),
         ("waterfall_timed_samples", ctypes.c_int64),
+        ("timed_blocks", ctypes.c_int64),
     ]
 
 

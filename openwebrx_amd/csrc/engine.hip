@@ -291,6 +291,14 @@ struct Chain {
     int64_t sf_row_bytes() const { return sf_adpcm ? (sf_n + 10) / 2 : 4 * (int64_t)sf_n; }
 };
 
+// one descriptor upload of copy_jobs (process_block)
+struct CopyJob {
+    void* dst;
+    const void* src;
+    int64_t bytes;
+};
+constexpr int kMaxCopyJobs = 64;
+
 struct Slot {  // one block's outputs in flight on streams B / C
     bool chains_pending = false;
     std::vector<int> post_ids;
@@ -323,6 +331,19 @@ struct Slot {  // one block's outputs in flight on streams B / C
     bool timed = false;
     bool timed_wf = false;
     bool timed_wff = false;
+    // the slot's chain descriptors (h_posts, lane lists) as last built: rebuilt only when the
+    // engine's chain epoch moved, the set of groups with outputs changed, or a one-shot reset
+    // (NoiseFilter / secondary FFT) was carried; per block only nk / k_begin are patched
+    uint64_t post_epoch = ~0ull;
+    bool post_dirty = true;
+    std::vector<const ChainGroup*> post_groups;
+    std::vector<int> group_post0;  // first post of each group of post_groups
+    int np = 0, nlong = 0, long_taps = 0, nfill = 0;
+    int64_t long_fd = 0;
+    uint32_t sf_sizes = 0;  // secondary FFT sizes (log2 bit set)
+    bool any_nr = false;
+    int nsel[3][2] = {}, off[3][2] = {};
+    CopyJob* h_jobs = nullptr;  // pinned job table of copy_jobs
 };
 
 struct RowSlot {  // one block's waterfall rows being encoded / copied on stream R
@@ -368,6 +389,25 @@ copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n
         reinterpret_cast<V*>(dst)[i] = reinterpret_cast<const V*>(src)[i];
     const int64_t t = nv * W + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && t < n) dst[t] = src[t];
+}
+
+// One block's descriptor uploads in one launch: job y copies its bytes (16 B per lane where
+// both ends are 16-B aligned) from pinned host memory to the device.
+__global__ void __launch_bounds__(256)
+copy_jobs(const CopyJob* __restrict__ jobs) {
+    const CopyJob j = jobs[blockIdx.y];
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if ((((uintptr_t)j.dst | (uintptr_t)j.src) & 15) == 0) {
+        const int64_t n16 = j.bytes >> 4;
+        for (int64_t i = t0; i < n16; i += stride)
+            reinterpret_cast<uint4*>(j.dst)[i] = reinterpret_cast<const uint4*>(j.src)[i];
+        for (int64_t i = (n16 << 4) + t0; i < j.bytes; i += stride)
+            static_cast<uint8_t*>(j.dst)[i] = static_cast<const uint8_t*>(j.src)[i];
+    } else {
+        for (int64_t i = t0; i < j.bytes; i += stride)
+            static_cast<uint8_t*>(j.dst)[i] = static_cast<const uint8_t*>(j.src)[i];
+    }
 }
 
 static hipError_t kcopy(void* dst, const void* src, size_t n, hipStream_t st) {
@@ -421,6 +461,14 @@ gather_outputs(const ChainPost* __restrict__ posts, const ChainCounts* __restric
 
 using namespace owrx;
 
+// One group's DDC work in a block (process_block)
+struct GroupWork {
+    ChainGroup* g;
+    int64_t k_end;
+    int nk;
+    bool fast;
+};
+
 struct owrx_engine {
     int device = 0;
     // A: waterfall FFT + DDC + post_parallel; B: post_serial_front; C: ADPCM + output copies;
@@ -441,7 +489,10 @@ struct owrx_engine {
     int64_t slot_tail = 0;  // oldest block whose outputs are not yet in the host rings
     bool failed = false;
     bool debug = false;
-    bool timing = false;
+    int timing = 0;                  // timing events every `timing` blocks (0: off)
+    std::vector<GroupWork> work;     // per-block scratch: the groups with outputs
+    std::vector<Chain*> nr_resets;   // NoiseFilter states to zero before the next serial work
+    uint64_t chain_epoch = 0;        // bumped by every change of a chain's post descriptor
     int ddc_mode = OWRX_DDC_FAST;
     std::recursive_mutex mu;
     // push-path ring: blocks are appended at wp with `history` samples before them; when the
@@ -761,6 +812,8 @@ static int ensure_post_capacity(owrx_engine* e) {
         HIPCHK(halloc(&s.h_counts, (size_t)cap));
         HIPCHK(halloc(&s.h_out, (size_t)e->out_total));
         HIPCHK(halloc(&s.h_sm, (size_t)cap * e->sm_stride));
+        if (!s.h_jobs) HIPCHK(halloc(&s.h_jobs, (size_t)kMaxCopyJobs));
+        s.post_dirty = true;
         if (e->debug) {
             HIPCHK(dalloc(&s.d_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
             HIPCHK(halloc(&s.h_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
@@ -1075,6 +1128,179 @@ static int wide_serial_chains() {
     return v;
 }
 
+// A slot's post descriptors (pinned S.h_posts), the lane lists of the serial kernels and the
+// long-bandpass list (S.h_sel), for the groups of e->work in that order; the per-block fields
+// (nk, k_begin, nseg) are patched by the caller.  One-shot flags (secondary FFT reset,
+// NoiseFilter reset) are consumed here, so the next use of this slot rebuilds without them.
+static int build_posts(owrx_engine* e, Slot& S, int si) {
+    S.post_ids.clear();
+    S.out_off.clear();
+    S.post_groups.clear();
+    S.group_post0.clear();
+    S.sf_sizes = 0;
+    S.any_nr = false;
+    bool one_shot = false;
+    int64_t out_off = 0;
+    int np = 0;
+    for (const GroupWork& gw : e->work) {
+        const ChainGroup* g = gw.g;
+        S.post_groups.push_back(g);
+        S.group_post0.push_back(np);
+        for (size_t i = 0; i < g->members.size(); ++i) {
+            Chain* c = e->chains[g->members[i]].get();
+            ChainPost& p = S.h_posts[np];
+            memset(&p, 0, sizeof(p));
+            const owrx_chain_params& q = c->prm;
+            p.demod = q.demod;
+            p.output = q.output;
+            p.frac_enabled = q.frac_rate != 1.0;
+            p.frac_rate = q.frac_rate;
+            p.bp_ntaps = q.bandpass ? c->bp_ntaps : 0;
+            p.bp_taps = c->d_bp_taps;
+            p.sq_len = q.sq_length;
+            p.sq_dec = q.sq_decimation;
+            p.sq_hang = q.sq_hang;
+            p.sq_flush = q.sq_flush;
+            p.sq_report = q.sq_report;
+            p.sq_level = q.sq_level;
+            p.deemph_alpha = nfm_deemphasis_alpha(q.audio_rate);
+            p.bp_hist = c->bp_hist;
+            p.bp_long = c->bp_hist > kBpHist ? 1 : 0;
+            if (q.demod == OWRX_DEMOD_WFM) {
+                // WfmDeemphasis(rate, tau): y += dt/(tau+dt) * (x - y) (csdr deemphasis_wfm_ff)
+                const double dt = 1.0 / (double)q.audio_rate;
+                const double tau = q.deemph_tau > 0 ? (double)q.deemph_tau : 50e-6;
+                p.deemph_alpha = (float)(dt / (tau + dt));
+                p.wfm_rate = q.if_rate / (double)q.audio_rate;
+                p.pf_taps = c->d_pf_taps;
+                p.pf_ntaps = c->pf_ntaps;
+                p.wf_buf = c->d_wf;
+                p.pf_buf = c->d_pf;
+            }
+            p.deemph_beta = 1.0f - p.deemph_alpha;
+            if (q.nr_enabled && c->d_nr_state && q.output != OWRX_OUT_IQ) {
+                if (c->nr_reset) {  // zeroed on the serial stream before this block's work
+                    e->nr_resets.push_back(c);
+                    c->nr_reset = false;
+                    one_shot = true;
+                }
+                p.nr_enabled = 1;
+                p.nr_t = (float)std::pow(10.0, (double)q.nr_threshold / 10.0);
+                p.nr_state = c->d_nr_state;
+                p.nr_in = c->d_nr_in;
+                p.nr_pow = c->d_nr_pow;
+                p.nr_ola = c->d_nr_ola;
+                p.nr_win = e->d_nr_win;
+                p.nr_tw = e->d_nr_tw;
+                S.any_nr = true;
+            }
+            p.agc = agc_profile(q.agc_profile);
+            if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
+            if (q.agc_max_gain >= 0) p.agc.max_gain = q.agc_max_gain;
+            if (q.demod == OWRX_DEMOD_WFM) p.agc.max_gain = std::max(1.0f, p.agc.max_gain);
+            p.pstate = c->d_pstate;
+            p.sstate = c->d_sstate;
+            p.ddc_buf = c->d_ddc;
+            p.fd_buf = c->d_fd;
+            p.sq_buf = c->d_sq;
+            p.dem = c->d_dem[si];
+            p.s16 = c->d_s16[si];
+            p.partial = g->d_partial[si];
+            p.nseg = gw.fast ? 1 : g->nseg;
+            p.group_chains = (int)g->members.size();
+            p.chain_in_group = (int)i;
+            p.k_first = c->k_first;
+            p.out = S.d_out + out_off;
+            p.out_cap = c->out_cap;
+            S.out_off.push_back(out_off);
+            out_off += out_region(c->out_cap);
+            if (c->sf_n > 0 && q.output != OWRX_OUT_IQ) {
+                p.sf_n = c->sf_n;
+                p.sf_hop = c->sf_hop;
+                p.sf_avg = std::max(1, c->sf_avg);
+                p.sf_adpcm = c->sf_adpcm;
+                p.sf_reset = c->sf_reset ? 1 : 0;
+                one_shot |= c->sf_reset;
+                c->sf_reset = false;
+                p.sf_corr = (float)((double)c->sf_add_db - 10.0 * std::log10((double)p.sf_avg));
+                p.sf_buf = c->d_sf;
+                p.sf_acc = c->d_sf_acc;
+                p.sf_window = c->d_sf_window;
+                p.sf_tw = c->d_sf_tw;
+                p.sf_out = S.d_out + out_off;
+                p.sf_out_cap = c->sf_out_cap;
+                S.sf_sizes |= 1u << c->sf_logn;
+            }
+            out_off += out_region(c->sf_out_cap);
+            if (c->tap_sq_cap > 0 && q.output != OWRX_OUT_IQ) {
+                p.tap_sq = (float2*)(S.d_out + out_off);
+                p.tap_sq_cap = c->tap_sq_cap / 8;
+            }
+            if (c->tap_agc_cap > 0 && q.output != OWRX_OUT_IQ) {
+                p.tap_agc = (float*)(S.d_out + out_off + out_region(c->tap_sq_cap));
+                p.tap_agc_cap = c->tap_agc_cap / 4;
+            }
+            out_off += c->tap_bytes();
+            p.smeter = S.d_sm + (int64_t)np * e->sm_stride;
+            p.smeter_cap = (int)e->sm_stride;
+            p.debug = (e->debug && S.d_dbg) ? 1 : 0;
+            if (p.debug) {
+                uint8_t* base = S.d_dbg + (int64_t)np * kDebugStages * e->dbg_stride;
+                p.dbg_ddc = (float2*)(base + 0 * e->dbg_stride);
+                p.dbg_fd = (float2*)(base + 1 * e->dbg_stride);
+                p.dbg_bp = (float2*)(base + 2 * e->dbg_stride);
+                p.dbg_sq = (float2*)(base + 3 * e->dbg_stride);
+                p.dbg_dem = (float*)(base + 4 * e->dbg_stride);
+                p.dbg_agc = (float*)(base + 5 * e->dbg_stride);
+                p.dbg_cap = e->dbg_stride / 8;
+            }
+            S.post_ids.push_back(g->members[i]);
+            np++;
+        }
+    }
+    S.np = np;
+    // long-bandpass chains (indices after the serial lane lists in the sel buffer)
+    S.nlong = 0;
+    S.long_taps = 0;
+    S.long_fd = 0;
+    S.long_off = e->post_cap + kSelPad;
+    for (int i = 0; i < np; ++i)
+        if (S.h_posts[i].bp_long && S.h_posts[i].output != OWRX_OUT_IQ) {
+            S.h_sel[S.long_off + S.nlong++] = i;
+            S.long_taps = std::max(S.long_taps, S.h_posts[i].bp_ntaps);
+            S.long_fd = std::max<int64_t>(S.long_fd, e->chains[S.post_ids[i]]->cap);
+        }
+    // one post_serial_front launch per output format present (S16 / ADPCM / F32); within a
+    // format the chains are ordered by demodulator and every demodulator's run is padded to
+    // whole 64-lane workgroups (-1 = idle lane), so each wave has a uniform demodulator; lists
+    // per (output, NoiseFilter): a NoiseFilter chain's front stores for chain_nr instead of
+    // converting; the two ADPCM lists are adjacent (one chain_adpcm launch)
+    std::vector<int>(&bk)[3][2][4] = e->sel_buckets;
+    for (auto& a : bk)
+        for (auto& b : a)
+            for (auto& v : b) v.clear();
+    for (int i = 0; i < np; ++i) {
+        const ChainPost& p = S.h_posts[i];
+        if (p.output >= 0 && p.output < 3 && p.demod >= 0 && p.demod < 4)
+            bk[p.output][p.nr_enabled != 0][p.demod].push_back(i);
+    }
+    int nfill = 0;
+    for (int o = 0; o < 3; ++o)
+        for (int nr = 0; nr < 2; ++nr) {
+            S.off[o][nr] = nfill;
+            for (int dm = 0; dm < 4; ++dm) {
+                const std::vector<int>& v = bk[o][nr][dm];
+                for (int i : v) S.h_sel[nfill++] = i;
+                for (size_t run = v.size(); run % 64; ++run) S.h_sel[nfill++] = -1;
+            }
+            S.nsel[o][nr] = nfill - S.off[o][nr];
+        }
+    S.nfill = nfill;
+    S.post_epoch = e->chain_epoch;
+    S.post_dirty = one_shot;
+    return OWRX_OK;
+}
+
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const double t_enter = now_ms();
     // Block k's host descriptors and push staging are indexed by block parity, so they need
@@ -1082,11 +1308,11 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     // wait for block k - 1 (whose input the caller may reuse once this call returns: the
     // owrx_process_device contract) comes at the end, after block k is built and enqueued, so
     // stream A runs block k - 1 while the host builds block k.  That order is the A/B option
-    // OWRX_IN_WAIT=end (+1-2 % at C3); the default waits before the build, the order every
-    // round-1/2 parity run used.
+    // default since round 3 (+1-2 % at C3 in round 2); OWRX_IN_WAIT=start waits before the
+    // build (the round-1/2 order, A/B).
     static const bool wait_first = [] {
         const char* v = getenv("OWRX_IN_WAIT");
-        return !(v && strcmp(v, "end") == 0);
+        return v && strcmp(v, "start") == 0;
     }();
     if (wait_first && e->in_pending) {
         HIPCHK(hipEventSynchronize(e->evIn[(e->block_index + 1) & 1]));
@@ -1104,28 +1330,19 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         RCCHK(drain_slots(e, true, kSlots - 1));
         e->stats.host_ms_wait_slots += now_ms() - t;
     }
-    const bool timed = e->timing;
+    const bool timed = e->timing > 0 && e->block_index % e->timing == 0;
+    if (timed) e->stats.timed_blocks++;
     if (timed) HIPCHK(hipEventRecord(S.a0, e->sA));
 
     // ---- waterfalls (stream A); row encoding + copy on the row slot's own stream
-    RCCHK(run_waterfalls(e, blk, blk_start, blk_end, false, timed, &S));
+    // (every waterfall launch is timed when timing is on: batched launches are rare)
+    RCCHK(run_waterfalls(e, blk, blk_start, blk_end, false, e->timing > 0, &S));
     e->last_blk = blk;
     e->last_start = blk_start;
     e->last_end = blk_end;
     // ---- chains: DDC per group (A); post_parallel + post_serial_front (B); ADPCM + copies (C)
-    e->posts.clear();
-    S.post_ids.clear();
-    S.out_off.clear();
-    int64_t out_off = 0;
-    struct GroupWork {
-        ChainGroup* g;
-        int64_t k_end;
-        int nk;
-        bool fast;
-    };
-    std::vector<GroupWork> work;
-    uint32_t sf_sizes = 0;  // secondary FFT sizes (log2 bit set) present this step
-    bool any_nr = false;    // a chain runs a NoiseFilter this step
+    std::vector<GroupWork>& work = e->work;
+    work.clear();
     for (auto& gp : e->groups) {  // descriptors first, so the DDC bracket holds only kernels
         ChainGroup* g = gp.get();
         if (g->members.empty()) continue;
@@ -1150,9 +1367,54 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             d.n0 = c->n0;
             d.P0 = c->P0;
         }
-        HIPCHK(kcopy(g->d_chains, g->h_chains[bp], sizeof(DdcChain) * g->members.size(), e->sA));
         work.push_back(GroupWork{g, k_end, (int)nk64,
                                  g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST});
+    }
+    // the slot's post descriptors and lane lists: as built for its last block unless a chain
+    // changed since (or the groups with outputs differ); then this block's nk / k_begin
+    bool same_groups = S.post_groups.size() == work.size();
+    for (size_t gi = 0; same_groups && gi < work.size(); ++gi) same_groups = S.post_groups[gi] == work[gi].g;
+    if (S.post_dirty || S.post_epoch != e->chain_epoch || !same_groups) RCCHK(build_posts(e, S, si));
+    for (size_t gi = 0; gi < work.size(); ++gi) {
+        const GroupWork& gw = work[gi];
+        ChainPost* p = S.h_posts + S.group_post0[gi];
+        const int nseg = gw.fast ? 1 : gw.g->nseg;
+        for (size_t i = 0; i < gw.g->members.size(); ++i) {
+            p[i].nk = gw.nk;
+            p[i].k_begin = gw.g->k_next;
+            p[i].nseg = nseg;
+        }
+    }
+    const int np = S.np;
+    // every descriptor of the block in one upload: the groups' DDC descriptors, the posts, the
+    // serial lane lists and the long-bandpass list (stream B / C read them after event evA)
+    {
+        int nj = 0;
+        int64_t maxb = 0;
+        auto job = [&](void* dst, const void* src, int64_t bytes) {
+            if (bytes <= 0) return;
+            S.h_jobs[nj++] = CopyJob{dst, src, bytes};
+            maxb = std::max(maxb, bytes);
+        };
+        for (const GroupWork& gw : work) {
+            if (nj >= kMaxCopyJobs - 3) {  // many groups: flush this table
+                hipLaunchKernelGGL(copy_jobs, dim3((unsigned)std::min<int64_t>(64, (maxb + 4095) / 4096), nj),
+                                   dim3(256), 0, e->sA, S.h_jobs);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipStreamSynchronize(e->sA));  // the table is reused right away
+                nj = 0;
+                maxb = 0;
+            }
+            job(gw.g->d_chains, gw.g->h_chains[bp], (int64_t)sizeof(DdcChain) * (int64_t)gw.g->members.size());
+        }
+        job(S.d_posts, S.h_posts, (int64_t)sizeof(ChainPost) * np);
+        job(S.d_sel, S.h_sel, (int64_t)sizeof(int) * S.nfill);
+        job(S.d_sel + S.long_off, S.h_sel + S.long_off, (int64_t)sizeof(int) * S.nlong);
+        if (nj > 0) {
+            hipLaunchKernelGGL(copy_jobs, dim3((unsigned)std::min<int64_t>(64, (maxb + 4095) / 4096), nj),
+                               dim3(256), 0, e->sA, S.h_jobs);
+            HIPCHK(hipGetLastError());
+        }
     }
     if (timed) {
         HIPCHK(hipEventRecord(S.a1, e->sA));
@@ -1186,150 +1448,18 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                               g->d_partial[si], e->sA));
         e->stats.ddc_launches++;
         if (gw.fast) e->stats.ddc_fast_launches++;
-        for (size_t i = 0; i < g->members.size(); ++i) {
-            Chain* c = e->chains[g->members[i]].get();
-            ChainPost p;
-            memset(&p, 0, sizeof(p));
-            const owrx_chain_params& q = c->prm;
-            p.demod = q.demod;
-            p.output = q.output;
-            p.frac_enabled = q.frac_rate != 1.0;
-            p.frac_rate = q.frac_rate;
-            p.bp_ntaps = q.bandpass ? c->bp_ntaps : 0;
-            p.bp_taps = c->d_bp_taps;
-            p.sq_len = q.sq_length;
-            p.sq_dec = q.sq_decimation;
-            p.sq_hang = q.sq_hang;
-            p.sq_flush = q.sq_flush;
-            p.sq_report = q.sq_report;
-            p.sq_level = q.sq_level;
-            p.deemph_alpha = nfm_deemphasis_alpha(q.audio_rate);
-            p.bp_hist = c->bp_hist;
-            p.bp_long = c->bp_hist > kBpHist ? 1 : 0;
-            if (q.demod == OWRX_DEMOD_WFM) {
-                // WfmDeemphasis(rate, tau): y += dt/(tau+dt) * (x - y) (csdr deemphasis_wfm_ff)
-                const double dt = 1.0 / (double)q.audio_rate;
-                const double tau = q.deemph_tau > 0 ? (double)q.deemph_tau : 50e-6;
-                p.deemph_alpha = (float)(dt / (tau + dt));
-                p.wfm_rate = q.if_rate / (double)q.audio_rate;
-                p.pf_taps = c->d_pf_taps;
-                p.pf_ntaps = c->pf_ntaps;
-                p.wf_buf = c->d_wf;
-                p.pf_buf = c->d_pf;
-            }
-            p.deemph_beta = 1.0f - p.deemph_alpha;
-            if (q.nr_enabled && c->d_nr_state && q.output != OWRX_OUT_IQ) {
-                if (c->nr_reset) {  // a fresh NoiseFilter (ClientAudioChain._updateConverter)
-                    // on the serial stream in use (a switch orders the other one behind it)
-                    hipStream_t sb = e->serial_wide ? e->sBw : e->sB;
-                    HIPCHK(hipMemsetAsync(c->d_nr_state, 0, sizeof(NrState), sb));
-                    HIPCHK(hipMemsetAsync(c->d_nr_in, 0, sizeof(float) * kNrHop, sb));
-                    HIPCHK(hipMemsetAsync(c->d_nr_pow, 0, sizeof(float) * 2 * (kNrN / 2 + 1), sb));
-                    HIPCHK(hipMemsetAsync(c->d_nr_ola, 0, sizeof(float) * kNrHop, sb));
-                    c->nr_reset = false;
-                }
-                p.nr_enabled = 1;
-                p.nr_t = (float)std::pow(10.0, (double)q.nr_threshold / 10.0);
-                p.nr_state = c->d_nr_state;
-                p.nr_in = c->d_nr_in;
-                p.nr_pow = c->d_nr_pow;
-                p.nr_ola = c->d_nr_ola;
-                p.nr_win = e->d_nr_win;
-                p.nr_tw = e->d_nr_tw;
-                any_nr = true;
-            }
-            p.agc = agc_profile(q.agc_profile);
-            if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
-            if (q.agc_max_gain >= 0) p.agc.max_gain = q.agc_max_gain;
-            if (q.demod == OWRX_DEMOD_WFM) p.agc.max_gain = std::max(1.0f, p.agc.max_gain);
-            p.pstate = c->d_pstate;
-            p.sstate = c->d_sstate;
-            p.ddc_buf = c->d_ddc;
-            p.fd_buf = c->d_fd;
-            p.sq_buf = c->d_sq;
-            p.dem = c->d_dem[si];
-            p.s16 = c->d_s16[si];
-            p.partial = g->d_partial[si];
-            p.nseg = gw.fast ? 1 : g->nseg;
-            p.group_chains = (int)g->members.size();
-            p.chain_in_group = (int)i;
-            p.nk = nk;
-            p.k_begin = g->k_next;
-            p.k_first = c->k_first;
-            const int slot = (int)e->posts.size();
-            p.out = S.d_out + out_off;
-            p.out_cap = c->out_cap;
-            S.out_off.push_back(out_off);
-            out_off += out_region(c->out_cap);
-            if (c->sf_n > 0 && q.output != OWRX_OUT_IQ) {
-                p.sf_n = c->sf_n;
-                p.sf_hop = c->sf_hop;
-                p.sf_avg = std::max(1, c->sf_avg);
-                p.sf_adpcm = c->sf_adpcm;
-                p.sf_reset = c->sf_reset ? 1 : 0;
-                c->sf_reset = false;
-                p.sf_corr = (float)((double)c->sf_add_db - 10.0 * std::log10((double)p.sf_avg));
-                p.sf_buf = c->d_sf;
-                p.sf_acc = c->d_sf_acc;
-                p.sf_window = c->d_sf_window;
-                p.sf_tw = c->d_sf_tw;
-                p.sf_out = S.d_out + out_off;
-                p.sf_out_cap = c->sf_out_cap;
-                sf_sizes |= 1u << c->sf_logn;
-            }
-            out_off += out_region(c->sf_out_cap);
-            if (c->tap_sq_cap > 0 && q.output != OWRX_OUT_IQ) {
-                p.tap_sq = (float2*)(S.d_out + out_off);
-                p.tap_sq_cap = c->tap_sq_cap / 8;
-            }
-            if (c->tap_agc_cap > 0 && q.output != OWRX_OUT_IQ) {
-                p.tap_agc = (float*)(S.d_out + out_off + out_region(c->tap_sq_cap));
-                p.tap_agc_cap = c->tap_agc_cap / 4;
-            }
-            out_off += c->tap_bytes();
-            p.smeter = S.d_sm + (int64_t)slot * e->sm_stride;
-            p.smeter_cap = (int)e->sm_stride;
-            p.debug = (e->debug && S.d_dbg) ? 1 : 0;
-            if (p.debug) {
-                uint8_t* base = S.d_dbg + (int64_t)slot * kDebugStages * e->dbg_stride;
-                p.dbg_ddc = (float2*)(base + 0 * e->dbg_stride);
-                p.dbg_fd = (float2*)(base + 1 * e->dbg_stride);
-                p.dbg_bp = (float2*)(base + 2 * e->dbg_stride);
-                p.dbg_sq = (float2*)(base + 3 * e->dbg_stride);
-                p.dbg_dem = (float*)(base + 4 * e->dbg_stride);
-                p.dbg_agc = (float*)(base + 5 * e->dbg_stride);
-                p.dbg_cap = e->dbg_stride / 8;
-            }
-            e->posts.push_back(p);
-            S.post_ids.push_back(g->members[i]);
-        }
         g->k_next = k_end;
     }
-    const int np = (int)e->posts.size();
     if (timed) HIPCHK(hipEventRecord(S.a2, e->sA));
     if (np > 0) {
         // stream A: post_parallel (wide); stream B: post_serial_front (serial, own CUs)
-        memcpy(S.h_posts, e->posts.data(), sizeof(ChainPost) * np);
-        // long-bandpass chains (indices after the serial lane lists in the sel buffer)
-        int nlong = 0, long_taps = 0;
-        int64_t long_fd = 0;
-        S.long_off = e->post_cap + kSelPad;
-        for (int i = 0; i < np; ++i)
-            if (e->posts[i].bp_long && e->posts[i].output != OWRX_OUT_IQ) {
-                S.h_sel[S.long_off + nlong++] = i;
-                long_taps = std::max(long_taps, e->posts[i].bp_ntaps);
-                long_fd = std::max<int64_t>(long_fd, e->chains[S.post_ids[i]]->cap);
-            }
-        HIPCHK(kcopy(S.d_posts, S.h_posts, sizeof(ChainPost) * np, e->sA));
         if (timed) HIPCHK(hipEventRecord(S.b0, e->sA));
         HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
-        if (nlong > 0) {  // long bandpass chains: bp_long + post_tail (after post_parallel)
-            HIPCHK(kcopy(S.d_sel + S.long_off, S.h_sel + S.long_off, sizeof(int) * nlong, e->sA));
-            HIPCHK(launch_post_long(S.d_posts, S.d_counts, S.d_sel + S.long_off, nlong, long_fd,
-                                    long_taps, e->sA));
-        }
+        if (S.nlong > 0)  // long bandpass chains: bp_long + post_tail (after post_parallel)
+            HIPCHK(launch_post_long(S.d_posts, S.d_counts, S.d_sel + S.long_off, S.nlong, S.long_fd,
+                                    S.long_taps, e->sA));
         for (int lg = 0; lg < 32; ++lg)
-            if (sf_sizes & (1u << lg)) HIPCHK(launch_chain_sfft(lg, S.d_posts, np, S.d_counts, e->sA));
+            if (S.sf_sizes & (1u << lg)) HIPCHK(launch_chain_sfft(lg, S.d_posts, np, S.d_counts, e->sA));
         HIPCHK(hipEventRecord(S.evA, e->sA));
         // serial streams for this block: the CU-masked pair, or past kWideSerialChains chains
         // (more waves than their CUs hold) the unmasked pair; on a switch the new pair first
@@ -1349,47 +1479,26 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             e->serial_wide = wide;
         }
         HIPCHK(hipStreamWaitEvent(sB, S.evA, 0));
-        // one post_serial_front launch per output format present (S16 / ADPCM / F32); within
-        // a format the chains are ordered by demodulator and every demodulator's run is padded
-        // to whole 64-lane workgroups (-1 = idle lane), so each wave has a uniform demodulator
-        // lists per (output, NoiseFilter): a NoiseFilter chain's front stores for chain_nr
-        // instead of converting; the two ADPCM lists are adjacent (one chain_adpcm launch)
-        int nsel[3][2] = {}, off[3][2] = {};
-        int nfill = 0;
-        {
-            // one pass: bucket the posts by (output, NoiseFilter, demodulator), in index order
-            std::vector<int>(&bk)[3][2][4] = e->sel_buckets;
-            for (auto& a : bk)
-                for (auto& b : a)
-                    for (auto& v : b) v.clear();
-            for (int i = 0; i < np; ++i) {
-                const ChainPost& p = e->posts[i];
-                if (p.output >= 0 && p.output < 3 && p.demod >= 0 && p.demod < 4)
-                    bk[p.output][p.nr_enabled != 0][p.demod].push_back(i);
-            }
-            for (int o = 0; o < 3; ++o)
-                for (int nr = 0; nr < 2; ++nr) {
-                    off[o][nr] = nfill;
-                    for (int dm = 0; dm < 4; ++dm) {
-                        const std::vector<int>& v = bk[o][nr][dm];
-                        for (int i : v) S.h_sel[nfill++] = i;
-                        for (size_t run = v.size(); run % 64; ++run) S.h_sel[nfill++] = -1;
-                    }
-                    nsel[o][nr] = nfill - off[o][nr];
-                }
+        // NoiseFilter resets the rebuild asked for (a fresh NoiseFilter: ClientAudioChain.
+        // _updateConverter), on the serial stream in use, before this block's serial work
+        for (Chain* c : e->nr_resets) {
+            HIPCHK(hipMemsetAsync(c->d_nr_state, 0, sizeof(NrState), sB));
+            HIPCHK(hipMemsetAsync(c->d_nr_in, 0, sizeof(float) * kNrHop, sB));
+            HIPCHK(hipMemsetAsync(c->d_nr_pow, 0, sizeof(float) * 2 * (kNrN / 2 + 1), sB));
+            HIPCHK(hipMemsetAsync(c->d_nr_ola, 0, sizeof(float) * kNrHop, sB));
         }
-        HIPCHK(kcopy(S.d_sel, S.h_sel, sizeof(int) * nfill, sB));
+        e->nr_resets.clear();
         const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
         for (int o = 0; o < 3; ++o)
             for (int nr = 0; nr < 2; ++nr)
-                HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + off[o][nr],
-                                          nsel[o][nr], o, dbg, nr, sB));
-        if (any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, sB));
+                HIPCHK(launch_post_serial(S.d_posts, S.d_counts, S.d_sel + S.off[o][nr],
+                                          S.nsel[o][nr], o, dbg, nr, sB));
+        if (S.any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, sB));
         HIPCHK(hipEventRecord(S.evF, sB));
         // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host
         HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
-        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + off[1][0],
-                                  nsel[1][0] + nsel[1][1], sC));
+        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + S.off[1][0],
+                                  S.nsel[1][0] + S.nsel[1][1], sC));
         if (timed) HIPCHK(hipEventRecord(S.b1, sC));
         // the copies to host go on stream R (behind this block's encoder), so stream C runs
         // encoders back to back: its kernel is the pipeline's longest serial stage
@@ -1616,6 +1725,7 @@ int owrx_engine_destroy(owrx_engine* e) {
         if (ev) hipEventDestroy(ev);
     for (auto& s : e->slots) {
         free_slot_staging(s);
+        hfree(s.h_jobs);
         for (hipEvent_t ev : {s.evA, s.evF, s.evB, s.evC, s.a0, s.a1, s.a2, s.a3, s.b0, s.b1, s.m0, s.m1,
                               s.w0, s.w1})
             if (ev) hipEventDestroy(ev);
@@ -1942,6 +2052,7 @@ static int chain_set_bandpass_taps(owrx_engine* e, Chain* c) {
 
 int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     if (!handle || chain_validate(p)) {
         set_last_error("owrx_chain_create: invalid chain parameters");
         return OWRX_EINVAL;
@@ -2099,6 +2210,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
 
 int owrx_chain_destroy(owrx_engine* e, int handle) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     RC_FAIL(e, drain_all(e));
@@ -2135,6 +2247,7 @@ int owrx_chain_set_shift_rate(owrx_engine* e, int handle, float rate) {
 
 int owrx_chain_set_bandpass(owrx_engine* e, int handle, int enabled, float low, float high) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     Chain* c = it->second.get();
@@ -2149,6 +2262,7 @@ int owrx_chain_set_bandpass(owrx_engine* e, int handle, int enabled, float low, 
 
 int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     it->second->prm.sq_level = level;
@@ -2157,6 +2271,7 @@ int owrx_chain_set_squelch_level(owrx_engine* e, int handle, float level) {
 
 int owrx_chain_set_noise_filter(owrx_engine* e, int handle, int enabled, float threshold_db) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || it->second->prm.output == OWRX_OUT_IQ) return OWRX_EINVAL;
     Chain* c = it->second.get();
@@ -2213,6 +2328,7 @@ int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float
 
 int owrx_chain_set_taps(owrx_engine* e, int handle, int selector, int audio) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     Chain* c = it->second.get();
@@ -2245,6 +2361,7 @@ int64_t owrx_chain_read_tap(owrx_engine* e, int handle, int which, uint8_t* dst,
 int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int every_n_samples,
                                  int avg_number, float add_db, int adpcm) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     Chain* c = it->second.get();
@@ -2325,6 +2442,7 @@ int64_t owrx_chain_origin(owrx_engine* e, int handle) {
 
 int owrx_set_debug(owrx_engine* e, int enable) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     RC_FAIL(e, drain_all(e));
     e->debug = enable != 0;
     e->post_cap = 0;  // force reallocation with debug staging
@@ -2358,6 +2476,7 @@ int owrx_get_stats(owrx_engine* e, owrx_stats* s) {
 
 int owrx_set_ddc_mode(owrx_engine* e, int mode) {
     ENGINE_GUARD(e);
+    e->chain_epoch++;  // the slots rebuild their post descriptors
     if (mode != OWRX_DDC_FAST && mode != OWRX_DDC_DIRECT) return OWRX_EINVAL;
     e->ddc_mode = mode;
     return OWRX_OK;
@@ -2365,7 +2484,7 @@ int owrx_set_ddc_mode(owrx_engine* e, int mode) {
 
 int owrx_set_timing(owrx_engine* e, int enable) {
     ENGINE_GUARD(e);
-    e->timing = enable != 0;
+    e->timing = std::max(0, enable);
     return OWRX_OK;
 }
 

@@ -109,8 +109,9 @@ class Engine:
         """DDC form: "fast" (fast-convolution filter bank, default) or "direct" (polyphase FIR)."""
         check(lib.owrx_set_ddc_mode(self._h, {"fast": 0, "direct": 1}[mode]), "owrx_set_ddc_mode")
 
-    def set_timing(self, on=True):
-        check(lib.owrx_set_timing(self._h, 1 if on else 0), "owrx_set_timing")
+    def set_timing(self, on=True, every=1):
+        """HIP-event timing of the kernel groups in every `every`-th block (off: on=False)."""
+        check(lib.owrx_set_timing(self._h, int(every) if on else 0), "owrx_set_timing")
 
     def stats(self):
         s = _lib.Stats()

@@ -194,7 +194,9 @@ def _wf_batched(amd, iq, fs, N, hop, avg, block, min_frames, history, ingest=Fal
         piece = iq[i:i + block]
         if ingest:  # owrx_ingest_buffer / owrx_commit: the caller writes the ring slot
             import ctypes
-            hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+            # the HIP runtime this process already loaded (torch may bring its own build)
+            path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+            hip = ctypes.CDLL(path)
             ptr, cap = eng.ingest_buffer()
             assert cap >= piece.size
             piece = np.ascontiguousarray(piece)
