@@ -1,20 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: the OpenWebRX IQ hot path on MI355X (BASELINE.json metric).
 
-Workload (N=1): BASELINE config 2 -- 10 Msps synthetic cf32 IQ -> 16384-bin waterfall
-(FftChain: fps 9, v-overlap 0.3 -> avg 97, hop 11454, ADPCM rows) + 32 client chains
-(16 NFM + 16 AM ClientDemodulatorChain: Shift -> FirDecimate(833, 22223 taps) ->
-FractionalDecimator -> Bandpass -> Squelch -> demod -> Agc -> Convert -> AdpcmEncoder(sync)).
-`--config c3|c4|c5` runs the other BASELINE shapes per GPU (256 NFM/USB/CW chains; 61.44 Msps
-with a 65536-bin waterfall and 128 chains; 64 USB chains with NoiseFilter) for reference; the
-metric line is config 2.
-A step is one block of `--block` IQ samples pushed through all of it, inputs resident in HBM,
-outputs (waterfall rows, ADPCM audio, s-meter) copied back to host rings and drained.
+Workload (N=1, default `--config c3`, BASELINE config 3 = the north_star target on one GPU):
+10 Msps synthetic cf32 IQ -> 16384-bin waterfall (FftChain: fps 9, v-overlap 0.3 -> avg 97,
+hop 11454, ADPCM rows) + 256 client chains (86 NFM + 85 USB + 85 CW ClientDemodulatorChain:
+Shift -> FirDecimate(833, 22223 taps) -> FractionalDecimator -> Bandpass -> Squelch -> demod ->
+Agc -> Convert -> AdpcmEncoder(sync)).  `--config c2|c4|c5` runs the other BASELINE shapes per
+GPU (32 NFM/AM chains; 61.44 Msps with a 65536-bin waterfall and 128 chains; 64 USB chains with
+NoiseFilter).
+A step is one block of `--block` IQ samples (default 2^20) pushed through all of
+it, inputs resident in HBM, outputs (waterfall rows, ADPCM audio, s-meter) copied back to host
+rings and drained.  The waterfall FFT launches once per `--wf-batch` frames (owrx_waterfall_
+set_batch; four per stream-A CU by default), not once per block.
 
 N>1 (torchrun, one rank per GPU): rank 0 owns the stream and broadcasts each block over RCCL
-(the path's one exchange step); every rank runs its own 32 chains (weak scaling:
-per-GPU work fixed), rank 0 also the waterfall.  value = aggregate IQ samples demodulated by all
-ranks' 32-chain groups per second (= stream Msps x N).
+(the path's one exchange step); every rank runs its own chains (weak scaling:
+per-GPU work fixed), rank 0 also the waterfall.  value = the ingested stream's Msps (one stream
+at any N); chains_total and chain_msamples_per_s give the aggregate chain work.
 """
 import argparse
 import json
@@ -428,7 +430,7 @@ def main():
           % (host_s["process"], host_s["drain"], dt), file=sys.stderr)
     print("step marks (ms): " + " ".join("%.2f" % (1e3 * m) for m in marks), file=sys.stderr)
     samples = args.steps * block
-    value = world * samples / dt / 1e6
+    value = samples / dt / 1e6  # the one ingested stream, at any N (chains scale with N)
     ms_step = dt * 1e3 / args.steps
     # DDC work: the fast-convolution GEMM (fc_mac) is the dominant kernel of the chain path;
     # achieved = its algorithmic flop per launch / its average launch time (HIP events on the
@@ -502,10 +504,11 @@ def main():
                 "parallelism": "1 GPU" if world == 1 else
                 "IQ broadcast over RCCL from rank 0, %d chains per rank" % C,
             },
-            "value_definition": ("wideband IQ Msamples/s processed summed over the GPUs: each GPU "
-                                 "runs the whole stream (waterfall on GPU 0) for its own %d chains, "
-                                 "so at N GPUs this is N x the single-stream rate below; ONE stream "
-                                 "is ingested (iq_msps_stream)" % C),
+            "value_definition": ("Msamples/s of the ONE wideband IQ stream ingested, at any N: "
+                                 "each GPU runs the whole stream (broadcast from rank 0; waterfall "
+                                 "on GPU 0) for its own %d chains, so the chain work scales with N "
+                                 "(chains_total, chain_msamples_per_s) while the ingested rate "
+                                 "does not" % C),
             "iq_msps_stream": round(samples / dt / 1e6, 2),
             "chain_msamples_per_s": round(C * world * samples / dt / 1e6, 1),
             "realtime_factor": round(samples / dt / fs, 1),

@@ -881,7 +881,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     if constexpr (T2) adpcm_tab2_fill(NS, threadIdx.x, 128);
-    else adpcm_tab_fill(NS, threadIdx.x, 128);
+    else adpcm_tab_fill(NS, threadIdx.x, 128);  // (array references: the extent is checked)
     const SerLane sl = ser_lane(sel, nsel);
     const int c = sl.c;
     const ChainPost* Pp = posts + c;

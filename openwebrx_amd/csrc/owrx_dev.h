@@ -237,7 +237,11 @@ OWRX_DEV uint32_t adpcm_tab_rec(int index) {
     return (uint32_t)kAdpcmStep[index] | ((uint32_t)(index * 8) << 16);
 }
 
-OWRX_DEV void adpcm_tab_fill(uint32_t* NS, int tid, int nthreads) {
+// The tables are filled through references to arrays, so a table declared smaller than the
+// fill cannot compile (commits dd5bbb0..dfdd34f had an 89 x 8 LDS array under the 89 x 16 fill).
+template <int EXT>
+OWRX_DEV void adpcm_tab_fill(uint32_t (&NS)[EXT], int tid, int nthreads) {
+    static_assert(EXT >= kAdpcmTabEntries, "successor table too small");
     for (int e = tid; e < kAdpcmTabEntries; e += nthreads) {
         const int i = e >> 3, m = e & 7;
         int ni = i + kAdpcmIndex[m];
@@ -285,7 +289,9 @@ OWRX_DEV int adpcm_encode_tab(AdpcmTab& s, int sample, const uint32_t* __restric
 // adpcm_encode.
 constexpr int kAdpcmTab2Entries = 89 * 16;
 
-OWRX_DEV void adpcm_tab2_fill(uint32_t* NS2, int tid, int nthreads) {
+template <int EXT>
+OWRX_DEV void adpcm_tab2_fill(uint32_t (&NS2)[EXT], int tid, int nthreads) {
+    static_assert(EXT >= kAdpcmTab2Entries, "byte-addressed successor table too small");
     for (int e = tid; e < kAdpcmTab2Entries; e += nthreads) {
         const int i = e >> 4, m = e & 7;
         int ni = i + kAdpcmIndex[m];

@@ -126,16 +126,31 @@ class Engine:
         n = len(chains)
         handles = np.fromiter((c.id for c in chains), dtype=np.int32, count=n)
         alens = np.zeros(n, np.int64)
-        scounts = np.zeros(n, np.int64)
         abuf = _scratch(max_bytes)
         na = check(lib.owrx_chains_read_audio(self._h, n, handles.ctypes.data_as(_lib._pi32),
                                               abuf.ctypes.data, max_bytes,
                                               alens.ctypes.data_as(_lib._pi64)), "read_chains")
-        sbuf = np.empty(max_values, np.float32)
-        ns = check(lib.owrx_chains_read_smeter(self._h, n, handles.ctypes.data_as(_lib._pi32),
-                                               sbuf.ctypes.data, max_values,
-                                               scounts.ctypes.data_as(_lib._pi64)), "read_chains")
-        return abuf[:na], alens, sbuf[:ns], scounts
+        # s-meter values: a call that fills the buffer leaves the later chains' values in their
+        # rings; read again until a call comes back short, then put each chain's pieces together
+        rounds = []
+        while True:
+            sbuf = np.empty(max_values, np.float32)
+            cnt = np.zeros(n, np.int64)
+            ns = check(lib.owrx_chains_read_smeter(self._h, n, handles.ctypes.data_as(_lib._pi32),
+                                                   sbuf.ctypes.data, max_values,
+                                                   cnt.ctypes.data_as(_lib._pi64)), "read_chains")
+            rounds.append((sbuf[:ns], cnt))
+            if ns < max_values:
+                break
+        if len(rounds) == 1:
+            return abuf[:na], alens, rounds[0][0], rounds[0][1]
+        offs = [np.concatenate(([0], np.cumsum(c)[:-1])) for _, c in rounds]
+        parts = []
+        for i in range(n):
+            for (buf, c), o in zip(rounds, offs):
+                parts.append(buf[o[i]:o[i] + c[i]])
+        scounts = sum(c for _, c in rounds)
+        return abuf[:na], alens, np.concatenate(parts) if parts else np.empty(0, np.float32), scounts
 
     def waterfall(self, fft_size, every_n_samples, avg_number, add_db=-70.0, adpcm=True):
         return Waterfall(self, fft_size, every_n_samples, avg_number, add_db, adpcm)

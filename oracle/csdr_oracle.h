@@ -108,11 +108,12 @@ int64_t orc_run_chains_parallel(const float* iq, int64_t n, const orc_chain_para
 int64_t orc_run_workload(const float* iq, int64_t n, int N, int hop, int avg, float add_db,
                          const orc_chain_params* p, int nchains, int nthreads);
 
-#ifdef __cplusplus
-}
-#endif
 void orc_fir_real(const float* in, int64_t n, const float* taps, int ntaps, float* out);
 int64_t orc_fractional_decimator_f(const float* in, int64_t n, double rate, float* out);
 float orc_wfm_deemphasis_alpha(int sample_rate, float tau);
 int64_t orc_noise_filter(const float* in, int64_t n, float threshold_db, float* out);
+
+#ifdef __cplusplus
+}
+#endif
 #endif

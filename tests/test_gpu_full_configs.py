@@ -65,7 +65,9 @@ def _waterfall_full(amd, fs, N, avg_expected, nrows, block, parity_report, name,
     parity_report(name, bins=N, avg=avg, rows=nrows, max_db_err=err_db,
                   int16_exact_fraction=exact, int16_max_lsb=int(d.max()))
     assert d.max() <= 1, int(d.max())
-    assert exact > 0.95, exact
+    # measured 0.9996-0.9997 at C2 / C4 full averaging (fp32 FFT vs the double oracle at the
+    # (short)(dB * 100) truncation boundary); the floor sits just under it so a regression shows
+    assert exact > 0.999, exact
     for r in range(nrows):  # the GPU encoder over the GPU rows: bit-exact
         assert ra[r].tobytes() == oracle.fft_adpcm_row(rf[r]), r
     return iq

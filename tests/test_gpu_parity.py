@@ -606,8 +606,8 @@ def test_ddc_fast_convolution_frame_lengths(amd, m, monkeypatch):
 
 def test_ddc_fast_convolution_membership_churn(amd):
     """Chains leaving a fast-convolution group mid-stream: the last member takes the freed slot
-    of the group's filter-spectra matrix (swap-remove) and a retuned chain gets rebuilt spectra;
-    the surviving chains' DDC output over the whole stream still equals the oracle's."""
+    of the group's filter-spectra matrix (swap-remove); the surviving chains' DDC output over the
+    whole stream still equals the oracle's."""
     from openwebrx_amd import synth
     fs = 2400000
     modes = [("nfm", "am", "usb", "cw")[c % 4] for c in range(40)]
@@ -630,6 +630,50 @@ def test_ddc_fast_convolution_membership_churn(amd):
         got = chains[c].read_debug(0)
         assert got.size == ref["ddc"].size, (c, got.size, ref["ddc"].size)
         assert rel_rms(got, ref["ddc"]) < 1e-5, (c, rel_rms(got, ref["ddc"]))
+    eng.close()
+
+
+def test_retune_after_swap_remove(amd):
+    """A chain that swap-remove moved into a freed slot of its group's filter-spectra matrix,
+    then retuned (Shift.setRate): its spectra are rebuilt at that slot (fc_build_w after the
+    move), and its DDC output follows the piecewise phase like test_retune_is_phase_continuous."""
+    from openwebrx_amd import synth
+    fs, B = 2400000, 1 << 17
+    modes = [("nfm", "usb")[c % 2] for c in range(8)]
+    iq, offs = synth.make_iq(fs, 6 * B, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16) for o, m in zip(offs, modes)]
+    eng = amd.Engine(fs, max_block=B)
+    eng.set_debug(True)
+    chains = [eng.chain(p) for p in plist]
+    eng.push(iq[:2 * B])
+    chains[2].close()  # chain 7 (the last member) moves into slot 2
+    eng.push(iq[2 * B:3 * B])
+    new_rate = amd.params.f32(amd.params.shift_rate(offs[1] + 2500.0, fs))
+    chains[7].set_shift_rate(new_rate)
+    eng.push(iq[3 * B:])
+    eng.sync()
+    p = plist[7]
+    got = chains[7].read_debug(0)
+    c = oracle.chain_from_engine_params(p)
+    T, D = c.ntaps, p.decimation
+    nb = ((3 * B - T) // D + 1) * D  # first input sample of the first output after the retune
+    n = np.arange(iq.size, dtype=np.uint64)
+    f0, f1 = np.uint64(_rate_fx(p.shift_rate)), np.uint64(_rate_fx(new_rate))
+    with np.errstate(over="ignore"):
+        ph = np.where(n < nb, (n + np.uint64(1)) * f0,
+                      np.uint64(nb) * f0 + (n - np.uint64(nb) + np.uint64(1)) * f1)
+    turns = ph.astype(np.float64) / 18446744073709551616.0
+    x = (iq.astype(np.complex128) * np.exp(2j * np.pi * turns)).astype(np.complex64)
+    ref = oracle.fir_decimate(x, c._keep[0], D)
+    k = nb // D
+    old = oracle.fir_decimate(oracle.shift(iq, p.shift_rate), c._keep[0], D)
+    assert got.size == ref.size, (got.size, ref.size)
+    assert rel_rms(got[:k], old[:k]) < 1e-5
+    assert rel_rms(got[k:], ref[k:]) < 1e-5
+    for i in (0, 1, 3, 6):  # the other members are untouched
+        r = oracle.stages(iq, plist[i])["ddc"]
+        g = chains[i].read_debug(0)
+        assert g.size == r.size and rel_rms(g, r) < 1e-5, i
     eng.close()
 
 

@@ -135,6 +135,58 @@ def test_buffer_multireader_and_stop():
     assert got == [None]
 
 
+def test_reader_stop_drops_unread_bytes():
+    """Reader.stop() (csdr/module/__init__.py:36-53 pumps exit on None): read() returns None at
+    once, whatever the buffer still holds for this reader -- unread bytes are dropped, which is
+    the mechanism behind round 2's truncated collector (r02ag: a collector stopped right after
+    the engine finished).  resume() re-arms it and the held bytes come back."""
+    b = M.Buffer(Format.CHAR)
+    r = b.getReader()
+    b.write(b"abcdef")
+    assert bytes(r.read()) == b"abcdef"
+    b.write(b"ghij")
+    r.stop()
+    assert r.available() == 4
+    assert r.read() is None  # stopped: the 4 pending bytes are not returned
+    r.resume()
+    assert bytes(r.read()) == b"ghij"
+
+
+def test_collector_stopped_after_draining_sees_every_byte():
+    """A collector thread behind a fast writer: stopped without draining it loses the tail (the
+    r02ag symptom); stopped once available() is 0 (_stop_collector) it sees every byte, in order."""
+    payload = [bytes([i % 251]) * (1 + (i * 7) % 300) for i in range(2000)]
+    total = b"".join(payload)
+
+    def run(drain):
+        b = M.Buffer(Format.CHAR, size=1 << 22)
+        r = b.getReader()
+        out = []
+        slow = threading.Event()
+
+        def collect():
+            for x in iter(r.read, None):
+                out.append(bytes(x))
+                if not slow.is_set():
+                    time.sleep(0.1)  # behind the writer at first
+                    slow.set()
+        t = threading.Thread(target=collect)
+        t.start()
+        for p in payload:
+            b.write(p)
+        if drain:
+            deadline = time.time() + 5
+            while r.available() > 0 and time.time() < deadline:
+                time.sleep(0.002)
+        r.stop()
+        t.join(5)
+        return b"".join(out)
+
+    assert run(True) == total
+    got = run(False)
+    assert total.startswith(got) and len(got) < len(total)
+
+
 def test_format_mismatch_raises_valueerror():
     """setReader / setWriter raise ValueError (callers catch it, csdr/chain/__init__.py:60-84)."""
     with pytest.raises(ValueError):
