@@ -98,11 +98,14 @@ _T0 = time.perf_counter()
 
 
 def cpu_baseline(fs, n_fft, hop, avg, plist):
-    """The CPU baseline: oracle/cpu_baseline.c -- the same waterfall + chains
-    with the costly stages in fp32 / AVX2-FMA like csdr (Shift + FirDecimate, waterfall FFT),
-    the 12 kHz tail from the oracle -- timed on this host: once on 1 core and once on every core
-    this process may use (the cgroup quota if one is set, else the affinity set).  `value` is
-    the all-cores rate."""
+    """The CPU baseline: oracle/cpu_baseline.c -- the same
+    waterfall + chains with the costly stages in fp32 / AVX2-FMA like csdr (Shift + FirDecimate,
+    waterfall FFT), the 12 kHz tail from the oracle -- timed on this host: once on 1 core and once
+    on every core this process may use (the cgroup quota if one is set, else the affinity set).
+    `value` is the all-cores rate.  Also: the waterfall alone (csdr runs it as one thread:
+    FftChain's modules are one pipe), and the largest chain count the host keeps real time with
+    at this stream rate -- predicted from the 1-core per-chain and waterfall costs on the
+    available cores, then checked on 2 s of stream (stepped down until it keeps up)."""
     import ctypes
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
@@ -117,79 +120,137 @@ def cpu_baseline(fs, n_fft, hop, avg, plist):
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                    ctypes.c_float, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     cps = [orc.chain_from_engine_params(p) for p in plist]
-    arr = (orc.ChainParams * len(cps))(*cps)
+    iq_cache = {}
 
-    def timed(n, threads):
-        iq, _ = synth.make_iq(fs, n, ["nfm"])
+    def timed(n, threads, nchains):
+        if n not in iq_cache:
+            iq_cache.clear()
+            iq_cache[n] = synth.make_iq(fs, n, ["nfm"])[0]
+        arr = (orc.ChainParams * max(1, nchains))(*[cps[c % len(cps)] for c in range(max(1, nchains))])
         t0 = time.perf_counter()
-        fn(iq.ctypes.data, n, n_fft, hop, avg, -70.0, arr, len(cps), threads)
+        fn(iq_cache[n].ctypes.data, n, n_fft, hop, avg, -70.0, arr, nchains, threads)
         return time.perf_counter() - t0
 
     # sized for a few seconds each: 2^21 samples on one core, 2^22 x cores/8 on all of them
     n1 = 1 << 21
-    dt1 = timed(n1, 1)
+    dt1 = timed(n1, 1, len(cps))
     nall = max(n1, (1 << 22) * max(1, allc) // 8)
-    dta = timed(nall, allc)
+    dta = timed(nall, allc, len(cps))
+    _log("cpu baseline: waterfall only")
+    nw = 1 << 22
+    dtw = timed(nw, 1, 0)
+    t_w = dtw / nw                                    # core-seconds per sample, waterfall
+    t_c = max(1e-15, (dt1 / n1 - t_w) / len(cps))     # core-seconds per sample and chain
+    if t_w * fs >= 1.0:
+        c_pred = 0
+    else:
+        c_pred = max(0, int((allc / fs - t_w) / t_c))
+    checks = []
+    nv = int(2 * fs)
+    c_try = c_pred
+    c_ok = 0
+    for _ in range(4):
+        if c_try <= 0:
+            break
+        _log("cpu baseline: real-time check with %d chains" % c_try)
+        dtv = timed(nv, allc, c_try)
+        checks.append({"chains": c_try, "stream_seconds": round(nv / fs, 2), "wall_s": round(dtv, 2)})
+        if dtv <= nv / fs:
+            c_ok = c_try
+            break
+        c_try = int(c_try * 0.85)
     return {"value": round(nall / dta / 1e6, 3), "unit": "Msps", "cores": allc,
             "kind": "port",
             "one_core_msps": round(n1 / dt1 / 1e6, 4),
+            "waterfall_only_msps": round(nw / dtw / 1e6, 3),
+            "waterfall_only_cores": 1,
+            "max_realtime_chains": c_ok,
+            "max_realtime_chains_predicted": c_pred,
+            "max_realtime_chains_checks": checks,
             "host": host,
             "sample": "%d samples (%.2f s of %.2f Msps IQ) through the waterfall + %d chains on %d "
-                      "cores, %.2f s wall (1 core: %d samples, %.2f s); oracle/cpu_baseline.c "
-                      "(fp32, AVX2+FMA, OpenMP over chains)"
-                      % (nall, nall / fs, fs / 1e6, len(plist), allc, dta, n1, dt1)}
+                      "cores, %.2f s wall (1 core: %d samples, %.2f s); waterfall alone: %d samples "
+                      "on 1 core, %.2f s; oracle/cpu_baseline.c (fp32, AVX2+FMA, OpenMP over chains)"
+                      % (nall, nall / fs, fs / 1e6, len(plist), allc, dta, n1, dt1, nw, dtw)}
 
 
 def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block,
-                   ddc_mode="fast", churn=False):
+                   ddc_mode="fast", churn=False, pipelined=None):
     """SURVEY.md 8d measurement 1: feed the stream at its nominal rate through the host push path
     (SDR -> host cf32 -> PCIe -> HBM, owrx_push_iq) to a fresh engine with the same waterfall and
-    chains; every block is pushed on its wall-clock deadline, then synced and drained.  Keeps up
-    when no output ring overran and every block finished within its own period.  With `churn`,
-    one client leaves and another joins (owrx_chain_destroy + owrx_chain_create) while every
-    other block is still in flight: their latency is reported (both drain the pipeline)."""
+    chains; every block is pushed on its wall-clock deadline.  Without `churn` each block is then
+    synced and drained (latency = push to outputs in the host rings).  Keeps up when no output
+    ring overran and every block finished within its own period.
+
+    `pipelined` (default: with churn) runs the loop like a live server instead: no per-block sync (outputs are read as
+    they arrive, the pipeline keeps up to four blocks in flight); with `churn`, right after each
+    push one client leaves, another joins (owrx_chain_destroy + owrx_chain_create) and a third drags its
+    bandpass (owrx_chain_set_bandpass) while that block and its predecessors are in flight.  It
+    keeps up when every push returned before the next deadline (a GPU slower than the stream
+    back-pressures push) and nothing overran; `pipeline_drains` counts full pipeline drains inside
+    the loop (none: those calls do not drain); the host latency of each call is reported."""
+    if pipelined is None:
+        pipelined = churn
     t_setup = time.perf_counter()
     eng = Engine(fs, max_block=block)
     eng.set_ddc_mode(ddc_mode)
     wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
     chains = []
-    for i, p in enumerate(plist):
-        chains.append(eng.chain(p))
-        if i % 1024 == 1023:
-            _log("  %d chains created" % (i + 1))
-    eng.sync()
+    try:
+        for i, p in enumerate(plist):
+            chains.append(eng.chain(p))
+            if i % 4096 == 4095:
+                _log("  %d chains created" % (i + 1))
+        eng.sync()
+    except Exception:  # e.g. out of device memory: give it back before the caller goes on
+        eng.close()
+        raise
     t_setup = time.perf_counter() - t_setup
     period = block / fs
     nblocks = max(1, int(seconds / period))
-    lat, joins, leaves = [], [], []
+    lat, joins, leaves, bps = [], [], [], []
     tp = ts = tr = 0.0  # host seconds in push (block build + launches), sync, output reads
     st0 = eng.stats()
+    rng = np.random.default_rng(7)
     t0 = time.perf_counter()
     for i in range(nblocks):
-        wait = t0 + i * period - time.perf_counter()
+        deadline = t0 + i * period
+        wait = deadline - time.perf_counter()
         if wait > 0:
             time.sleep(wait)
         a = time.perf_counter()
         eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
         b = time.perf_counter()
         tp += b - a
-        if churn and i % 2 == 1 and chains:
+        if churn and chains:
             c0 = time.perf_counter()
-            chains.pop(i % len(chains)).close()
+            chains.pop(int(rng.integers(len(chains)))).close()
             c1 = time.perf_counter()
-            chains.append(eng.chain(plist[(i * 7) % len(plist)]))
+            chains.append(eng.chain(plist[int(rng.integers(len(plist)))]))
             c2 = time.perf_counter()
+            k = int(rng.integers(len(chains)))
+            lo = float(rng.uniform(-0.2, 0.0))
+            chains[k].set_bandpass(params.f32(lo), params.f32(lo + 0.15))
+            c3 = time.perf_counter()
             leaves.append(c1 - c0)
             joins.append(c2 - c1)
+            bps.append(c3 - c2)
         c = time.perf_counter()
-        eng.sync()
+        if not pipelined:
+            eng.sync()
         d = time.perf_counter()
         eng.read_chains(chains)
         wf.read()
         e = time.perf_counter()
         ts += d - c
         tr += e - d
-        lat.append(e - a)
+        # pipelined: how late the block's push (and this iteration) ran against its deadline
+        lat.append(e - a if not pipelined else e - deadline)
+    st_loop = eng.stats()
+    eng.sync()
+    # pipelined: the level's last outputs are in the host rings within one period of its last
+    # deadline (a GPU slower than the stream accumulates lag block by block)
+    finish_lag = time.perf_counter() - (t0 + nblocks * period)
     st = eng.stats()
     host = {"push_ms": round(1e3 * tp / nblocks, 3), "sync_ms": round(1e3 * ts / nblocks, 3),
             "read_ms": round(1e3 * tr / nblocks, 3)}
@@ -197,32 +258,45 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
         host[k] = round((st[k] - st0[k]) / nblocks, 3)
     eng.close()
     extra = {}
+
+    def summ(v):
+        return {"mean": round(1e3 * sum(v) / len(v), 3), "max": round(1e3 * max(v), 3), "n": len(v)}
     if joins:
-        extra = {"client_join_ms": {"mean": round(1e3 * sum(joins) / len(joins), 3),
-                                    "max": round(1e3 * max(joins), 3), "n": len(joins)},
-                 "client_leave_ms": {"mean": round(1e3 * sum(leaves) / len(leaves), 3),
-                                     "max": round(1e3 * max(leaves), 3), "n": len(leaves)}}
+        extra = {"client_join_ms": summ(joins), "client_leave_ms": summ(leaves),
+                 "set_bandpass_ms": summ(bps),
+                 "pipeline_drains": int(st_loop["pipeline_drains"] - st0["pipeline_drains"])}
     return {**extra, "seconds": round(nblocks * period, 2), "stream_msps": fs / 1e6, "chains": len(plist),
             "setup_s": round(t_setup, 2),
             "blocks": nblocks, "block_period_ms": round(1e3 * period, 2),
             "max_block_latency_ms": round(1e3 * max(lat), 3),
             "mean_block_latency_ms": round(1e3 * sum(lat) / len(lat), 3),
+            "latency_definition": ("push start to outputs in the host rings (sync per block)"
+                                   if not pipelined else
+                                   "deadline to the end of the block's push + churn + reads "
+                                   "(pipelined, no per-block sync)"),
             "overruns": int(st["overruns"]),
             "host_per_block": host,
-            "keeps_up": bool(st["overruns"] == 0 and max(lat) < period),
-            "path": "host cf32 -> owrx_push_iq (PCIe) -> engine, sync + drain per block"}
+            "finish_lag_ms": round(1e3 * finish_lag, 3) if pipelined else None,
+            "keeps_up": bool(st["overruns"] == 0 and max(lat) < period and
+                             (not pipelined or finish_lag < period)),
+            "path": "host cf32 -> owrx_push_iq (PCIe) -> engine"}
 
 
 def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, stream_host,
-                        seconds, block, ladder, ddc_mode, budget_s):
+                        seconds, block, ladder, ddc_mode, budget_s, agree=None, world=1):
     """BASELINE.md 3 / SURVEY.md 8d: the largest chain count C (from `ladder`) for which the paced
     real-time check at the config's stream rate keeps up (no overrun, every block within its
-    period), with the waterfall running too.  Stops at the first failure or when the next level
-    would exceed the time budget (chain creation grows with C)."""
+    period), with the waterfall running too.  Stops at the first failure (a level that does not
+    keep up, or cannot even be set up, e.g. out of device memory) or when the next level would
+    exceed the time budget.  At N>1 every rank runs each level at the same time on its own GPU
+    (C chains each, the stream pushed to every rank); a level passes when every rank kept up
+    (`agree` reduces over ranks), and the job's figure is C x N."""
+    agree = agree or (lambda v, op: v)
     levels, best = [], 0
     t0 = time.perf_counter()
     for C in ladder:
-        if levels and time.perf_counter() - t0 + 4 * levels[-1]["setup_s"] + seconds > budget_s:
+        elapsed = agree(time.perf_counter() - t0, "max")
+        if levels and elapsed + 2.5 * levels[-1].get("setup_s", 0) + seconds > budget_s:
             levels.append({"chains": C, "skipped": "time budget"})
             break
         ms = [modes[c % len(modes)] for c in range(C)]
@@ -230,24 +304,35 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
         _log("capacity level: %d chains" % C)
         try:
             r = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds,
-                               block, ddc_mode)
+                               block, ddc_mode, pipelined=True)
+            ok = r["keeps_up"]
         except Exception as exc:  # e.g. out of device memory: this level does not run
-            levels.append({"chains": C, "keeps_up": False, "error": str(exc)[:200]})
+            r, ok = {"chains": C, "error": str(exc)[:200], "setup_s": 0.0}, False
             _log("  failed: %s" % exc)
-            break
-        _log("  setup %.2f s, keeps_up %s, max block latency %.2f ms"
-             % (r["setup_s"], r["keeps_up"], r["max_block_latency_ms"]))
-        levels.append({k: r[k] for k in ("chains", "keeps_up", "max_block_latency_ms",
-                                         "mean_block_latency_ms", "overruns", "setup_s",
-                                         "host_per_block")})
-        if not r["keeps_up"]:
+        ok = bool(agree(1.0 if ok else 0.0, "min") > 0)
+        lvl = {k: r[k] for k in ("chains", "max_block_latency_ms", "mean_block_latency_ms",
+                                 "finish_lag_ms", "overruns", "setup_s", "host_per_block", "error")
+               if k in r}
+        lvl["keeps_up"] = ok
+        if world > 1:
+            lvl["max_block_latency_ms_all_ranks"] = round(agree(r.get("max_block_latency_ms", 1e9), "max"), 3)
+        levels.append(lvl)
+        if "error" not in r:
+            _log("  setup %.2f s, keeps_up %s, max block latency %.2f ms"
+                 % (r["setup_s"], ok, r["max_block_latency_ms"]))
+        if not ok:
             break
         best = C
-    return {"max_realtime_chains": best, "stream_msps": fs / 1e6, "block_samples": block,
+    failing = next((l["chains"] for l in levels if l.get("keeps_up") is False), None)
+    return {"max_realtime_chains": best * world, "per_gpu": best, "first_failing_level": failing,
+            "stream_msps": fs / 1e6, "block_samples": block,
             "seconds_per_level": seconds, "levels": levels,
             "note": "paced pushes of host cf32 through owrx_push_iq at the stream's wall-clock rate, "
-                    "waterfall + C chains (modes cycled), sync + drain per block; largest C that kept "
-                    "up; the ladder stops at the first level that did not (or the time budget)"}
+                    "waterfall + C chains per GPU (modes cycled), pipelined like a server (outputs "
+                    "read as they arrive, no per-block sync: a push that cannot keep its deadline "
+                    "fails the level); largest C "
+                    "that kept up on every GPU, times N; the ladder stops at the first level that did "
+                    "not (first_failing_level) or the time budget"}
 
 
 def pmc_traffic(prefix, config):
@@ -288,7 +373,11 @@ def main():
                     help="skip the per-kernel HIP-event brackets (roofline fields become null)")
     ap.add_argument("--ddc", default="fast", choices=("fast", "direct"),
                     help="DDC form: fast-convolution filter bank (default) or direct polyphase FIR")
-    ap.add_argument("--capacity-ladder", default="256,1024,4096,16384,32768,65536",
+    ap.add_argument("--churn-chains", type=int, default=16384,
+                    help="chains of the paced churn check (join + leave + setBandpass every "
+                         "block, no per-block sync; 0: skip)")
+    ap.add_argument("--capacity-ladder",
+                    default="256,1024,4096,16384,32768,65536,98304,131072,196608,262144",
                     help="chain counts tried by the max_realtime_chains sweep ('' = skip)")
     ap.add_argument("--capacity-seconds", type=float, default=2.0,
                     help="seconds of paced stream per sweep level")
@@ -468,14 +557,38 @@ def main():
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
         _log("real-time check")
         rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
-                            args.realtime_seconds, 1 << 20, args.ddc, churn=True)
-    cap = None
-    if rank == 0 and world == 1 and args.capacity_ladder:
+                            args.realtime_seconds, 1 << 20, args.ddc)
+    churn = None
+    if rank == 0 and world == 1 and args.realtime_seconds > 0 and args.churn_chains > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        Cc = args.churn_chains
+        _log("paced churn check: %d chains" % Cc)
+        pc = [params.chain_params(fs, o, cfg["modes"][c % len(cfg["modes"])])
+              for c, o in enumerate(carrier_offsets(fs, Cc))]
+        churn = realtime_check(Engine, params, fs, n_fft, hop, avg, pc, host,
+                               args.realtime_seconds, 1 << 20, args.ddc, churn=True)
+    cap = None
+    if args.capacity_ladder:
+        # every rank: 2 s of the same stream on the host (rank 0 slices its own; the others
+        # generate it, the synthetic source being deterministic)
+        if stream is not None:
+            host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        else:
+            host = gen_stream_torch(torch, dev, fs, hist + int(fs * 2), modes, offs)[hist:].cpu().numpy()
         ladder = [int(v) for v in args.capacity_ladder.split(",") if v]
+
+        def agree(v, op):
+            if not dist:
+                return v
+            t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
+            return float(t.item())
+        if dist:
+            dist.barrier()
         cap = max_realtime_chains(Engine, params, fs, n_fft, hop, avg, cfg["modes"],
                                   lambda c: carrier_offsets(fs, c), host,
-                                  args.capacity_seconds, 1 << 20, ladder, args.ddc, 150.0)
+                                  args.capacity_seconds, 1 << 20, ladder, args.ddc, 150.0,
+                                  agree=agree, world=world)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -582,6 +695,7 @@ def main():
                                  ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots",
                                   "host_ms_wait_rows")},
             "realtime": rt,
+            "realtime_churn": churn,
             "max_realtime_chains": cap["max_realtime_chains"] if cap else None,
             "capacity": cap,
             "cpu_baseline": cpu,

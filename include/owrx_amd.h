@@ -242,6 +242,9 @@ typedef struct {
                                      alone (timing enabled), for the HBM roofline */
     int64_t waterfall_timed_samples; /* stream samples of the frames those timed launches did */
     int64_t timed_blocks;      /* blocks whose kernel groups were timed (owrx_set_timing) */
+    int64_t pipeline_drains;   /* full drains of the block pipeline (owrx_sync, waterfall
+                                  reconfiguration, staging growth); chain joins / leaves and
+                                  their setters do not drain */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

@@ -99,6 +99,7 @@ class Stats(ctypes.Structure):
         ("gpu_ms_waterfall_fft", ctypes.c_double),
         ("waterfall_timed_samples", ctypes.c_int64),
         ("timed_blocks", ctypes.c_int64),
+        ("pipeline_drains", ctypes.c_int64),
     ]
 
 

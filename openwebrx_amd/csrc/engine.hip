@@ -287,8 +287,20 @@ struct Chain {
     // and audioBuffer (f32 demodulator-chain output); staging bytes per step, 0 = off
     int64_t tap_sq_cap = 0, tap_agc_cap = 0;
     ByteRing tap_sel, tap_audio;
+    // bumped by owrx_chain_set_secondary_fft / owrx_chain_set_taps: blocks built before the
+    // change (still in flight, they are not drained) deliver no rows / tap bytes afterwards
+    uint32_t sf_gen = 0, tap_gen = 0;
     int64_t tap_bytes() const { return out_region(tap_sq_cap) + out_region(tap_agc_cap); }
     int64_t sf_row_bytes() const { return sf_adpcm ? (sf_n + 10) / 2 : 4 * (int64_t)sf_n; }
+    // bytes of this chain's output region in a slot's staging (audio, secondary FFT, taps)
+    int64_t staging_bytes() const { return out_region(out_cap) + out_region(sf_out_cap) + tap_bytes(); }
+};
+
+// A post's staging layout as built (drain_slot reads the block with the layout it was built
+// with, whatever the chain's configuration is by then)
+struct PostLayout {
+    int64_t out_cap, sf_cap, tsq_cap, tagc_cap;
+    uint32_t sf_gen, tap_gen;
 };
 
 // one descriptor upload of copy_jobs (process_block)
@@ -303,6 +315,7 @@ struct Slot {  // one block's outputs in flight on streams B / C
     bool chains_pending = false;
     std::vector<int> post_ids;
     std::vector<int64_t> out_off;  // per post: byte offset of its output region
+    std::vector<PostLayout> layout;
     bool debug = false;
     ChainPost* d_posts = nullptr;
     ChainPost* h_posts = nullptr;
@@ -525,6 +538,23 @@ struct owrx_engine {
     owrx_stats stats;
     float* d_nr_win = nullptr;    // NoiseFilter window and twiddles (shared by all chains)
     float2* d_nr_tw = nullptr;
+    // Live reconfiguration without a drain (client join / leave, setBandpass, taps, secondary
+    // FFT while other clients stream): chain buffers come from exact-size free lists, so joins
+    // and leaves call neither hipMalloc nor hipFree (which synchronises the device) once warm;
+    // a released buffer is parked until every block that may still read it has drained
+    // (slot_tail >= the block index at its release); new buffers are zeroed and initial states
+    // and taps uploaded on stream A, ordered before the first block that uses them.
+    std::unordered_map<size_t, std::vector<void*>> pool_free;
+    std::unordered_map<void*, size_t> pool_size;  // every pool allocation (freed at destroy)
+    struct Retired {
+        int64_t block;
+        void* p;
+    };
+    std::vector<Retired> pool_retired;
+    uint8_t* h_up = nullptr;  // pinned staging of those uploads (a ring; wraps after stream A)
+    size_t up_cap = 0, up_head = 0;
+    // post staging needs of the current chains (kept as chains come and go)
+    int64_t need_out = 256, need_sm = 4, need_dbg = 64;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -537,26 +567,85 @@ static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
     return nk;
 }
 
-static void free_chain(Chain* c) {
-    dfree(c->d_pstate);
-    dfree(c->d_sstate);
-    dfree(c->d_ddc);
-    dfree(c->d_fd);
-    dfree(c->d_sq);
-    for (int i = 0; i < kSlots; ++i) dfree(c->d_dem[i]);
-    for (int i = 0; i < kSlots; ++i) dfree(c->d_s16[i]);
-    dfree(c->d_bp_taps);
-    dfree(c->d_wf);
-    dfree(c->d_pf);
-    dfree(c->d_pf_taps);
-    dfree(c->d_nr_state);
-    dfree(c->d_nr_in);
-    dfree(c->d_nr_pow);
-    dfree(c->d_nr_ola);
-    dfree(c->d_sf);
-    dfree(c->d_sf_acc);
-    dfree(c->d_sf_window);
-    dfree(c->d_sf_tw);
+// pool allocation (see owrx_engine): zeroed on stream A
+template <typename T>
+static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
+    *p = nullptr;
+    const size_t bytes = (sizeof(T) * std::max<size_t>(count, 1) + 255) & ~(size_t)255;
+    void* q = nullptr;
+    auto it = e->pool_free.find(bytes);
+    if (it != e->pool_free.end() && !it->second.empty()) {
+        q = it->second.back();
+        it->second.pop_back();
+    } else {
+        const hipError_t r = hipMalloc(&q, bytes);
+        if (r != hipSuccess) return r;
+        e->pool_size[q] = bytes;
+    }
+    *p = static_cast<T*>(q);
+    return hipMemsetAsync(q, 0, bytes, e->sA);
+}
+
+// release to the pool once the blocks enqueued so far have drained
+template <typename T>
+static void prel(owrx_engine* e, T*& p) {
+    if (p) e->pool_retired.push_back({e->block_index, (void*)p});
+    p = nullptr;
+}
+
+static void pool_collect(owrx_engine* e) {
+    size_t k = 0;
+    for (const auto& r : e->pool_retired) {
+        if (r.block <= e->slot_tail)
+            e->pool_free[e->pool_size[r.p]].push_back(r.p);
+        else
+            e->pool_retired[k++] = r;
+    }
+    e->pool_retired.resize(k);
+}
+
+// n bytes from the host to device memory on stream A, through the pinned upload ring: the
+// caller's buffer is free on return, and the copy runs before any later stream-A work
+static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
+    if (n == 0) return OWRX_OK;
+    const size_t a = (n + 255) & ~(size_t)255;
+    if (a > e->up_cap) {
+        if (e->h_up) HIPCHK(hipStreamSynchronize(e->sA));
+        hfree(e->h_up);
+        e->up_cap = std::max<size_t>(4u << 20, a);
+        HIPCHK(halloc(&e->h_up, e->up_cap));
+        e->up_head = 0;
+    }
+    if (e->up_head + a > e->up_cap) {  // wrap: the ring's earlier copies must have run
+        HIPCHK(hipStreamSynchronize(e->sA));
+        e->up_head = 0;
+    }
+    memcpy(e->h_up + e->up_head, src, n);
+    HIPCHK(kcopy(dst, e->h_up + e->up_head, n, e->sA));
+    e->up_head += a;
+    return OWRX_OK;
+}
+
+static void free_chain(owrx_engine* e, Chain* c) {
+    prel(e, c->d_pstate);
+    prel(e, c->d_sstate);
+    prel(e, c->d_ddc);
+    prel(e, c->d_fd);
+    prel(e, c->d_sq);
+    for (int i = 0; i < kSlots; ++i) prel(e, c->d_dem[i]);
+    for (int i = 0; i < kSlots; ++i) prel(e, c->d_s16[i]);
+    prel(e, c->d_bp_taps);
+    prel(e, c->d_wf);
+    prel(e, c->d_pf);
+    prel(e, c->d_pf_taps);
+    prel(e, c->d_nr_state);
+    prel(e, c->d_nr_in);
+    prel(e, c->d_nr_pow);
+    prel(e, c->d_nr_ola);
+    prel(e, c->d_sf);
+    prel(e, c->d_sf_acc);
+    prel(e, c->d_sf_window);
+    prel(e, c->d_sf_tw);
 }
 
 static void free_wf(Waterfall* w) {
@@ -618,26 +707,27 @@ static int drain_slot(owrx_engine* e, int si) {
             if (it == e->chains.end()) continue;
             Chain* c = it->second.get();
             const ChainCounts& cc = s.h_counts[k];
-            const int64_t nb = std::min<int64_t>(cc.out_bytes, c->out_cap);
-            if (cc.out_bytes > c->out_cap) e->stats.overruns++;
+            const PostLayout& L = s.layout[k];  // as this block was built
+            const int64_t nb = std::min<int64_t>(cc.out_bytes, L.out_cap);
+            if (cc.out_bytes > L.out_cap) e->stats.overruns++;
             c->audio.push(s.h_out + s.out_off[k], (size_t)nb);
-            if (cc.sf_bytes > 0) {
-                const int64_t sb = std::min<int64_t>(cc.sf_bytes, c->sf_out_cap);
-                if (cc.sf_bytes > c->sf_out_cap) e->stats.overruns++;
-                c->sfft.push(s.h_out + s.out_off[k] + out_region(c->out_cap), (size_t)sb);
+            if (cc.sf_bytes > 0 && L.sf_gen == c->sf_gen) {
+                const int64_t sb = std::min<int64_t>(cc.sf_bytes, L.sf_cap);
+                if (cc.sf_bytes > L.sf_cap) e->stats.overruns++;
+                c->sfft.push(s.h_out + s.out_off[k] + out_region(L.out_cap), (size_t)sb);
             }
-            if (c->tap_bytes() > 0) {
-                const uint8_t* tb = s.h_out + s.out_off[k] + out_region(c->out_cap) +
-                                    out_region(c->sf_out_cap);
-                if (c->tap_sq_cap > 0) {
-                    const int64_t b = std::min<int64_t>(8 * cc.n_gate, c->tap_sq_cap);
-                    if (8 * cc.n_gate > c->tap_sq_cap) e->stats.overruns++;
+            if (L.tsq_cap + L.tagc_cap > 0 && L.tap_gen == c->tap_gen) {
+                const uint8_t* tb = s.h_out + s.out_off[k] + out_region(L.out_cap) +
+                                    out_region(L.sf_cap);
+                if (L.tsq_cap > 0) {
+                    const int64_t b = std::min<int64_t>(8 * cc.n_gate, L.tsq_cap);
+                    if (8 * cc.n_gate > L.tsq_cap) e->stats.overruns++;
                     c->tap_sel.push(tb, (size_t)b);
                 }
-                if (c->tap_agc_cap > 0) {
-                    const int64_t b = std::min<int64_t>(4 * cc.n_front, c->tap_agc_cap);
-                    if (4 * cc.n_front > c->tap_agc_cap) e->stats.overruns++;
-                    c->tap_audio.push(tb + out_region(c->tap_sq_cap), (size_t)b);
+                if (L.tagc_cap > 0) {
+                    const int64_t b = std::min<int64_t>(4 * cc.n_front, L.tagc_cap);
+                    if (4 * cc.n_front > L.tagc_cap) e->stats.overruns++;
+                    c->tap_audio.push(tb + out_region(L.tsq_cap), (size_t)b);
                 }
             }
             e->stats.audio_bytes += nb;
@@ -725,10 +815,12 @@ static int drain_slots(owrx_engine* e, bool block, int keep) {
         RCCHK(drain_slot(e, si));
         e->slot_tail++;
     }
+    if (!e->pool_retired.empty()) pool_collect(e);
     return OWRX_OK;
 }
 
 static int drain_all(owrx_engine* e) {
+    e->stats.pipeline_drains++;
     HIPCHK(hipStreamSynchronize(e->sA));
     RCCHK(drain_rows(e, true, 0));
     return drain_slots(e, true, 0);
@@ -780,15 +872,10 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
 static int ensure_post_capacity(owrx_engine* e) {
     const int n = (int)e->chains.size();
     // output staging: one region per chain, sized by that chain's own worst case (ADPCM audio
-    // is ~2.6 KB per C2 block, a service resampler's cf32 IF up to 8 B per decimated sample)
-    int64_t need_out = 256, need_sm = 4, need_dbg = 64;
-    for (auto& kv : e->chains) {
-        need_out += out_region(kv.second->out_cap) + out_region(kv.second->sf_out_cap) +
-                    kv.second->tap_bytes();
-        need_sm = std::max<int64_t>(need_sm, kv.second->sm_cap);
-        // squelch / demod taps hold up to cap + sq_length samples per step
-        need_dbg = std::max<int64_t>(need_dbg, (kv.second->cap + kv.second->prm.sq_length + 16) * 8 + 64);
-    }
+    // is ~2.6 KB per C2 block, a service resampler's cf32 IF up to 8 B per decimated sample);
+    // the sums are kept by chain create / destroy / set_taps / set_secondary_fft (the staging
+    // only grows: slots in flight were built within the current size)
+    const int64_t need_out = e->need_out, need_sm = e->need_sm, need_dbg = e->need_dbg;
     if (n <= e->post_cap && need_out <= e->out_total && need_sm <= e->sm_stride &&
         (!e->debug || need_dbg <= e->dbg_stride))
         return OWRX_OK;
@@ -918,21 +1005,21 @@ static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
     return OWRX_OK;
 }
 
-// Room for `slots` members' spectra (the engine is drained): grows W[kappa][slot][Dp] by
+// Room for `slots` members' spectra: grows W[kappa][slot][Dp] by
 // doubling, moving the existing rows with one strided copy.
 static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
     if (!g->fc_M || slots <= g->fc_w_cap) return OWRX_OK;
     const int M = g->fc_M;
     const int cap = std::max(std::max(32, 2 * g->fc_w_cap), slots);
     float2* nw = nullptr;
-    HIPCHK(dalloc(&nw, (size_t)M * cap * g->fc_Dp));
+    // on stream A behind the blocks that read the old spectra (those release it when drained)
+    HIPCHK(palloc(e, &nw, (size_t)M * cap * g->fc_Dp));
     if (g->d_fc_w && g->fc_w_cap > 0) {
         const size_t row = sizeof(float2) * (size_t)g->fc_w_cap * g->fc_Dp;
         HIPCHK(hipMemcpy2DAsync(nw, sizeof(float2) * (size_t)cap * g->fc_Dp, g->d_fc_w, row, row,
                                 (size_t)M, hipMemcpyDeviceToDevice, e->sA));
-        HIPCHK(hipStreamSynchronize(e->sA));
     }
-    dfree(g->d_fc_w);
+    prel(e, g->d_fc_w);
     g->d_fc_w = nw;
     g->fc_w_cap = cap;
     return OWRX_OK;
@@ -1135,6 +1222,7 @@ static int wide_serial_chains() {
 static int build_posts(owrx_engine* e, Slot& S, int si) {
     S.post_ids.clear();
     S.out_off.clear();
+    S.layout.clear();
     S.post_groups.clear();
     S.group_post0.clear();
     S.sf_sizes = 0;
@@ -1241,6 +1329,8 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
                 p.tap_agc_cap = c->tap_agc_cap / 4;
             }
             out_off += c->tap_bytes();
+            S.layout.push_back(PostLayout{c->out_cap, c->sf_out_cap, c->tap_sq_cap, c->tap_agc_cap,
+                                          c->sf_gen, c->tap_gen});
             p.smeter = S.d_sm + (int64_t)np * e->sm_stride;
             p.smeter_cap = (int)e->sm_stride;
             p.debug = (e->debug && S.d_dbg) ? 1 : 0;
@@ -1702,22 +1792,22 @@ int owrx_engine_destroy(owrx_engine* e) {
         if (st) hipStreamSynchronize(st);
     for (auto& r : e->rslots)
         if (r.stream) hipStreamSynchronize(r.stream);
-    for (auto& kv : e->chains) free_chain(kv.second.get());
+    for (auto& kv : e->chains) free_chain(e, kv.second.get());
     for (auto& kv : e->wfs) free_wf(kv.second.get());
-    dfree(e->d_nr_win);
-    dfree(e->d_nr_tw);
     for (auto& g : e->groups) {
         dfree(g->d_taps);
         dfree(g->d_h);
         dfree(g->d_fc_tw);
         dfree(g->d_fc_u);
         dfree(g->d_fc_y);
-        dfree(g->d_fc_w);
+        prel(e, g->d_fc_w);
         dfree(g->d_chains);
         for (int i = 0; i < kSlots; ++i) dfree(g->d_partial[i]);
         hfree(g->h_chains[0]);
         hfree(g->h_chains[1]);
     }
+    for (auto& kv : e->pool_size) hipFree(kv.first);  // the pool's buffers, in use or not
+    hfree(e->h_up);
     dfree(e->d_ring);
     dfree(e->d_cs16);
     hfree(e->h_in);
@@ -2001,16 +2091,16 @@ static int chain_nr_alloc(owrx_engine* e, Chain* c) {
         for (int i = 0; i < kNrN; ++i)
             w[i] = (float)std::sqrt(0.5 - 0.5 * std::cos(2.0 * M_PI * (double)i / kNrN));
         std::vector<float> tw = fft_twiddles(kNrN);
-        HIPCHK(dalloc(&e->d_nr_win, (size_t)kNrN));
-        HIPCHK(dalloc(&e->d_nr_tw, (size_t)kNrN));
-        HIPCHK(hipMemcpy(e->d_nr_win, w.data(), sizeof(float) * kNrN, hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(e->d_nr_tw, tw.data(), sizeof(float) * 2 * kNrN, hipMemcpyHostToDevice));
+        HIPCHK(palloc(e, &e->d_nr_win, (size_t)kNrN));
+        HIPCHK(palloc(e, &e->d_nr_tw, (size_t)kNrN));
+        RCCHK(upload(e, e->d_nr_win, w.data(), sizeof(float) * kNrN));
+        RCCHK(upload(e, e->d_nr_tw, tw.data(), sizeof(float) * 2 * kNrN));
     }
     if (!c->d_nr_state) {
-        HIPCHK(dalloc(&c->d_nr_state, 1));
-        HIPCHK(dalloc(&c->d_nr_in, (size_t)chain_nr_in_cap(c)));
-        HIPCHK(dalloc(&c->d_nr_pow, (size_t)2 * (kNrN / 2 + 1)));
-        HIPCHK(dalloc(&c->d_nr_ola, (size_t)kNrHop));
+        HIPCHK(palloc(e, &c->d_nr_state, 1));
+        HIPCHK(palloc(e, &c->d_nr_in, (size_t)chain_nr_in_cap(c)));
+        HIPCHK(palloc(e, &c->d_nr_pow, (size_t)2 * (kNrN / 2 + 1)));
+        HIPCHK(palloc(e, &c->d_nr_ola, (size_t)kNrHop));
     }
     c->nr_reset = true;
     return OWRX_OK;
@@ -2043,9 +2133,10 @@ static int chain_set_bandpass_taps(owrx_engine* e, Chain* c) {
         return OWRX_EINVAL;
     }
     std::vector<float> taps = firdes_bandpass_c(T, c->prm.bp_low, c->prm.bp_high);
-    RCCHK(drain_all(e));
-    if (!c->d_bp_taps) HIPCHK(dalloc(&c->d_bp_taps, (size_t)c->bp_hist + 1));
-    HIPCHK(hipMemcpy(c->d_bp_taps, taps.data(), sizeof(float) * 2 * T, hipMemcpyHostToDevice));
+    // no drain: the bandpass FIR runs on stream A (post_parallel / bp_long), so blocks enqueued
+    // before this copy filter with the old taps and every later block with the new ones
+    if (!c->d_bp_taps) HIPCHK(palloc(e, &c->d_bp_taps, (size_t)c->bp_hist + 1));
+    RCCHK(upload(e, c->d_bp_taps, taps.data(), sizeof(float) * 2 * T));
     c->bp_ntaps = T;
     return OWRX_OK;
 }
@@ -2068,7 +2159,8 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         set_last_error("owrx_chain_create: polyphase depth %d unsupported", (T + D - 1) / D);
         return OWRX_EINVAL;
     }
-    RC_FAIL(e, drain_all(e));
+    // no drain: the new chain starts at the next block (its origin is past every block in
+    // flight); its buffers come from the pool and are initialised on stream A
     // group lookup by (D, transition, cutoff)
     uint32_t tb, cb;
     memcpy(&tb, &p->transition, 4);
@@ -2162,45 +2254,48 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     AgcParams ap = agc_profile(p->agc_profile);
     if (p->agc_initial_gain >= 0) ap.initial_gain = p->agc_initial_gain;
     ss.agc.env = ap.reference / ap.initial_gain;
-    HIPCHK(dalloc(&c->d_pstate, 1));
-    HIPCHK(dalloc(&c->d_sstate, 1));
-    HIPCHK(hipMemcpy(c->d_pstate, &ps, sizeof(ps), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_sstate, &ss, sizeof(ss), hipMemcpyHostToDevice));
-    HIPCHK(dalloc(&c->d_ddc, (size_t)(kFdHist + c->cap)));
-    HIPCHK(dalloc(&c->d_fd, (size_t)(c->bp_hist + c->cap)));
+    HIPCHK(palloc(e, &c->d_pstate, 1));
+    HIPCHK(palloc(e, &c->d_sstate, 1));
+    RCCHK(upload(e, c->d_pstate, &ps, sizeof(ps)));
+    RCCHK(upload(e, c->d_sstate, &ss, sizeof(ss)));
+    HIPCHK(palloc(e, &c->d_ddc, (size_t)(kFdHist + c->cap)));
+    HIPCHK(palloc(e, &c->d_fd, (size_t)(c->bp_hist + c->cap)));
     if (p->demod == OWRX_DEMOD_WFM && p->output != OWRX_OUT_IQ) {
         // FractionalDecimator(FLOAT, if_rate / audio_rate, prefilter=True): prefilter lowpass
         // at 0.5 / rate (output Nyquist), transition 0.03 (csdr's default; recalled, unpinned)
         const double r = p->if_rate / (double)p->audio_rate;
         c->pf_ntaps = firdes_filter_len(0.03f);
         std::vector<float> pf = firdes_lowpass(c->pf_ntaps, 0.5 / r);
-        HIPCHK(dalloc(&c->d_pf_taps, (size_t)c->pf_ntaps));
-        HIPCHK(hipMemcpy(c->d_pf_taps, pf.data(), sizeof(float) * pf.size(),
-                         hipMemcpyHostToDevice));
-        HIPCHK(dalloc(&c->d_wf, (size_t)(kWfHist + scap)));
-        HIPCHK(dalloc(&c->d_pf, (size_t)(kWfHist + scap)));
+        HIPCHK(palloc(e, &c->d_pf_taps, (size_t)c->pf_ntaps));
+        RCCHK(upload(e, c->d_pf_taps, pf.data(), sizeof(float) * pf.size()));
+        HIPCHK(palloc(e, &c->d_wf, (size_t)(kWfHist + scap)));
+        HIPCHK(palloc(e, &c->d_pf, (size_t)(kWfHist + scap)));
     }
-    HIPCHK(dalloc(&c->d_sq, (size_t)scap));
+    HIPCHK(palloc(e, &c->d_sq, (size_t)scap));
     // slack: the serial kernels read whole 64-sample chunks / 8-sample prefetches unguarded
-    for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_dem[i], (size_t)scap + 160));
+    for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_dem[i], (size_t)scap + 160));
     // + kNrN: a NoiseFilter emits up to one frame more than its input per step
-    for (int i = 0; i < kSlots; ++i) HIPCHK(dalloc(&c->d_s16[i], (size_t)scap + 160 + kNrN));
+    for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_s16[i], (size_t)scap + 160 + kNrN));
     int rc = chain_set_bandpass_taps(e, c.get());
     if (!rc && p->nr_enabled && p->output != OWRX_OUT_IQ) rc = chain_nr_alloc(e, c.get());
     if (rc) {
-        free_chain(c.get());
+        free_chain(e, c.get());
         return rc;
     }
     if (g->fc_M) {
         int wrc = fc_reserve(e, g, (int)g->members.size() + 1);
         if (!wrc) wrc = fc_build_w(e, c.get(), (int)g->members.size());
         if (wrc) {
-            free_chain(c.get());
+            free_chain(e, c.get());
             return wrc;
         }
     }
     const int h = e->next_handle++;
     g->members.push_back(h);
+    e->need_out += c->staging_bytes();
+    e->need_sm = std::max<int64_t>(e->need_sm, c->sm_cap);
+    // squelch / demod debug taps hold up to cap + sq_length samples per step
+    e->need_dbg = std::max<int64_t>(e->need_dbg, (c->cap + c->prm.sq_length + 16) * 8 + 64);
     e->chains[h] = std::move(c);
     RC_FAIL(e, group_refresh_device(e, g));
     RC_FAIL(e, ensure_post_capacity(e));
@@ -2213,8 +2308,9 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     e->chain_epoch++;  // the slots rebuild their post descriptors
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
-    RC_FAIL(e, drain_all(e));
-    for (hipStream_t st : {e->sB, e->sC, e->sBw, e->sCw}) HIPCHK(hipStreamSynchronize(st));
+    // no drain: blocks in flight keep their descriptors (their outputs for this chain are
+    // dropped at drain_slot), its buffers return to the pool once those blocks have drained,
+    // and the spectra move below runs on stream A behind their DDC
     ChainGroup* g = it->second->group;
     // swap-remove: the last member takes the slot (and its filter spectra move with it)
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
@@ -2229,7 +2325,8 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     }
     g->members[slot] = g->members[last];
     g->members.pop_back();
-    free_chain(it->second.get());
+    e->need_out -= it->second->staging_bytes();
+    free_chain(e, it->second.get());
     e->chains.erase(it);
     if (!g->members.empty()) RC_FAIL(e, group_refresh_device(e, g));
     return OWRX_OK;
@@ -2336,10 +2433,13 @@ int owrx_chain_set_taps(owrx_engine* e, int handle, int selector, int audio) {
         set_last_error("owrx_chain_set_taps: the chain has no Selector output / audio");
         return OWRX_EINVAL;
     }
-    RC_FAIL(e, drain_all(e));
+    // no drain: the slots in flight were built with the old layout (drain_slot uses theirs)
     const int64_t scap = c->cap + c->prm.sq_length + 16;  // samples per step, as the staging
+    e->need_out -= c->staging_bytes();
     c->tap_sq_cap = selector ? 8 * scap : 0;
     c->tap_agc_cap = audio ? 4 * scap : 0;
+    e->need_out += c->staging_bytes();
+    c->tap_gen++;
     if (!selector) c->tap_sel.clear();
     if (!audio) c->tap_audio.clear();
     RC_FAIL(e, ensure_post_capacity(e));
@@ -2374,28 +2474,29 @@ int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int e
                        "[1024, 8192], every_n_samples > 0, on an audio chain");
         return OWRX_EINVAL;
     }
-    RC_FAIL(e, drain_all(e));
+    // no drain: the old buffers go back to the pool once the blocks in flight (built with
+    // them) have drained; rows those blocks still produce are dropped (sf_gen)
+    e->need_out -= c->staging_bytes();
     if (fft_size != c->sf_n) {
-        dfree(c->d_sf);
-        dfree(c->d_sf_acc);
-        dfree(c->d_sf_window);
-        dfree(c->d_sf_tw);
+        prel(e, c->d_sf);
+        prel(e, c->d_sf_acc);
+        prel(e, c->d_sf_window);
+        prel(e, c->d_sf_tw);
         c->sf_n = 0;
         c->sf_out_cap = 0;
         if (fft_size > 0) {
             const int64_t scap = c->cap + c->prm.sq_length + 16;
-            HIPCHK(dalloc(&c->d_sf, (size_t)(fft_size + scap + 64)));
-            HIPCHK(dalloc(&c->d_sf_acc, (size_t)fft_size));
-            HIPCHK(dalloc(&c->d_sf_window, (size_t)fft_size));
-            HIPCHK(dalloc(&c->d_sf_tw, (size_t)fft_size));
+            HIPCHK(palloc(e, &c->d_sf, (size_t)(fft_size + scap + 64)));
+            HIPCHK(palloc(e, &c->d_sf_acc, (size_t)fft_size));
+            HIPCHK(palloc(e, &c->d_sf_window, (size_t)fft_size));
+            HIPCHK(palloc(e, &c->d_sf_tw, (size_t)fft_size));
             std::vector<float> win = hamming_window(fft_size);
             std::vector<float> tw = fft_twiddles(fft_size);
-            HIPCHK(hipMemcpy(c->d_sf_window, win.data(), sizeof(float) * fft_size,
-                             hipMemcpyHostToDevice));
-            HIPCHK(hipMemcpy(c->d_sf_tw, tw.data(), sizeof(float) * 2 * fft_size,
-                             hipMemcpyHostToDevice));
+            RCCHK(upload(e, c->d_sf_window, win.data(), sizeof(float) * fft_size));
+            RCCHK(upload(e, c->d_sf_tw, tw.data(), sizeof(float) * 2 * fft_size));
         }
     }
+    c->sf_gen++;
     c->sf_n = fft_size;
     c->sf_logn = logn;
     c->sf_hop = every_n_samples;
@@ -2411,6 +2512,7 @@ int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int e
         const int64_t rows = frames / std::max(1, avg_number) + 2;
         c->sf_out_cap = rows * c->sf_row_bytes();
     }
+    e->need_out += c->staging_bytes();
     RC_FAIL(e, ensure_post_capacity(e));
     return OWRX_OK;
 }

@@ -118,7 +118,7 @@ class Engine:
         check(lib.owrx_get_stats(self._h, ctypes.byref(s)), "owrx_get_stats")
         return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
 
-    def read_chains(self, chains, max_bytes=64 << 20, max_values=1 << 16):
+    def read_chains(self, chains, max_bytes=64 << 20, max_values=1 << 20):
         """Drains the audio and s-meter rings of many chains with two native calls
         (owrx_chains_read_audio / owrx_chains_read_smeter) -- the one-thread pump for a server with
         hundreds of clients.  Returns (audio, alens, smeter, scounts): the concatenated bytes and
@@ -144,13 +144,16 @@ class Engine:
                 break
         if len(rounds) == 1:
             return abuf[:na], alens, rounds[0][0], rounds[0][1]
-        offs = [np.concatenate(([0], np.cumsum(c)[:-1])) for _, c in rounds]
-        parts = []
-        for i in range(n):
-            for (buf, c), o in zip(rounds, offs):
-                parts.append(buf[o[i]:o[i] + c[i]])
+        # chain i's values: its piece of round 0, then of round 1, ... (vectorised scatter)
         scounts = sum(c for _, c in rounds)
-        return abuf[:na], alens, np.concatenate(parts) if parts else np.empty(0, np.float32), scounts
+        start = np.concatenate(([0], np.cumsum(scounts)[:-1]))  # chain i's output offset
+        out = np.empty(int(scounts.sum()), np.float32)
+        before = np.zeros(n, np.int64)  # chain i's values placed by the earlier rounds
+        for buf, c in rounds:
+            src0 = np.concatenate(([0], np.cumsum(c)[:-1]))
+            out[np.repeat(start + before - src0, c) + np.arange(buf.size)] = buf
+            before += c
+        return abuf[:na], alens, out, scounts
 
     def waterfall(self, fft_size, every_n_samples, avg_number, add_db=-70.0, adpcm=True):
         return Waterfall(self, fft_size, every_n_samples, avg_number, add_db, adpcm)

@@ -724,8 +724,14 @@ def test_batched_chain_reads_equal_per_chain_reads(amd):
         assert np.array_equal(ch.read_smeter(), sm[so[i]:so[i + 1]]), i
     again, alens2, _, _ = e2.read_chains(c2)
     assert again.size == 0 and not alens2.any()
+    # a value buffer smaller than the pending s-meter values: several native reads, each chain's
+    # pieces put back together in order
+    e3, c3 = _run_chains(amd, iq, fs, plist, 1 << 17, debug=False)
+    _, _, sm3, sc3 = e3.read_chains(c3, max_values=5)
+    assert np.array_equal(sc3, scounts) and np.array_equal(sm3, sm)
     e1.close()
     e2.close()
+    e3.close()
 
 
 def test_c4_chains_61msps(amd):
@@ -902,6 +908,68 @@ def test_retune_is_phase_continuous(amd):
     old = oracle.fir_decimate(oracle.shift(iq, p.shift_rate), c._keep[0], D)
     assert rel_rms(got[:k], old[:k]) < 1e-5
     assert rel_rms(got[k:], ref[k:]) < 1e-5
+    eng.close()
+
+
+def test_live_changes_without_drain(amd):
+    """Clients join, leave and drag the bandpass while others stream (owrx/dsp.py:538-562,
+    Bandpass.setBandpass csdr/chain/selector.py:159-166) without draining the pipeline: the
+    bandpass change applies from the next block, so chain 1's Bandpass output equals the oracle
+    with the old taps up to the switch and with the new taps (same FIR history) after it; a
+    chain leaving and one joining mid-stream leave the others untouched; the joiner's DDC follows
+    its own origin; no call drained the block pipeline."""
+    from openwebrx_amd import synth
+    fs, B = 2400000, 1 << 17
+    modes = ["nfm", "usb", "nfm", "am"]
+    iq, offs = synth.make_iq(fs, 8 * B, modes + ["nfm"])
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16) for o, m in zip(offs, modes)]
+    eng = amd.Engine(fs, max_block=B)
+    eng.set_debug(True)
+    chains = [eng.chain(p) for p in plist]
+    d0 = eng.stats()["pipeline_drains"]
+    eng.push(iq[:3 * B])
+    lo, hi = amd.params.f32(300.0 / 12000), amd.params.f32(2400.0 / 12000)
+    chains[1].set_bandpass(lo, hi)
+    eng.push(iq[3 * B:4 * B])
+    chains[3].close()
+    pn = amd.params.chain_params(fs, offs[4], "nfm", output=amd._lib.OUT_S16)
+    cn = eng.chain(pn)
+    eng.push(iq[4 * B:])
+    assert eng.stats()["pipeline_drains"] == d0  # join / leave / setBandpass: no drain
+    eng.sync()
+    # chain 1: Bandpass output piecewise (old taps, then new taps from the switch block on)
+    p1 = plist[1]
+    ref = oracle.stages(iq, p1)
+    c1 = oracle.chain_from_engine_params(p1)
+    T, D = c1.ntaps, p1.decimation
+    k3 = (3 * B - T) // D + 1  # DDC outputs of the first three blocks
+    fd = ref["frac"]
+    s = (oracle.fractional_decimator(ref["ddc"][:k3], p1.frac_rate).size
+         if p1.frac_rate != 1.0 else k3)
+    new_taps = oracle.bandpass_taps(oracle.filter_len(p1.bp_transition), lo, hi)
+    old = ref["bandpass"]
+    new = oracle.fir_complex(fd, new_taps)
+    got = chains[1].read_debug(2)
+    assert got.size == fd.size, (got.size, fd.size)
+    assert 0 < s < got.size
+    assert rel_rms(got[:s], old[:s]) < 1e-5
+    assert rel_rms(got[s:], new[s:]) < 1e-5
+    assert rel_rms(got[s:], old[s:]) > 1e-2  # the change did take effect
+    # untouched chains: whole stream vs the oracle
+    _check_sampled_chains(iq, plist, chains, (0, 2))
+    # the joiner: its shift phase starts at its origin (absolute sample index)
+    org = cn.origin
+    assert org > 0 and org % pn.decimation == 0
+    cc = oracle.chain_from_engine_params(pn)
+    n = np.arange(iq.size, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        ph = (n - np.uint64(org) + np.uint64(1)) * np.uint64(_rate_fx(pn.shift_rate))
+    x = (iq.astype(np.complex128) * np.exp(2j * np.pi * ph.astype(np.float64) / 2.0 ** 64)).astype(np.complex64)
+    refn = oracle.fir_decimate(x, cc._keep[0], pn.decimation)[org // pn.decimation:]
+    gn = cn.read_debug(0)
+    assert gn.size == refn.size, (gn.size, refn.size)
+    assert rel_rms(gn, refn) < 1e-5
+    assert len(cn.read_audio()) > 0
     eng.close()
 
 
