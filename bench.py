@@ -423,7 +423,10 @@ def main():
     wf_batch = 0
     if world == 1 and not args.no_waterfall:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        wf_batch = 4 * max(1, cus - 16) if args.wf_batch < 0 else args.wf_batch
+        # four frames per stream-A CU for the 16384-point kernel (4 frames per workgroup); one
+        # per CU above it (each frame is 4 or 2 sub-frames of that kernel after the DIF split)
+        per_cu = 4 if n_fft <= 16384 else 1
+        wf_batch = per_cu * max(1, cus - 16) if args.wf_batch < 0 else args.wf_batch
     history = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
     eng = Engine(fs, max_block=block, device=local, history=history)
     eng.set_ddc_mode(args.ddc)
@@ -549,7 +552,14 @@ def main():
     wf_fft_ms = d["gpu_ms_waterfall_fft"]
     wf_bytes = 8.0 * d["waterfall_timed_samples"]
     wf_gbs = wf_bytes / (wf_fft_ms / 1e3) / 1e9 if wf_fft_ms > 0 else None
-    wf_traffic, wf_traffic_src = pmc_traffic("wf_fft_l32", args.config)
+    wf_kernels = (["wf_dif_split", "wf_fft_l32", "wf_finalize"] if n_fft > 16384 else
+                  ["wf_fft_l32", "wf_finalize"])
+    wf_traffic, wf_traffic_src = 0, []
+    for kname in wf_kernels:
+        b, src = pmc_traffic(kname, args.config)
+        wf_traffic = None if (b is None or wf_traffic is None) else wf_traffic + b
+        wf_traffic_src.append(src)
+    wf_traffic_src = "; ".join(sorted(set(wf_traffic_src)))
 
     traffic, traffic_src = pmc_traffic("fc_mac<" if fast else "ddc_lds<", args.config)
     rt = None
@@ -650,13 +660,14 @@ def main():
                         "passes of this config: " + traffic_src,
                 "waterfall": None if wf_gbs is None else {
                     "bound": "hbm",
-                    "kernel": "wf_fft_l32 + wf_finalize (FftChain: Hamming FFT, |X|^2 summed over "
-                              "avg frames, 10 log10, FftSwap, quantise)",
+                    "kernel": " + ".join(wf_kernels) + " (FftChain: Hamming FFT, |X|^2 summed "
+                              "over avg frames, 10 log10, FftSwap, quantise)",
                     "achieved": round(wf_gbs, 1),
                     "peak": HBM_PEAK_GBS,
                     "unit": "GB/s",
                     "frac": round(wf_gbs / HBM_PEAK_GBS, 4),
                     "traffic": wf_traffic,
+                    "algorithmic_bytes_per_launch": round(wf_bytes / max(1, wf_launches)),
                     "frames_per_launch": round(d["waterfall_frames"] / max(1, wf_launches), 1),
                     "launches": wf_launches,
                     "ms_per_launch": round(wf_fft_ms / max(1, wf_launches), 4),

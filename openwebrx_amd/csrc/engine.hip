@@ -44,8 +44,9 @@ void set_last_error(const char* fmt, ...) {
 
 // kernel launchers (kernels_*.hip)
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
-                         int ngroups, const float* window, const float2* tw, float* partial,
-                         float2* scratch, hipStream_t st);
+                         int ngroups, int fpg, const float* window, const float* ones,
+                         const float2* tw, float* partial, float2* scratch, hipStream_t st);
+bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
 bool wf_uses_l32(int logn);  // kernels_waterfall.hip: the N = 16384 kernel in use
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
@@ -81,6 +82,7 @@ hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const
 
 constexpr int kWfMaxFramesPerGroup = 16;  // frames one FFT workgroup sums (N <= kWfLdsMaxN)
 constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
+constexpr int kWfSplitMaxFpg = 4;      // frames per group of the DIF-split path (N > kWfLdsMaxN)
 constexpr int kWfMaxN = 65536;
 constexpr int kBlMaxTaps = 4095;       // longest bandpass of the bp_long path (kernels_post.hip)
 constexpr int kSelPad = 64 * 4 * 6;    // serial lane lists: 64-lane padding per (output, NR, demod)
@@ -176,7 +178,9 @@ struct Waterfall {
     float* d_window = nullptr;
     float2* d_tw = nullptr;
     float* d_partial = nullptr;
-    float2* d_y4 = nullptr;  // four-step FFT scratch (N > 16384): one cf32 frame per group
+    float2* d_y4 = nullptr;  // N > 16384: DIF-split sub-frames (fpg frames per group) or the
+                             // four-step scratch (one cf32 frame per group)
+    float* d_ones = nullptr; // DIF split: the sub-frames' window (the split applied the frame's)
     int partial_groups = 0;
     WfGroup* h_groups[2] = {};  // pinned copy sources, per block parity
     WfRow* h_rows[2] = {};
@@ -653,6 +657,7 @@ static void free_wf(Waterfall* w) {
     dfree(w->d_tw);
     dfree(w->d_partial);
     dfree(w->d_y4);
+    dfree(w->d_ones);
     dfree(w->d_carry[0]);
     dfree(w->d_carry[1]);
     dfree(w->d_groups);
@@ -839,7 +844,8 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
         dfree(w->d_groups);
         dfree(w->d_y4);
         HIPCHK(dalloc(&w->d_partial, (size_t)groups * w->N));
-        if (w->N > kWfLdsMaxN) HIPCHK(dalloc(&w->d_y4, (size_t)groups * w->N));
+        if (w->N > kWfLdsMaxN)
+            HIPCHK(dalloc(&w->d_y4, (size_t)groups * w->N * (wf_uses_split(w->logn) ? kWfSplitMaxFpg : 1)));
         HIPCHK(dalloc(&w->d_groups, (size_t)groups));
         for (int b = 0; b < 2; ++b) {
             hfree(w->h_groups[b]);
@@ -1038,12 +1044,16 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
 //    geometry: 366 frames F=2 21.3 us vs F=1 24.6 / F=3 27.6; 960 frames F=4 41.4 us vs F=2
 //    45.5; profiles/r03a_wf_micro_*.txt);
 //  - wf_fft_r16: enough that a launch's frames occupy stream A's CUs about once;
-//  - the four-step FFT (N > kWfLdsMaxN): one frame per group.
+//  - the DIF split (N = 16384 Q): wf_fft_l32's rule on the Q sub-frames of each frame;
+//  - the four-step FFT (OWRX_WF_KERNEL=fourstep): one frame per group.
 static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
-    if (w->N > kWfLdsMaxN) return 1;
     const int64_t hop = std::max(1, w->hop);
     const int64_t frames = std::max<int64_t>(w->batch_min, e->max_block / hop);
     const int64_t cus = std::max(1, e->cus_a);
+    if (w->N > kWfLdsMaxN) {
+        if (!wf_uses_split(w->logn)) return 1;
+        return frames * (w->N / kWfLdsMaxN) >= 3 * cus ? kWfSplitMaxFpg : 2;
+    }
     if (wf_uses_l32(w->logn)) return frames >= 3 * cus ? 4 : 2;
     int64_t fpg = (frames + cus - 1) / cus;
     fpg = std::min(fpg, (e->history - w->N) / hop);
@@ -1134,8 +1144,8 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         HIPCHK(hipEventRecord(S->w0, e->sA));
         e->stats.waterfall_timed_samples += nfr * w->hop;
     }
-    HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(),
-                         w->d_window, w->d_tw, w->d_partial, w->d_y4, e->sA));
+    HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(), w->fpg,
+                         w->d_window, w->d_ones, w->d_tw, w->d_partial, w->d_y4, e->sA));
     const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
     const int cin = w->carry_idx, cout = 1 - w->carry_idx;
     HIPCHK(launch_wf_finalize(w->d_partial, w->d_rows, (int)w->rowdesc.size(), w->d_carry[cin],
@@ -1988,6 +1998,11 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
     HIPCHK(dalloc(&w->d_carry[1], (size_t)fft_size));
     HIPCHK(hipMemcpy(w->d_window, win.data(), sizeof(float) * fft_size, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(w->d_tw, tw.data(), sizeof(float) * 2 * fft_size, hipMemcpyHostToDevice));
+    if (fft_size > kWfLdsMaxN) {
+        const std::vector<float> ones(kWfLdsMaxN, 1.0f);
+        HIPCHK(dalloc(&w->d_ones, (size_t)kWfLdsMaxN));
+        HIPCHK(hipMemcpy(w->d_ones, ones.data(), sizeof(float) * kWfLdsMaxN, hipMemcpyHostToDevice));
+    }
     int rc = wf_alloc_buffers(e, w.get());
     if (rc) {
         free_wf(w.get());

@@ -614,19 +614,26 @@ struct WfL32 {
 };
 OWRX_DEV int wf_swz32(int e) { return e ^ ((e >> 5) & 15); }
 
+// qlog > 0 (N = 16384 << qlog, wf_dif_split first): workgroup blockIdx.x = (group << qlog) + j
+// transforms sub-frame j of its group's frames from the split scratch (blk; sub-frames of one
+// group `fstride` frames apart), its partial row landing at partial + group * (N << qlog) +
+// j * N; tw then is the (N << qlog)-point table, read at stride 1 << qlog.
 __global__ void __launch_bounds__(WfL32::NT)
 wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
            const float* __restrict__ window, const float2* __restrict__ tw,
-           float* __restrict__ partial) {
+           float* __restrict__ partial, int qlog, int fstride) {
     using K = WfL32;
     constexpr int N = K::N, NT = K::NT;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     const int t0 = threadIdx.x;
     WF_RSTAMP(14);
     WF_STAMP(0);
-    const WfGroup g = groups[blockIdx.x];
-    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
-    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
+    const int gi = blockIdx.x >> qlog;
+    const WfGroup g = groups[gi];
+    const int64_t g0 = __builtin_amdgcn_readfirstlane(
+        qlog ? (int)((((int64_t)gi * fstride << qlog) + (blockIdx.x & ((1 << qlog) - 1))) * N)
+             : (int)(g.start - blk_start));
+    const int hop = __builtin_amdgcn_readfirstlane(qlog ? N << qlog : g.hop);
     const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
     const auto xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
@@ -650,12 +657,12 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     // L2-resident tables first (vmcnt retires in order: the frame's HBM loads queue behind them)
     float2 tp[4];  // W_N^(2^i t), i < 4: P3's bases W_N^(r t) are products of at most four
 #pragma unroll
-    for (int i = 0; i < 4; ++i) tp[i] = tw[(t0 << i) & (N - 1)];
+    for (int i = 0; i < 4; ++i) tp[i] = tw[((t0 << i) & (N - 1)) << qlog];
     float2 t2v[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int e = t0 + NT * i;  // 992 entries: (r - 1) * 32 + k
-        t2v[i] = e < 31 * 32 ? tw[(((e >> 5) + 1) * (e & 31)) << 4] : make_float2(0.f, 0.f);
+        t2v[i] = e < 31 * 32 ? tw[(((e >> 5) + 1) * (e & 31)) << (4 + qlog)] : make_float2(0.f, 0.f);
     }
     float2 nx[32];
     load_x(0, nx);
@@ -738,14 +745,59 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         }
         if (f < 2) WF_STAMP(sb + 5);
     }
-    float* out = partial + (int64_t)blockIdx.x * N;
+    float* out = partial + (int64_t)blockIdx.x * N;  // = group * (N << qlog) + j * N
 #pragma unroll
     for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
     WF_STAMP(13);
     WF_RSTAMP(15);
 }
 
-// ---- FFT sizes above one CU's LDS (32768, 65536): four-step, two launches ------------------
+// ---- FFT sizes above one CU's LDS (32768, 65536): decimation-in-frequency split ------------
+// N = Q * 16384 (Q = 2, 4): X[Q k + j] = sum_n y_j[n] W_16384^(n k) with
+//   y_j[n] = W_N^(n j) * sum_q w[n + 16384 q] x[n + 16384 q] W_Q^(q j),   n < 16384,
+// so one frame becomes Q independent 16384-point sub-frames that wf_fft_l32 transforms (the
+// |X|^2 of bins Q k + j lands j-major in the partial row; wf_finalize reads it back in bin
+// order).  wf_dif_split: one thread per (frame, n) -- reads the frame once (Q loads), writes the
+// Q sub-frames to the scratch (frame f of group g at ((g fstride + f) Q + j) 16384).
+template <int QLOG>
+__global__ void __launch_bounds__(256)
+wf_dif_split(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+             const float* __restrict__ window, const float2* __restrict__ tw, int fstride,
+             float2* __restrict__ y) {
+    constexpr int M = 16384, Q = 1 << QLOG, N = M << QLOG;
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    const int f = blockIdx.y;
+    const WfGroup g = groups[blockIdx.z];
+    if (f >= g.nframes) return;
+    const float2* x = blk + (g.start - blk_start) + (int64_t)f * g.hop;
+    float2 v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const float2 a = x[n + q * M];
+        const float w = window[n + q * M];
+        v[q] = make_float2(a.x * w, a.y * w);
+    }
+    float2 s[Q];
+    if constexpr (Q == 2) {
+        s[0] = f2add(v[0], v[1]);
+        s[1] = f2sub(v[0], v[1]);
+    } else {
+        static_assert(Q == 4, "split");
+        // DFT4 over q: s_j = sum_q v_q (-i)^(q j)
+        const float2 t0 = f2add(v[0], v[2]), t1 = f2sub(v[0], v[2]);
+        const float2 t2 = f2add(v[1], v[3]), d = f2mi(f2sub(v[1], v[3]));
+        s[0] = f2add(t0, t2);
+        s[2] = f2sub(t0, t2);
+        s[1] = f2add(t1, d);
+        s[3] = f2sub(t1, d);
+    }
+    float2* o = y + ((int64_t)blockIdx.z * fstride + f) * N + n;
+    o[0] = s[0];
+#pragma unroll
+    for (int j = 1; j < Q; ++j) o[j * M] = f2mul(s[j], tw[(n * j) & (N - 1)]);
+}
+
+// ---- the four-step form (N = 32768, 65536; OWRX_WF_KERNEL=fourstep, A/B) ------------------
 // N = N1 * N2, n = N2*n1 + n2, k = k1 + N1*k2:
 //   X[k1 + N1 k2] = sum_n2 W_N2^(n2 k2) * W_N^(n2 k1) * sum_n1 x[N2 n1 + n2] W_N1^(n1 k1).
 // wf_fft4_cols: 32 columns n2 of one frame per workgroup -- windowed loads (32 consecutive
@@ -811,14 +863,17 @@ __global__ void __launch_bounds__(256)
 wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
             const float* __restrict__ carry_in, float* __restrict__ carry_out, int N,
             float add_corr, int adpcm, int16_t* __restrict__ s16_out,
-            float* __restrict__ f32_out) {
+            float* __restrict__ f32_out, int qlog) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const WfRow r = rows[blockIdx.y];
     float s = r.use_carry ? carry_in[i] : 0.0f;
+    // bin i's place in a partial row: natural, or j-major after the DIF split (bin Q k + j at
+    // j (N / Q) + k)
+    const int pi = qlog ? ((i & ((1 << qlog) - 1)) * (N >> qlog)) + (i >> qlog) : i;
     // the groups' partials in order (the row's summation order); loads batched 8 deep
-    const float* pp = partial + (int64_t)r.first_group * N + i;
+    const float* pp = partial + (int64_t)r.first_group * N + pi;
     int gi = 0;
     for (; gi + 8 <= r.ngroups; gi += 8) {
         float v[8];
@@ -958,9 +1013,18 @@ static bool wf_force_r16() {
 
 bool wf_uses_l32(int logn) { return logn == 14 && !wf_force_r16(); }
 
+// N = 32768, 65536: the DIF split onto wf_fft_l32 (OWRX_WF_KERNEL=fourstep: the four-step, A/B)
+bool wf_uses_split(int logn) {
+    static const bool fourstep = [] {
+        const char* s = getenv("OWRX_WF_KERNEL");
+        return s && strcmp(s, "fourstep") == 0;
+    }();
+    return (logn == 15 || logn == 16) && !fourstep;
+}
+
 static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw,
-                                 float* partial, hipStream_t st) {
+                                 float* partial, hipStream_t st, int qlog = 0, int fstride = 0) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)wf_fft_l32,
@@ -969,9 +1033,21 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(wf_fft_l32, dim3(ngroups), dim3(WfL32::NT), WfL32::kLds, st, blk, blk_start,
-                       groups, window, tw, partial);
+    hipLaunchKernelGGL(wf_fft_l32, dim3(ngroups << qlog), dim3(WfL32::NT), WfL32::kLds, st, blk,
+                       blk_start, groups, window, tw, partial, qlog, fstride);
     return hipGetLastError();
+}
+
+// N = 16384 << QLOG: the split into sub-frames, then wf_fft_l32 on them (window of ones: the
+// split applied the frame's window)
+template <int QLOG>
+static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                   int ngroups, int fpg, const float* window, const float* ones,
+                                   const float2* tw, float* partial, float2* scratch, hipStream_t st) {
+    if (!scratch || !ones || fpg < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wf_dif_split<QLOG>, dim3(16384 / 256, fpg, ngroups), dim3(256), 0, st, blk,
+                       blk_start, groups, window, tw, fpg, scratch);
+    return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, st, QLOG, fpg);
 }
 
 template <int LOGN>
@@ -979,14 +1055,20 @@ static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfG
                                  int ngroups, const float* window, const float2* tw, float* partial,
                                  hipStream_t st) {
     if constexpr (LOGN == 14)
-        if (!wf_force_r16()) return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        if (!wf_force_r16())
+            return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, st);
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
 
 
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
-                         int ngroups, const float* window, const float2* tw, float* partial,
-                         float2* scratch, hipStream_t st) {
+                         int ngroups, int fpg, const float* window, const float* ones,
+                         const float2* tw, float* partial, float2* scratch, hipStream_t st) {
+    if (wf_uses_split(logn))
+        return logn == 15 ? launch_fft_split<1>(blk, blk_start, groups, ngroups, fpg, window, ones, tw,
+                                                partial, scratch, st)
+                          : launch_fft_split<2>(blk, blk_start, groups, ngroups, fpg, window, ones, tw,
+                                                partial, scratch, st);
     switch (logn) {
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
@@ -1006,8 +1088,11 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st) {
+    int logn = 0;
+    while ((1 << logn) < N) ++logn;
+    const int qlog = wf_uses_split(logn) ? logn - 14 : 0;
     hipLaunchKernelGGL(wf_finalize, dim3((N + 255) / 256, nrows), dim3(256), 0, st, partial,
-                       rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out);
+                       rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out, qlog);
     return hipGetLastError();
 }
 

@@ -79,7 +79,8 @@ def test_waterfall_c2_full_averaging(amd, parity_report):
 
 
 def test_waterfall_c4_full_averaging(amd, parity_report):
-    """C4 waterfall: 61.44 Msps, 65536 bins (four-step FFT), avg 149 frames per row."""
+    """C4 waterfall: 61.44 Msps, 65536 bins (DIF split onto the 16384-point kernel), avg 149
+    frames per row."""
     _waterfall_full(amd, 61440000, 65536, 149, 2, 1 << 21, parity_report, "waterfall_c4_avg149")
 
 

@@ -252,11 +252,12 @@ def test_engine_ring_ingest_commit(amd):
     assert a.shape[0] == 3 and np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("variant", ["r16"])
-def test_waterfall_kernel_variants(variant):
-    """The A/B waterfall kernel (OWRX_WF_KERNEL=r16: the radix-16 kernel at N = 16384 instead of
-    wf_fft_l32) gives the oracle's rows at N = 1024 .. 16384 (<= 2e-3 dB, as the production
-    kernels); it runs in a child process since the selection is read once per process."""
+@pytest.mark.parametrize("variant,sizes", [("r16", 5), ("fourstep", 2)])
+def test_waterfall_kernel_variants(variant, sizes):
+    """The A/B waterfall kernels (OWRX_WF_KERNEL=r16: the radix-16 kernel at N = 16384 instead of
+    wf_fft_l32; =fourstep: the four-step FFT at N = 32768 / 65536 instead of the DIF split onto
+    wf_fft_l32) give the oracle's rows (<= 2e-3 dB, as the production kernels); each runs in a
+    child process since the selection is read once per process."""
     import json
     import os
     import subprocess
@@ -267,7 +268,7 @@ def test_waterfall_kernel_variants(variant):
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     errs = json.loads(r.stdout.strip().splitlines()[-1])
-    assert len(errs) == 5 and all(e is not None and e < 2e-3 for e in errs.values()), errs
+    assert len(errs) == sizes and all(e is not None and e < 2e-3 for e in errs.values()), errs
 
 
 def test_wide_serial_streams_same_audio():

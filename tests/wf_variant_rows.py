@@ -1,7 +1,7 @@
 """Waterfall rows of the kernel OWRX_WF_KERNEL selects (run as a subprocess by
 tests/test_gpu_parity.py::test_waterfall_kernel_variants: the selection is read once per
-process).  For each FFT size 1024 .. 16384 prints the worst |dB| difference to the oracle's
-double-precision rows, one JSON object."""
+process).  For each FFT size it covers (1024 .. 16384; 32768 and 65536 for "fourstep") prints
+the worst |dB| difference to the oracle's double-precision rows, one JSON object."""
 import json
 import os
 import sys
@@ -16,7 +16,10 @@ import openwebrx_amd as amd  # noqa: E402
 from openwebrx_amd import synth  # noqa: E402
 
 out = {}
-for N, fs in [(1024, 250000), (2048, 1000000), (4096, 2400000), (8192, 4800000), (16384, 10000000)]:
+sizes = [(1024, 250000), (2048, 1000000), (4096, 2400000), (8192, 4800000), (16384, 10000000)]
+if os.environ.get("OWRX_WF_KERNEL") == "fourstep":
+    sizes = [(32768, 20000000), (65536, 61440000)]
+for N, fs in sizes:
     avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
     avg = min(avg, 4)
     n = hop * avg * 3 + N + 1000

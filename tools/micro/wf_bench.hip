@@ -161,7 +161,7 @@ int main(int argc, char** argv) {
                }));
         report("l32", G, F, time_us([&] {
                    hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, (int64_t)0, dg,
-                                      dwin, dtw, dpart2);
+                                      dwin, dtw, dpart2, 0, 0);
                }));
         const int nwg = frame_table(F);
         report("h32", G, F, time_us([&] {
@@ -191,7 +191,7 @@ int main(int argc, char** argv) {
         }
         printf("       lean vs r16: max rel %.3e, rel-RMS %.3e\n", worst, sqrt(rms_d / rms_a));
         hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, (int64_t)0, dg, dwin, dtw,
-                           dpart2);
+                           dpart2, 0, 0);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(b.data(), dpart2, sizeof(float) * b.size(), hipMemcpyDeviceToHost));
         worst = 0; rms_d = 0;
@@ -225,7 +225,7 @@ int main(int argc, char** argv) {
             // l32 phase stamps of wave 0: medians over workgroups
             time_us([&] {
                 hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, (int64_t)0, dg,
-                                   dwin, dtw, dpart2);
+                                   dwin, dtw, dpart2, 0, 0);
             });
             std::vector<unsigned long long> st((size_t)1024 * 16);
             CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wf_stamp), sizeof(unsigned long long) * st.size()));
