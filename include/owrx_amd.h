@@ -40,6 +40,10 @@ extern "C" {
                                FractionalDecimator(FLOAT, IF/audio_rate, prefilter=True),
                                WfmDeemphasis(audio_rate, deemph_tau); no AGC.  The Selector
                                runs at the fixed 250 kHz IF (analog.py:81-82). */
+#define OWRX_DEMOD_SAM 4    /* SAm / RawSAm (csdr/chain/analog.py:141-167): Afc(afc_update,
+                               afc_sample) -> RealPart -> DcBlock -> Agc, or -> Gain(audio_gain)
+                               with audio_gain > 0 (RawSAm); RawAm (analog.py:23-31) is
+                               OWRX_DEMOD_AM with audio_gain > 0 (DcBlock -> Gain) */
 
 #define OWRX_OUT_S16 0      /* Convert(FLOAT, SHORT) */
 #define OWRX_OUT_ADPCM 1    /* Convert + AdpcmEncoder(sync=True) */
@@ -156,6 +160,10 @@ typedef struct {
     int32_t nr_enabled;      /* ClientAudioChain NoiseFilter(nr_threshold) before Convert
                                 (csdr/chain/clientaudio.py:12-13; owrx/dsp.py:496-509) */
     float   nr_threshold;    /* dB, the UI's -20..20 slider (htdocs/index.html:278) */
+    int32_t afc_update;      /* OWRX_DEMOD_SAM: Afc(updatePeriod, samplePeriod): SAm 10, 4;  */
+    int32_t afc_sample;      /*   RawSAm 50, 8 (analog.py:143-144, :158-159) */
+    float   audio_gain;      /* > 0 => Gain(FLOAT, audio_gain) after DcBlock instead of Agc
+                                (RawAm, RawSAm: 100, analog.py:29, :165); 0 => Agc */
 } owrx_chain_params;
 
 int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle);

@@ -19,7 +19,7 @@ OWRX_EINVAL = -22
 OWRX_ENOSPC = -28
 OWRX_ENODEV = -19
 
-DEMOD_NFM, DEMOD_AM, DEMOD_SSB, DEMOD_WFM = 0, 1, 2, 3
+DEMOD_NFM, DEMOD_AM, DEMOD_SSB, DEMOD_WFM, DEMOD_SAM = 0, 1, 2, 3, 4
 OUT_S16, OUT_ADPCM, OUT_F32, OUT_IQ, OUT_SEL = 0, 1, 2, 3, 4
 AGC_FAST, AGC_SLOW, AGC_MID, AGC_LAGGY = 0, 1, 2, 3
 
@@ -69,6 +69,9 @@ class ChainParams(ctypes.Structure):
         ("if_rate", ctypes.c_double),
         ("nr_enabled", ctypes.c_int32),
         ("nr_threshold", ctypes.c_float),
+        ("afc_update", ctypes.c_int32),
+        ("afc_sample", ctypes.c_int32),
+        ("audio_gain", ctypes.c_float),
     ]
 
 

@@ -26,9 +26,40 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include "../../include/owrx_amd.h"
 #include "design.h"
 #include "owrx_types.h"
+
+// OWRX_SEGV_TRACE=1: a host SIGSEGV prints the faulting thread's native frames (library +
+// offset, for addr2line) before the default action -- Python's faulthandler shows only the
+// Python frames of a crash inside a C-ABI call
+static void owrx_segv_trace(int sig) {
+    void* fr[48];
+    const int n = backtrace(fr, 48);
+    for (int i = 0; i < n; ++i) {
+        Dl_info di;
+        char line[512];
+        int len;
+        if (dladdr(fr[i], &di) && di.dli_fname)
+            len = snprintf(line, sizeof line, "  #%d %s +0x%lx (%s)\n", i, di.dli_fname,
+                           (unsigned long)((char*)fr[i] - (char*)di.dli_fbase),
+                           di.dli_sname ? di.dli_sname : "?");
+        else
+            len = snprintf(line, sizeof line, "  #%d %p\n", i, fr[i]);
+        if (len > 0) (void)!write(2, line, (size_t)std::min(len, (int)sizeof line - 1));
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+static const bool g_segv_trace = [] {
+    if (getenv("OWRX_SEGV_TRACE")) signal(SIGSEGV, owrx_segv_trace);
+    return true;
+}();
 
 namespace owrx {
 
@@ -77,6 +108,8 @@ hipError_t launch_chain_nr(const ChainPost* posts, int nposts, ChainCounts* coun
                            hipStream_t st);
 hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, ChainCounts* counts,
                              hipStream_t st);
+hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const int* sel, int nsel,
+                            hipStream_t st);
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st);
 
@@ -326,6 +359,7 @@ struct Slot {  // one block's outputs in flight on streams B / C
     int* d_sel = nullptr;   // post indices grouped by output mode, then long-bandpass posts
     int* h_sel = nullptr;
     int long_off = 0;
+    int afc_off = 0, nafc = 0;  // chain_afc's lane list (SAm chains) in d_sel
     ChainCounts* d_counts = nullptr;
     ChainCounts* h_counts = nullptr;
     uint8_t* d_out = nullptr;
@@ -896,9 +930,10 @@ static int ensure_post_capacity(owrx_engine* e) {
         free_slot_staging(s);
         HIPCHK(dalloc(&s.d_posts, cap));
         HIPCHK(halloc(&s.h_posts, cap));
-        // serial lane lists (+ demodulator-run padding), then the long-bandpass post list
-        HIPCHK(dalloc(&s.d_sel, (size_t)2 * cap + kSelPad));
-        HIPCHK(halloc(&s.h_sel, (size_t)2 * cap + kSelPad));
+        // serial lane lists (+ demodulator-run padding), then the long-bandpass post list and
+        // chain_afc's list (a RawSAm chain at 48 kHz is on both: up to cap entries each)
+        HIPCHK(dalloc(&s.d_sel, (size_t)3 * cap + kSelPad));
+        HIPCHK(halloc(&s.h_sel, (size_t)3 * cap + kSelPad));
         HIPCHK(dalloc(&s.d_counts, cap));
         HIPCHK(dalloc(&s.d_out, (size_t)e->out_total));
         HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
@@ -1250,6 +1285,8 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
             memset(&p, 0, sizeof(p));
             const owrx_chain_params& q = c->prm;
             p.demod = q.demod;
+            p.afc_update = q.afc_update;
+            p.afc_sample = q.afc_sample;
             p.output = q.output;
             p.frac_enabled = q.frac_rate != 1.0;
             p.frac_rate = q.frac_rate;
@@ -1296,6 +1333,10 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
             if (q.agc_initial_gain >= 0) p.agc.initial_gain = q.agc_initial_gain;
             if (q.agc_max_gain >= 0) p.agc.max_gain = q.agc_max_gain;
             if (q.demod == OWRX_DEMOD_WFM) p.agc.max_gain = std::max(1.0f, p.agc.max_gain);
+            if (q.audio_gain > 0) {  // Gain(audio_gain) replaces the Agc (post_serial_front)
+                p.fixed_gain = 1;
+                p.agc.max_gain = q.audio_gain;
+            }
             p.pstate = c->d_pstate;
             p.sstate = c->d_sstate;
             p.ddc_buf = c->d_ddc;
@@ -1381,8 +1422,10 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
             for (auto& v : b) v.clear();
     for (int i = 0; i < np; ++i) {
         const ChainPost& p = S.h_posts[i];
-        if (p.output >= 0 && p.output < 3 && p.demod >= 0 && p.demod < 4)
-            bk[p.output][p.nr_enabled != 0][p.demod].push_back(i);
+        // SAm's serial part after chain_afc is AM's (DcBlock -> Agc / Gain)
+        const int dm = p.demod == OWRX_DEMOD_SAM ? OWRX_DEMOD_AM : p.demod;
+        if (p.output >= 0 && p.output < 3 && dm >= 0 && dm < 4)
+            bk[p.output][p.nr_enabled != 0][dm].push_back(i);
     }
     int nfill = 0;
     for (int o = 0; o < 3; ++o)
@@ -1396,6 +1439,12 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
             S.nsel[o][nr] = nfill - S.off[o][nr];
         }
     S.nfill = nfill;
+    // SAm chains: chain_afc's lane list after the long-bandpass list
+    S.afc_off = S.long_off + S.nlong;
+    S.nafc = 0;
+    for (int i = 0; i < np; ++i)
+        if (S.h_posts[i].demod == OWRX_DEMOD_SAM && S.h_posts[i].output != OWRX_OUT_IQ)
+            S.h_sel[S.afc_off + S.nafc++] = i;
     S.post_epoch = e->chain_epoch;
     S.post_dirty = one_shot;
     return OWRX_OK;
@@ -1509,7 +1558,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         }
         job(S.d_posts, S.h_posts, (int64_t)sizeof(ChainPost) * np);
         job(S.d_sel, S.h_sel, (int64_t)sizeof(int) * S.nfill);
-        job(S.d_sel + S.long_off, S.h_sel + S.long_off, (int64_t)sizeof(int) * S.nlong);
+        job(S.d_sel + S.long_off, S.h_sel + S.long_off, (int64_t)sizeof(int) * (S.nlong + S.nafc));
         if (nj > 0) {
             hipLaunchKernelGGL(copy_jobs, dim3((unsigned)std::min<int64_t>(64, (maxb + 4095) / 4096), nj),
                                dim3(256), 0, e->sA, S.h_jobs);
@@ -1588,6 +1637,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             HIPCHK(hipMemsetAsync(c->d_nr_ola, 0, sizeof(float) * kNrHop, sB));
         }
         e->nr_resets.clear();
+        // SAm: Afc -> RealPart per chain (serial, lane per chain) ahead of the front
+        if (S.nafc > 0) HIPCHK(launch_chain_afc(S.d_posts, S.d_counts, S.d_sel + S.afc_off, S.nafc, sB));
         const int dbg = (e->debug && S.d_dbg) ? 1 : 0;
         for (int o = 0; o < 3; ++o)
             for (int nr = 0; nr < 2; ++nr)
@@ -2127,7 +2178,7 @@ static int chain_validate(const owrx_chain_params* p) {
                    ? OWRX_EINVAL : OWRX_OK;
     if (!p || p->decimation < 1 || p->transition <= 0 || p->cutoff <= 0 || p->frac_rate <= 0 ||
         p->sq_length <= 0 || p->sq_length > (1 << 20) || p->sq_decimation <= 0 || p->demod < 0 ||
-        p->demod > OWRX_DEMOD_WFM || p->output < 0 || p->output > OWRX_OUT_SEL ||
+        p->demod > OWRX_DEMOD_SAM || p->output < 0 || p->output > OWRX_OUT_SEL ||
         p->output == OWRX_OUT_IQ || p->audio_rate <= 0 ||
         p->agc_profile < 0 || p->agc_profile > 3)
         return OWRX_EINVAL;
@@ -2136,6 +2187,12 @@ static int chain_validate(const owrx_chain_params* p) {
     if (p->demod == OWRX_DEMOD_WFM && (p->if_rate <= 0 || p->if_rate / p->audio_rate < 1.0))
         return OWRX_EINVAL;
     if (p->bandpass && (p->bp_transition <= 0 || p->bp_low >= p->bp_high)) return OWRX_EINVAL;
+    if (p->demod == OWRX_DEMOD_SAM &&
+        (p->afc_update <= 0 || p->afc_sample <= 0 || p->output == OWRX_OUT_SEL))
+        return OWRX_EINVAL;
+    if (p->audio_gain < 0 || (p->audio_gain > 0 && p->demod != OWRX_DEMOD_AM &&
+                              p->demod != OWRX_DEMOD_SAM))
+        return OWRX_EINVAL;
     return OWRX_OK;
 }
 
@@ -2288,7 +2345,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     }
     HIPCHK(palloc(e, &c->d_sq, (size_t)scap));
     // slack: the serial kernels read whole 64-sample chunks / 8-sample prefetches unguarded
-    for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_dem[i], (size_t)scap + 160));
+    // (SAm: the Selector output, cf32, until chain_afc leaves the RealPart in place)
+    const size_t dem_n = (p->demod == OWRX_DEMOD_SAM ? 2 : 1) * ((size_t)scap + 160);
+    for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_dem[i], dem_n));
     // + kNrN: a NoiseFilter emits up to one frame more than its input per step
     for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_s16[i], (size_t)scap + 160 + kNrN));
     int rc = chain_set_bandpass_taps(e, c.get());

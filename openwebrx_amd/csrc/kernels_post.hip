@@ -424,6 +424,10 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
         if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;
         if (P.tap_sq && i < P.tap_sq_cap) P.tap_sq[i] = x;  // selectorBuffer readers
         if (P.sf_n > 0) P.sf_buf[sf_fill + i] = x;  // Selector output -> secondary FFT
+        if (P.demod == OWRX_DEMOD_SAM) {  // SAm: the Selector output for chain_afc (cf32)
+            gp(reinterpret_cast<float2*>(P.dem))[i] = x;
+            continue;
+        }
         float v;
         if (P.demod == 0 || P.demod == 3) {
             float2 prev = fm_prev0;
@@ -630,7 +634,11 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     const int nfull = nmin / kSerChunk;  // chunks in which every active lane has kSerChunk samples
     const AgcParams agcp = Pp->agc;
     ChainStateS* sp = Pp->sstate;
-    const int demod = __builtin_amdgcn_readfirstlane(Pp->demod);  // uniform (see ser_lane)
+    // uniform (see ser_lane); SAm continues as AM after chain_afc (DcBlock -> Agc / Gain)
+    int demod = __builtin_amdgcn_readfirstlane(Pp->demod);
+    if (demod == OWRX_DEMOD_SAM) demod = OWRX_DEMOD_AM;
+    // Gain(agc.max_gain) instead of the Agc (RawAm / RawSAm): envelope 0 selects the clamp
+    const bool fixed_gain = Pp->fixed_gain != 0;
 
     // Data movement is lane = chain, in quads of samples (samples 4q .. 4q+3 of a chunk).
     // Input staging: the recurrences are a few dependent VALU ops per sample, so a global load
@@ -695,7 +703,8 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     }
                     // WFm has no Agc (csdr/chain/analog.py:66-71): envelope = reference makes
                     // the gain exactly 1 (correctly rounded x / x; the host keeps max_gain >= 1)
-                    dst[i + j][lane] = make_float2(u, DM == 3 ? agcp.reference : agc.env);
+                    dst[i + j][lane] = make_float2(u, DM == 3 ? agcp.reference
+                                                          : fixed_gain ? 0.0f : agc.env);
                     if (!FULL && base + i + j >= n) {  // past this lane's end: keep state
                         deemph_y = ky;
                         dc_xp = kx;
@@ -849,6 +858,48 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             __syncthreads();
         }
     }
+}
+
+// Afc -> RealPart of the SAm / RawSAm chains (csdr/chain/analog.py:141-167), one LANE per chain
+// (64 per workgroup) on the serial stream ahead of post_serial_front: the front left the
+// Selector output (cf32) in the chain's dem slot; the corrected real part goes back in place
+// (sample i's float lands at float index i, below the cf32 still to be read at 2 (i + 1)).
+// Loads run 8 samples ahead of the AFC recurrence (double sincos per sample).
+__global__ void __launch_bounds__(64)
+chain_afc(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
+          const int* __restrict__ sel, int nsel) {
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= nsel) return;
+    const int c = sel[k];
+    const ChainPost& P = posts[c];
+    const int n = (int)counts[c].n_sq;
+    const int U = P.afc_update, S = P.afc_sample;
+    AfcState st = P.sstate->afc;
+    const float2* in = reinterpret_cast<const float2*>(P.dem);
+    float* out = P.dem;
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {
+        float2 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = in[i + u];
+        float y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) y[u] = afc_step(st, x[u], U, S).x;  // RealPart
+#pragma unroll
+        for (int u = 0; u < 8; ++u) out[i + u] = y[u];
+    }
+    for (; i < n; ++i) {
+        const float2 x = in[i];
+        out[i] = afc_step(st, x, U, S).x;
+    }
+    P.sstate->afc = st;
+}
+
+hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const int* sel, int nsel,
+                            hipStream_t st) {
+    if (nsel <= 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_afc, dim3((nsel + 63) / 64), dim3(64), 0, st, posts, counts, sel, nsel);
+    return hipGetLastError();
 }
 
 // AdpcmEncoder(sync=True), one LANE per chain (64 chains per workgroup).  IMA-ADPCM's

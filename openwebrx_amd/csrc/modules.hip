@@ -18,12 +18,7 @@ struct ModState {
     float2 fm_last;
     float yp, xp, yp2;
     AgcState agc;
-    // Afc: NCO phase / frequency (rad, rad per sample), pair accumulator, the corrected sample
-    // of the last pair point, samples seen, pairs accumulated
-    double afc_ph, afc_w, afc_re, afc_im;
-    float2 afc_prev;
-    int64_t afc_n;
-    int32_t afc_pairs;
+    AfcState afc;  // Afc (owrx_dev.h afc_step)
     AdpcmState adpcm;
     int64_t adpcm_bytes;
     int32_t has_left;
@@ -71,42 +66,9 @@ __global__ void mod_serial(ModParams p, const void* __restrict__ in, int64_t n,
             for (int64_t k = 0; k < n; ++k) of[k] = agc_step(iff[k], p.agc, s.agc);
             o = n;
             break;
-        case OWRX_MOD_AFC: {
-            // Afc(updatePeriod U, samplePeriod S), the build's choice (csdr's is not in the
-            // reference): y = x e^{-j ph}, ph += w; every S samples the pair product
-            // y[n] conj(y[n - S]) is summed, and after U pairs w += arg(sum) / (2 S): the
-            // residual rotation per sample, half-corrected per update
+        case OWRX_MOD_AFC: {  // Afc(updatePeriod U, samplePeriod S): owrx_dev.h afc_step
             float2* oc = (float2*)out;
-            const int U = p.i0, S = p.i1;
-            for (int64_t k = 0; k < n; ++k) {
-                double sn, cs;
-                sincos(s.afc_ph, &sn, &cs);
-                const float c = (float)cs, si = (float)sn;
-                const float2 x = ic[k];
-                float2 y;
-                {
-#pragma clang fp contract(off)
-                    y = make_float2(x.x * c + x.y * si, x.y * c - x.x * si);
-                }
-                s.afc_ph += s.afc_w;
-                if (s.afc_ph > M_PI) s.afc_ph -= 2.0 * M_PI;
-                else if (s.afc_ph < -M_PI) s.afc_ph += 2.0 * M_PI;
-                if (s.afc_n % S == 0) {
-                    if (s.afc_n >= S) {
-                        const double pr = s.afc_prev.x, pi = s.afc_prev.y;
-                        s.afc_re += (double)y.x * pr + (double)y.y * pi;
-                        s.afc_im += (double)y.y * pr - (double)y.x * pi;
-                        if (++s.afc_pairs == U) {
-                            s.afc_w += atan2(s.afc_im, s.afc_re) / (2.0 * S);
-                            s.afc_re = s.afc_im = 0.0;
-                            s.afc_pairs = 0;
-                        }
-                    }
-                    s.afc_prev = y;
-                }
-                s.afc_n++;
-                oc[k] = y;
-            }
+            for (int64_t k = 0; k < n; ++k) oc[k] = afc_step(s.afc, ic[k], p.i0, p.i1);
             o = n;
             break;
         }

@@ -133,6 +133,46 @@ OWRX_DEV float dcblock_step(float x, float& xp, float& yp) {
     return y;
 }
 
+// Afc(updatePeriod U, samplePeriod S) of SAm / RawSAm (csdr/chain/analog.py:141-167), the build's
+// choice (csdr's algorithm is not in the reference; oracle afc): y = x e^{-j ph}, ph += w (ph
+// wrapped to [-pi, pi]); every S samples the pair product y[n] conj(y[n - S]) is summed, and
+// after U pairs w += arg(sum) / (2 S).  Phase and frequency in double, the rotation in float.
+struct AfcState {
+    double ph, w, re, im;
+    float2 prev;
+    int64_t n;
+    int32_t pairs;
+    int32_t pad;
+};
+OWRX_DEV float2 afc_step(AfcState& s, float2 x, int U, int S) {
+    double sn, cs;
+    sincos(s.ph, &sn, &cs);
+    const float c = (float)cs, si = (float)sn;
+    float2 y;
+    {
+#pragma clang fp contract(off)
+        y = make_float2(x.x * c + x.y * si, x.y * c - x.x * si);
+    }
+    s.ph += s.w;
+    if (s.ph > M_PI) s.ph -= 2.0 * M_PI;
+    else if (s.ph < -M_PI) s.ph += 2.0 * M_PI;
+    if (s.n % S == 0) {
+        if (s.n >= S) {
+            const double pr = s.prev.x, pi = s.prev.y;
+            s.re += (double)y.x * pr + (double)y.y * pi;
+            s.im += (double)y.y * pr - (double)y.x * pi;
+            if (++s.pairs == U) {
+                s.w += atan2(s.im, s.re) / (2.0 * S);
+                s.re = s.im = 0.0;
+                s.pairs = 0;
+            }
+        }
+        s.prev = y;
+    }
+    s.n++;
+    return y;
+}
+
 // Agc(FLOAT) (analog.py:13-15, 38-40, 121-122): continuous attack/decay envelope follower,
 // gain = reference / envelope clamped to max_gain (see oracle/csdr_oracle.c orc_agc).
 OWRX_DEV float agc_step(float x, const AgcParams& p, AgcState& s) {

@@ -63,6 +63,7 @@ struct ChainStateS {
     AdpcmState adpcm;
     int32_t has_left;      // ADPCM: one encoded nibble waiting for its pair
     int32_t left_code;
+    AfcState afc;          // SAm / RawSAm (chain_afc)
 };
 // NoiseFilter state (stream B; the host zeroes it with the filter's buffers on (re)start)
 struct NrState {
@@ -74,6 +75,8 @@ struct NrState {
 struct ChainPost {
     // configuration
     int32_t demod;         // OWRX_DEMOD_*
+    int32_t afc_update, afc_sample;  // OWRX_DEMOD_SAM: Afc(updatePeriod, samplePeriod)
+    int32_t fixed_gain;    // Gain(agc.max_gain) instead of Agc (RawAm, RawSAm)
     int32_t output;        // OWRX_OUT_*
     int32_t frac_enabled;
     int32_t bp_ntaps;      // 0 => no bandpass

@@ -22,9 +22,19 @@ MODE_BANDPASS = {  # owrx/modes.py:124-129
     "usb": (150, 3000),
     "cw": (700, 900),
     "wfm": (-124000, 124000),  # owrx/modes.py:125
+    "sam": (-4700, 4700),      # owrx/modes.py:130
+    "rawam": (-10000, 10000),  # owrx/modes.py:132
+    "rawsam": (-10000, 10000),  # owrx/modes.py:133
 }
 MODE_DEMOD = {"nfm": _lib.DEMOD_NFM, "am": _lib.DEMOD_AM, "usb": _lib.DEMOD_SSB,
-              "lsb": _lib.DEMOD_SSB, "cw": _lib.DEMOD_SSB, "wfm": _lib.DEMOD_WFM}
+              "lsb": _lib.DEMOD_SSB, "cw": _lib.DEMOD_SSB, "wfm": _lib.DEMOD_WFM,
+              "sam": _lib.DEMOD_SAM, "rawam": _lib.DEMOD_AM, "rawsam": _lib.DEMOD_SAM}
+# HdAudio demodulators: the Selector runs at the hd output rate (owrx/dsp.py:150-166)
+HD_MODES = ("rawam", "rawsam")
+# SAm: Afc(10, 4), Agc(Slow, initial gain 200); RawSAm: Afc(50, 8), Gain(100); RawAm: Gain(100)
+# (csdr/chain/analog.py:23-31, 141-167)
+MODE_AFC = {"sam": (10, 4), "rawsam": (50, 8)}
+MODE_GAIN = {"rawam": 100.0, "rawsam": 100.0}
 WFM_IF_RATE = 250000  # WFm.getFixedIfSampleRate (csdr/chain/analog.py:81-82)
 
 
@@ -80,9 +90,11 @@ def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=Non
     (ClientDemodulatorChain._getSelectorOutputRate, owrx/dsp.py:150-158) and the audio at
     hd_output_rate (owrx/dsp.py:494, :160-166)."""
     wfm = mode == "wfm"
-    audio_rate = hd_output_rate if wfm else output_rate
+    audio_rate = hd_output_rate if wfm or mode in HD_MODES else output_rate
     if wfm:
         output_rate = WFM_IF_RATE
+    elif mode in HD_MODES:
+        output_rate = hd_output_rate
     d, frac, tbw, cutoff = decimation(input_rate, output_rate)
     if bandpass is None:
         bandpass = MODE_BANDPASS.get(mode)
@@ -109,7 +121,8 @@ def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=Non
     if agc_profile is None:  # NFm/Am: SLOW (analog.py:35,12); Ssb: ssb_agc_profile "Fast"
         agc_profile = _lib.AGC_FAST if demod == _lib.DEMOD_SSB else _lib.AGC_SLOW
     p.agc_profile = agc_profile
-    p.agc_initial_gain = 200.0 if demod == _lib.DEMOD_AM else -1.0   # Am: setInitialGain(200)
+    # Am, SAm: setInitialGain(200)
+    p.agc_initial_gain = 200.0 if demod in (_lib.DEMOD_AM, _lib.DEMOD_SAM) else -1.0
     p.agc_max_gain = 3.0 if demod == _lib.DEMOD_NFM else -1.0        # NFm: setMaxGain(3)
     p.audio_rate = audio_rate
     p.output = output
@@ -118,6 +131,8 @@ def chain_params(input_rate, offset, mode="nfm", output_rate=12000, bandpass=Non
     if wfm:
         p.if_rate = float(WFM_IF_RATE)
         p.deemph_tau = f32(wfm_deemphasis_tau)
+    p.afc_update, p.afc_sample = MODE_AFC.get(mode, (0, 0))
+    p.audio_gain = MODE_GAIN.get(mode, 0.0)
     return p
 
 

@@ -106,8 +106,9 @@ def _readers_of(buf):
 # (selectorBuffer: the demodulator; audioBuffer: ClientAudioChain's first module)
 def _continuations():
     from . import modules as M
-    return (M.FmDemod, M.AmDemod, M.RealPart, M.FractionalDecimator, M.Bandpass, M.Squelch,
-            M.Limit, M.NfmDeemphasis, M.WfmDeemphasis, M.DcBlock, M.Agc, M.NoiseFilter,
+    return (M.FmDemod, M.AmDemod, M.Afc, M.RealPart, M.FractionalDecimator, M.Bandpass,
+            M.Squelch, M.Limit, M.NfmDeemphasis, M.WfmDeemphasis, M.DcBlock, M.Agc, M.Gain,
+            M.NoiseFilter,
             M.Convert, M.AdpcmEncoder, M.FirDecimate, M.LogAveragePower, M.LogPower, M.FftSwap,
             M.FftAdpcm)
 
@@ -224,7 +225,7 @@ def plan_segment(head):
     if fir is None:
         return None
     chain_next = (M.FractionalDecimator, M.Bandpass, M.Squelch, M.FmDemod, M.AmDemod,
-                  M.RealPart)
+                  M.RealPart, M.Afc)
     if fir.writer is not None and (i == len(mods) or not isinstance(mods[i], chain_next)):
         # Shift -> FirDecimate -> Buffer(COMPLEX_FLOAT): the service Resampler
         # (owrx/source/resampler.py:11-26); the engine emits the cf32 DDC output itself
@@ -240,8 +241,8 @@ def plan_segment(head):
     def _selector_output():
         """Selector output read by something the engine does not fuse (an IQ-input decoder:
         ServiceDemodulatorChain with Selector(withSquelch=False), owrx/service/chain.py:7-23;
-        SAm's Afc; a demodulator without Agc): the engine emits the cf32 Selector output itself
-        and whatever reads it runs as standalone modules."""
+        a demodulator chain the engine does not know): the engine emits the cf32 Selector output
+        itself and whatever reads it runs as standalone modules."""
         if selector_last.writer is None or selector_last is fir:
             return None
         p = dict(shift_rate=shift.rate, decimation=fir.decimation, transition=fir.transition,
@@ -263,7 +264,15 @@ def plan_segment(head):
 
     fm = take(M.FmDemod)
     wfm = None
-    if fm is not None:
+    afc = None
+    if fm is None:
+        afc = take(M.Afc)
+    if afc is not None:
+        # SAm / RawSAm (csdr/chain/analog.py:141-167): Afc -> RealPart -> DcBlock -> Agc / Gain
+        if take(M.RealPart) is None or take(M.DcBlock) is None:
+            return _selector_output()
+        demod, audio_rate = _lib.DEMOD_SAM, 12000
+    elif fm is not None:
         lim = take(M.Limit)
         if lim is None or lim.max_amplitude != 1.0:
             return None
@@ -286,10 +295,13 @@ def plan_segment(head):
     else:
         return _selector_output()
     agc = take(M.Agc) if wfm is None else None
+    gain = None
     if agc is None and wfm is None:
-        # a demodulator without Agc (RawAm: AmDemod -> DcBlock -> Gain(100),
-        # csdr/chain/analog.py:23-31): the Selector stays fused, the rest runs as GPU modules
-        return _selector_output()
+        # no Agc: RawAm (AmDemod -> DcBlock -> Gain(100), csdr/chain/analog.py:23-31) and
+        # RawSAm (:156-167) end in a FLOAT Gain, which the engine applies in the Agc's place
+        gain = take(M.Gain) if demod in (_lib.DEMOD_AM, _lib.DEMOD_SAM) else None
+        if gain is None or gain.input_format != M.Format.FLOAT or gain.gain <= 0:
+            return _selector_output()
     demod_last = mods[i - 1]  # writes audioBuffer (ClientDemodulatorChain._connect, dsp.py:86-92)
     nr = take(M.NoiseFilter)
     output = _lib.OUT_F32
@@ -310,7 +322,10 @@ def plan_segment(head):
              demod=demod, agc_profile=agc.profile.engine_id if agc is not None else 0,
              agc_initial_gain=-1.0 if agc is None or agc.initial_gain is None else agc.initial_gain,
              agc_max_gain=-1.0 if agc is None or agc.max_gain is None else agc.max_gain,
-             audio_rate=audio_rate, output=output, power_writer=None)
+             audio_rate=audio_rate, output=output, power_writer=None,
+             afc_update=afc.update_period if afc is not None else 0,
+             afc_sample=afc.sample_period if afc is not None else 0,
+             audio_gain=gain.gain if gain is not None else 0.0)
     if wfm is not None:
         p.update(wfm)
     p.update(nr_enabled=1 if nr is not None else 0,
@@ -591,5 +606,6 @@ def _compatible(kind, old, new):
         keys = ("decimation", "transition", "cutoff", "frac_rate", "bp_transition", "sq_length",
                 "sq_decimation", "sq_hang", "sq_flush", "sq_report", "demod", "agc_profile",
                 "agc_initial_gain", "agc_max_gain", "audio_rate", "output", "if_rate",
-                "deemph_tau", "nr_enabled", "nr_threshold")
+                "deemph_tau", "nr_enabled", "nr_threshold", "afc_update", "afc_sample",
+                "audio_gain")
     return all(old.get(k) == new.get(k) for k in keys)

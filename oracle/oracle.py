@@ -380,9 +380,12 @@ def stages(iq, p):
         dem = deemphasis(limit(fmdemod(sq)), c.deemph_alpha)
     elif p.demod == 1:
         dem = dcblock(amdemod(sq))
+    elif p.demod == 4:  # SAm / RawSAm: Afc -> RealPart -> DcBlock (csdr/chain/analog.py:141-167)
+        dem = dcblock(realpart(afc(sq, p.afc_update, p.afc_sample)))
     else:
         dem = realpart(sq)
-    ag = agc(dem, c.agc)
+    # RawAm / RawSAm: Gain(audio_gain) in the Agc's place (analog.py:29, :165)
+    ag = gain(dem, p.audio_gain) if getattr(p, "audio_gain", 0) > 0 else agc(dem, c.agc)
     out = dict(ddc=ddc, frac=fd, bandpass=bp, squelch=sq, smeter=power, demod=dem, agc=ag)
     if getattr(p, "nr_enabled", 0):
         out["nr"] = noise_filter(ag, p.nr_threshold)

@@ -169,12 +169,12 @@ def test_service_demodulator_chain_replay(step):
 @pytest.mark.parametrize("step", ["sam", "rawsam", "rawam"])
 def test_sam_chain_replay(step):
     """SAm / RawSAm / RawAm (csdr/chain/analog.py:23-31, 141-167) on the reference's
-    ClientDemodulatorChain (tests/golden/dsp_graph.json "sam", "rawsam", "rawam"): the fused
-    Selector (12 kHz; the Raw* chains at the 48 kHz hd rate) writes its output into the buffer
-    the standalone GPU modules read (OWRX_OUT_SEL); Afc -> RealPart -> DcBlock -> Agc(Slow,
-    initial gain 200) / Gain(100), or AmDemod -> DcBlock -> Gain(100), run as GPU modules.  The Selector output equals the oracle's squelch stage and
-    the Agc output the oracle's afc -> realpart -> dcblock -> agc of it, <=1e-5 rel-RMS; end to
-    end the bound adds the oracle's own sensitivity to the Selector difference (Afc parity
+    ClientDemodulatorChain (tests/golden/dsp_graph.json "sam", "rawsam", "rawam") fuse whole
+    into one engine chain (Selector at 12 kHz; the Raw* chains at the 48 kHz hd rate): Afc ->
+    RealPart in chain_afc, DcBlock -> Agc(Slow, initial gain 200) / Gain(100) in the serial
+    front, or AmDemod -> DcBlock -> Gain(100).  The Selector output the engine taps for the
+    test's reader equals the oracle's squelch stage, and the demodulator output (the audio tap)
+    the oracle's afc -> realpart -> dcblock -> agc / gain of it, <=1e-5 rel-RMS (Afc parity
     unpinned: csdr's Afc is not in the reference)."""
     import oracle
     from openwebrx_amd import _lib
@@ -211,7 +211,7 @@ def test_sam_chain_replay(step):
         col[1].join(5)
     assert fused, diag
     p = _graph.chain_params_struct(s["params"])
-    assert p.output == _lib.OUT_SEL
+    assert p.output == _lib.OUT_ADPCM and p.demod in (_lib.DEMOD_SAM, _lib.DEMOD_AM)
     tap = np.frombuffer(b"".join(sel[2]), np.complex64)
     ref = oracle.stages(iq, p)["squelch"]
     assert tap.size == ref.size > 8000, (tap.size, ref.size)

@@ -690,6 +690,56 @@ def _check_sampled_chains(iq, plist, chains, sample):
         assert np.mean(d <= 1) > 0.999, (c, np.mean(d <= 1))
 
 
+def test_sam_rawam_256_chains_one_engine(amd):
+    """256 SAm / RawAm / RawSAm chains in one engine (csdr/chain/analog.py:23-31, 141-167):
+    Afc in chain_afc (lane per chain), DcBlock -> Agc(Slow, 200) or Gain(100) in the serial
+    front, the Raw* Selectors at the 48 kHz hd rate (D = 50 at 2.4 Msps) next to SAm's 12 kHz
+    (D = 200).  Sampled chains of every mode vs the oracle: DDC and Selector output <= 1e-5
+    rel-RMS; the int16 audio within 1 LSB on 99.9 % of the oracle's tail (Afc -> RealPart ->
+    DcBlock -> Agc / Gain, or AmDemod -> DcBlock -> Gain) run on the engine's own Selector
+    output -- the Afc's frequency loop turns a 1e-7 input difference into a slowly drifting
+    phase, so end to end from the IQ only RawAm is held to that bar; every chain's audio length
+    as the oracle's."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    kinds = ("sam", "rawam", "rawsam")
+    C = 256
+    modes = [kinds[c % 3] for c in range(C)]
+    offs = synth.carrier_offsets(fs, C)
+    n = 1 << 20
+    iq, _ = synth.make_iq(fs, n, ["am"] * 24)  # AM carriers spread over the band
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16) for o, m in zip(offs, modes)]
+    eng, chains = _run_chains(amd, iq, fs, plist, 1 << 17)
+    for c in (0, 1, 2, 127, 128, 129, 253, 254, 255):
+        ref = oracle.stages(iq, plist[c])
+        ddc = chains[c].read_debug(0)
+        assert ddc.size == ref["ddc"].size and rel_rms(ddc, ref["ddc"]) < 1e-5, (c, modes[c])
+        sq = chains[c].read_debug(3)
+        assert sq.size == ref["squelch"].size and rel_rms(sq, ref["squelch"]) < 1e-5, c
+        p = plist[c]
+        if p.demod == amd._lib.DEMOD_SAM:
+            dem = oracle.dcblock(oracle.realpart(oracle.afc(sq, p.afc_update, p.afc_sample)))
+        else:
+            dem = oracle.dcblock(oracle.amdemod(sq))
+        ag = (oracle.gain(dem, p.audio_gain) if p.audio_gain > 0 else
+              oracle.agc(dem, oracle.agc_params(p.agc_profile, p.agc_initial_gain)))
+        want = oracle.convert_s16(ag)
+        s16 = np.frombuffer(chains[c].read_audio(), np.int16)
+        assert s16.size == ref["s16"].size == want.size, (c, modes[c], s16.size, ref["s16"].size)
+        d = np.abs(s16.astype(np.int32) - want)
+        assert np.mean(d <= 1) > 0.999, (c, modes[c], np.mean(d <= 1), np.max(d))
+        if modes[c] == "rawam":  # no Afc: end to end from the IQ as well
+            d = np.abs(s16.astype(np.int32) - ref["s16"])
+            assert np.mean(d <= 1) > 0.999, (c, modes[c], np.mean(d <= 1), np.max(d))
+    # the rest: as much audio as the oracle's chain of the same shape produces
+    sizes = {m: oracle.stages(iq, plist[kinds.index(m)])["s16"].size for m in kinds}
+    for c in range(C):
+        if c in (0, 1, 2, 127, 128, 129, 253, 254, 255):
+            continue
+        assert len(chains[c].read_audio()) == 2 * sizes[modes[c]], (c, modes[c])
+    eng.close()
+
+
 def test_c3_256_mixed_chains_10msps(amd):
     """BASELINE config 3 shape: 10 Msps, 256 chains (86 NFM + 85 USB + 85 CW), one
     (D=833, 22223-tap) design in one DDC group; sampled chains vs the oracle."""

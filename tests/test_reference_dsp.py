@@ -94,13 +94,16 @@ def test_service_demodulator_chains_fuse(step, output):
     assert p["sq_level"] == 0.0 and not s["tap_selector"] and not s["tap_audio"]
 
 
-def test_sam_keeps_the_selector_fused_and_runs_afc_on_the_gpu():
+def test_sam_fuses_whole():
     """SAm (csdr/chain/analog.py:141-154: Afc -> RealPart -> DcBlock -> Agc) set on the
-    reference's ClientDemodulatorChain: the Selector (with its squelch and s-meter) stays fused
-    and emits its output (OWRX_OUT_SEL) into the buffer the standalone GPU Afc reads; the rest
-    of the chain runs as standalone GPU modules."""
+    reference's ClientDemodulatorChain fuses whole into one engine chain: OWRX_DEMOD_SAM with
+    Afc(10, 4) and Agc(Slow, initial gain 200), ADPCM audio (Afc runs in chain_afc, lane per
+    chain, ahead of the serial front)."""
     s = dsp_replay.steps()["sam"]
-    assert s["fused"] and s["kind"] == "chain" and s["params"]["output"] == 4
+    assert s["fused"] and s["kind"] == "chain" and s["params"]["output"] == 1
+    p = s["params"]
+    assert (p["demod"], p["afc_update"], p["afc_sample"], p["audio_gain"]) == (4, 10, 4, 0.0)
+    assert (p["agc_profile"], p["agc_initial_gain"]) == (1, 200.0)
     cls = [d["class"] for _, d, _ in s["graph"]]
     assert cls.index("Squelch") < cls.index("Afc") < cls.index("RealPart") < cls.index("Agc")
     afc = [d for _, d, _ in s["graph"] if d["class"] == "Afc"][0]
@@ -109,10 +112,12 @@ def test_sam_keeps_the_selector_fused_and_runs_afc_on_the_gpu():
 
 def test_rawsam_runs_the_selector_at_the_hd_rate():
     """RawSAm (csdr/chain/analog.py:156-167) is HdAudio: ClientDemodulatorChain runs its
-    Selector at the hd output rate (48 kHz, owrx/dsp.py:150-166); still fused, its output
-    (OWRX_OUT_SEL) feeding Afc(50, 8) -> RealPart -> DcBlock -> Gain(100) on the GPU."""
+    Selector at the hd output rate (48 kHz, owrx/dsp.py:150-166); fused whole: Afc(50, 8) ->
+    RealPart -> DcBlock -> Gain(100) (audio_gain in the Agc's place)."""
     s = dsp_replay.steps()["rawsam"]
-    assert s["fused"] and s["params"]["output"] == 4 and s["params"]["decimation"] == 208
+    assert s["fused"] and s["params"]["output"] == 1 and s["params"]["decimation"] == 208
+    p = s["params"]
+    assert (p["demod"], p["afc_update"], p["afc_sample"], p["audio_gain"]) == (4, 50, 8, 100.0)
     cls = [d["class"] for _, d, _ in s["graph"]]
     assert cls.index("Squelch") < cls.index("Afc") < cls.index("RealPart") < cls.index("Gain")
     g = {d["class"]: d for _, d, _ in s["graph"]}
@@ -121,12 +126,12 @@ def test_rawsam_runs_the_selector_at_the_hd_rate():
 
 
 def test_rawam_and_ssbdigital_plan():
-    """RawAm (csdr/chain/analog.py:23-31: AmDemod -> DcBlock -> Gain(100), no Agc) keeps the
-    Selector fused (OWRX_OUT_SEL) and runs its demodulator as GPU modules; SsbDigital
-    (FixedAudioRateChain + HdAudio, :169-181) fuses whole as RealPart + Agc(Slow) with the
-    Selector at its fixed 48 kHz rate (D = 208)."""
+    """RawAm (csdr/chain/analog.py:23-31: AmDemod -> DcBlock -> Gain(100), no Agc) fuses whole
+    (OWRX_DEMOD_AM with audio_gain 100); SsbDigital (FixedAudioRateChain + HdAudio, :169-181)
+    fuses whole as RealPart + Agc(Slow) with the Selector at its fixed 48 kHz rate (D = 208)."""
     s = dsp_replay.steps()["rawam"]
-    assert s["fused"] and s["params"]["output"] == 4 and s["params"]["decimation"] == 208
+    assert s["fused"] and s["params"]["output"] == 1 and s["params"]["decimation"] == 208
+    assert (s["params"]["demod"], s["params"]["audio_gain"]) == (1, 100.0)
     cls = [d["class"] for _, d, _ in s["graph"]]
     assert cls.index("Squelch") < cls.index("AmDemod") < cls.index("DcBlock") < cls.index("Gain")
     s = dsp_replay.steps()["ssbdigital"]
