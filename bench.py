@@ -45,6 +45,7 @@ CONFIGS = {
 }
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: peak FP32 vector
 HBM_PEAK_GBS = 8000.0
+RIDGE = FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop per byte where the roofs meet
 
 
 def gen_stream_torch(torch, dev, fs, n, modes, offsets, seed=20251114):
@@ -430,6 +431,10 @@ def main():
     history = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
     eng = Engine(fs, max_block=block, device=local, history=history)
     eng.set_ddc_mode(args.ddc)
+    if world == 1:
+        # the stream is a resident recording: every block stays valid, so the host may run
+        # ahead of stream A (owrx_set_input_retention); the N>1 windows alternate two buffers
+        eng.set_input_retention(int(os.environ.get("OWRX_BENCH_RETENTION", "4")))
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:
@@ -460,19 +465,25 @@ def main():
             nbytes += len(wf.read())
         return nbytes
 
-    host_s = {"process": 0.0, "drain": 0.0}
+    host_s = {"process": 0.0, "drain": 0.0, "process_t": 0.0, "drain_t": 0.0}
 
-    def step(i):
+    def step(i, timed=False):
         t0 = time.perf_counter()
         n = _step(i)
-        host_s["drain"] += time.perf_counter() - t0
+        dt_ = time.perf_counter() - t0
+        host_s["drain"] += dt_
+        if timed:
+            host_s["drain_t"] += dt_
         return n
 
     def _step(i):
         if world == 1:
             t0 = time.perf_counter()
             eng.process_device(base + 8 * i * block, block)
-            host_s["process"] += time.perf_counter() - t0
+            dt_ = time.perf_counter() - t0
+            host_s["process"] += dt_
+            if i >= prime + args.warmup:
+                host_s["process_t"] += dt_
         else:  # the one exchange step: rank 0's block to every rank over RCCL
             t, off = bcast.step(i)
             # wait for this broadcast only (an event behind it on torch's stream), not for the
@@ -503,7 +514,7 @@ def main():
     out_bytes = 0
     marks = []
     for i in range(prime + args.warmup, nsteps):
-        out_bytes += step(i)
+        out_bytes += step(i, timed=True)
         marks.append(time.perf_counter() - t0)
     eng.sync()
     marks.append(time.perf_counter() - t0)
@@ -544,6 +555,13 @@ def main():
     else:
         achieved_tf = direct_flops / (ddc_ms / 1e3) / 1e12 if ddc_ms > 0 else 0.0
         mac_gbs = None
+    # the timed fc_mac launches (one per timed block: the first fast group's)
+    mac_flop_launch = d["ddc_mac_flop"] / tsteps if fast else None
+    mac_bytes_launch = d["ddc_mac_bytes"] / tsteps if fast else None
+    mac_ai = (d["ddc_mac_flop"] / d["ddc_mac_bytes"]) if fast and d["ddc_mac_bytes"] > 0 else None
+    mac_bound = ("hbm" if mac_ai is not None and mac_ai < RIDGE else "mfma") if fast else "valu"
+    if mac_gbs is None:
+        mac_gbs = 0.0
     wf_ms = d["gpu_ms_waterfall"]
     post_ms = d["gpu_ms_post"]
     wf_launches = d["waterfall_launches"]
@@ -637,27 +655,35 @@ def main():
             "realtime_factor": round(samples / dt / fs, 1),
             "chains_total": C * world,
             "roofline": {
-                "bound": "mfma" if fast else "valu",
+                "bound": mac_bound,
                 "kernel": ("fc_mac: the fast-convolution DDC's per-bin complex GEMM (frames x "
                            "chains x branches) on v_mfma_f32_16x16x4_f32" if fast else
                            "ddc_lds (direct polyphase Shift + FirDecimate)"),
-                "achieved": round(achieved_tf, 3),
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
+                "achieved": round(mac_gbs, 1) if mac_bound == "hbm" else round(achieved_tf, 3),
+                "peak": HBM_PEAK_GBS if mac_bound == "hbm" else FP32_PEAK_TFLOPS,
+                "unit": "GB/s" if mac_bound == "hbm" else "TFLOP/s",
+                "frac": round(mac_gbs / HBM_PEAK_GBS if mac_bound == "hbm"
+                              else achieved_tf / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
-                "algorithmic_bytes_per_launch": (round(d["ddc_mac_bytes"] / max(1, launches))
-                                                 if fast else None),
+                "algorithmic_bytes_per_launch": round(mac_bytes_launch) if mac_bytes_launch else None,
+                "algorithmic_flop_per_launch": round(mac_flop_launch) if mac_flop_launch else None,
+                "arithmetic_intensity_flop_per_byte": round(mac_ai, 2) if mac_ai else None,
+                "ridge_flop_per_byte": round(RIDGE, 2),
+                "achieved_tflops": round(achieved_tf, 3),
+                "mfma_frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                 "achieved_hbm_GBps": round(mac_gbs, 1) if mac_gbs else None,
                 "hbm_frac": round(mac_gbs / HBM_PEAK_GBS, 4) if mac_gbs else None,
-                "note": "achieved = algorithmic flop per launch (8 per complex MAC over the frames "
-                        "that carry outputs: 8 M Dp C F) / average launch time from HIP events "
-                        "around the kernel on the engine stream; peak = f32 MFMA = f32 vector "
-                        "(MI355X_MICROARCH.md).  Its operands stream once per launch (filter "
-                        "spectra W, branch spectra U, products Y: algorithmic_bytes_per_launch), "
-                        "so the HBM fraction is given beside it.  traffic = HBM bytes per launch "
-                        "from separate rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE "
-                        "passes of this config: " + traffic_src,
+                "note": "bound by the roofline model: the launch's algorithmic flop (8 per complex "
+                        "MAC over the frames that carry outputs: 8 M Dp C F) over its algorithmic "
+                        "bytes (filter spectra W, unique per chain and bin, + branch spectra U + "
+                        "products Y, each moved once) against the ridge 157.3 TFLOP/s / 8 TB/s; "
+                        "W's bytes do not depend on the frames per block, so 2^20-sample blocks "
+                        "(F ~ 10) sit under the ridge (HBM) and 2^22 (F ~ 31) over it (MFMA).  "
+                        "achieved = that bound's quantity / the average launch time from HIP "
+                        "events around the kernel on the engine stream; the other figure beside "
+                        "it.  traffic = HBM bytes per launch from separate rocprofv3 --pmc "
+                        "FETCH_SIZE (x2, gfx950) and WRITE_SIZE passes of this config: "
+                        + traffic_src,
                 "waterfall": None if wf_gbs is None else {
                     "bound": "hbm",
                     "kernel": " + ".join(wf_kernels) + " (FftChain: Hamming FFT, |X|^2 summed "
@@ -704,7 +730,11 @@ def main():
             },
             "host_ms_per_step": {k[8:]: round(d[k] / args.steps, 3) for k in
                                  ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots",
-                                  "host_ms_wait_rows")},
+                                  "host_ms_wait_rows", "host_ms_build", "host_ms_launch",
+                                  "host_ms_collect")},
+            "host_ms_per_step_python": {
+                "process_device": round(1e3 * host_s["process_t"] / args.steps, 3),
+                "step_total": round(1e3 * host_s["drain_t"] / args.steps, 3)},
             "realtime": rt,
             "realtime_churn": churn,
             "max_realtime_chains": cap["max_realtime_chains"] if cap else None,

@@ -96,6 +96,12 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq_cs16, int64_t nsamples, 
  * the block (with its history) must stay unmodified until the next owrx_process_device /
  * owrx_commit / owrx_push_iq / owrx_sync call on this engine has returned. */
 int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t nsamples);
+/* Callers whose input blocks stay valid longer (a resident recording, a ring of windows): with
+ * blocks = r the block handed to owrx_process_device (with its history) must stay unmodified
+ * until r further owrx_process_device / owrx_commit calls (or owrx_sync) have returned, and the
+ * engine waits only for block k - r + 1's stream-A work before returning from block k, so the
+ * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 15. */
+int owrx_set_input_retention(owrx_engine* e, int blocks);
 /* Device window slot for the next block (write there, e.g. with ncclBroadcast), then commit. */
 int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity);
 int owrx_commit(owrx_engine* e, int64_t nsamples);
@@ -253,6 +259,9 @@ typedef struct {
     int64_t pipeline_drains;   /* full drains of the block pipeline (owrx_sync, waterfall
                                   reconfiguration, staging growth); chain joins / leaves and
                                   their setters do not drain */
+    double  host_ms_build;     /* host time building a block's chain descriptors (of process) */
+    double  host_ms_launch;    /* host time enqueueing its kernels, copies and events */
+    double  host_ms_collect;   /* host time moving finished blocks into the output rings */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

@@ -103,6 +103,9 @@ class Stats(ctypes.Structure):
         ("waterfall_timed_samples", ctypes.c_int64),
         ("timed_blocks", ctypes.c_int64),
         ("pipeline_drains", ctypes.c_int64),
+        ("host_ms_build", ctypes.c_double),
+        ("host_ms_launch", ctypes.c_double),
+        ("host_ms_collect", ctypes.c_double),
     ]
 
 
@@ -133,6 +136,7 @@ PROTOTYPES = {
     "owrx_waterfall_create": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32, _pi32]),
     "owrx_waterfall_set": (_i32, [_vp, _i32, _i32, _i32, _i32]),
     "owrx_waterfall_set_batch": (_i32, [_vp, _i32, _i32, _i64]),
+    "owrx_set_input_retention": (_i32, [_vp, _i32]),
     "owrx_waterfall_destroy": (_i32, [_vp, _i32]),
     "owrx_waterfall_row_bytes": (_i64, [_vp, _i32]),
     "owrx_waterfall_read": (_i64, [_vp, _i32, _vp, _i64]),

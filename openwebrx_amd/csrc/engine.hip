@@ -99,7 +99,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
                          const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
                          hipEvent_t mac0, hipEvent_t mac1);
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
-                                hipStream_t st);
+                                const StepTable& steps, hipStream_t st);
 hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const int* idx,
                             int nlong, int64_t max_fd, int max_taps, hipStream_t st);
 hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const int* sel,
@@ -121,7 +121,11 @@ constexpr int kBlMaxTaps = 4095;       // longest bandpass of the bp_long path (
 constexpr int kSelPad = 64 * 4 * 6;    // serial lane lists: 64-lane padding per (output, NR, demod)
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
-constexpr int kSlots = 4;     // blocks of chain work in flight (streams A -> B -> C)
+#ifndef OWRX_SLOTS
+#define OWRX_SLOTS 8
+#endif
+constexpr int kSlots = OWRX_SLOTS;  // blocks of chain work in flight (streams A -> B -> C)
+constexpr int kInEv = 16;          // stream-A completion events kept (block index mod kInEv)
 constexpr int kRowSlots = 4;  // waterfall row blocks in flight (each on its own stream, R CUs)
 
 #define HIPCHK(expr)                                                                    \
@@ -215,8 +219,8 @@ struct Waterfall {
                              // four-step scratch (one cf32 frame per group)
     float* d_ones = nullptr; // DIF split: the sub-frames' window (the split applied the frame's)
     int partial_groups = 0;
-    WfGroup* h_groups[2] = {};  // pinned copy sources, per block parity
-    WfRow* h_rows[2] = {};
+    WfGroup* h_groups[kSlots] = {};  // pinned copy sources, per slot of the launching block
+    WfRow* h_rows[kSlots] = {};
     float* d_carry[2] = {nullptr, nullptr};
     WfGroup* d_groups = nullptr;
     WfRow* d_rows = nullptr;
@@ -246,7 +250,8 @@ struct ChainGroup {
     float2* d_partial[kSlots] = {};  // DDC segment partials, per slot (A writes, B reads)
     size_t partial_elems = 0;
     int nseg = 1;
-    DdcChain* h_chains[2] = {};  // pinned copy sources, per block parity
+    DdcChain* h_chains[kSlots] = {};  // pinned copy sources, per slot
+    bool chains_stale = true;  // d_chains needs an upload (membership changed, or a retune)
     int h_cap = 0;
     // fast-convolution form (kernels_fcddc.hip): frame length M; 0: direct form only
     int fc_M = 0;
@@ -387,6 +392,7 @@ struct Slot {  // one block's outputs in flight on streams B / C
     // (NoiseFilter / secondary FFT) was carried; per block only nk / k_begin are patched
     uint64_t post_epoch = ~0ull;
     bool post_dirty = true;
+    bool dev_stale = true;  // h_posts / h_sel rebuilt since the slot's device copy was made
     std::vector<const ChainGroup*> post_groups;
     std::vector<int> group_post0;  // first post of each group of post_groups
     int np = 0, nlong = 0, long_taps = 0, nfill = 0;
@@ -556,9 +562,11 @@ struct owrx_engine {
     float* h_in = nullptr;  // pinned staging for push_iq, two blocks (per block parity)
     int16_t* d_cs16 = nullptr;  // device staging of cs16 ingest (allocated on first use)
     // end of a block's stream-A work (its input and parity-indexed host descriptors reusable),
-    // per block parity; in_pending: the event of the last block is recorded and not waited for
-    hipEvent_t evIn[2] = {nullptr, nullptr};
-    bool in_pending = false;
+    // (evIn[k % kInEv] for block k); in_done: the newest block known to have finished it;
+    // retention: blocks the caller keeps each input valid for (owrx_set_input_retention)
+    hipEvent_t evIn[kInEv] = {};
+    int64_t in_done = -1;
+    int retention = 1;
     std::map<int, std::unique_ptr<Waterfall>> wfs;
     // hashed: the per-block loops and the batched reads look every chain up (a tree of 65 536
     // chains costs ~16 cache misses per lookup)
@@ -696,7 +704,7 @@ static void free_wf(Waterfall* w) {
     dfree(w->d_carry[1]);
     dfree(w->d_groups);
     dfree(w->d_rows);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kSlots; ++b) {
         hfree(w->h_groups[b]);
         hfree(w->h_rows[b]);
     }
@@ -861,6 +869,7 @@ static int drain_slots(owrx_engine* e, bool block, int keep) {
 static int drain_all(owrx_engine* e) {
     e->stats.pipeline_drains++;
     HIPCHK(hipStreamSynchronize(e->sA));
+    e->in_done = e->block_index - 1;
     RCCHK(drain_rows(e, true, 0));
     return drain_slots(e, true, 0);
 }
@@ -881,7 +890,7 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
         if (w->N > kWfLdsMaxN)
             HIPCHK(dalloc(&w->d_y4, (size_t)groups * w->N * (wf_uses_split(w->logn) ? kWfSplitMaxFpg : 1)));
         HIPCHK(dalloc(&w->d_groups, (size_t)groups));
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < kSlots; ++b) {
             hfree(w->h_groups[b]);
             HIPCHK(halloc(&w->h_groups[b], (size_t)groups));
         }
@@ -890,7 +899,7 @@ static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
     if (rows > w->rows_cap) {
         dfree(w->d_rows);
         HIPCHK(dalloc(&w->d_rows, (size_t)rows + 1));
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < kSlots; ++b) {
             hfree(w->h_rows[b]);
             HIPCHK(halloc(&w->h_rows[b], (size_t)rows + 1));
         }
@@ -957,12 +966,10 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     if (n > g->chains_cap) {
         RCCHK(drain_all(e));
         dfree(g->d_chains);
-        hfree(g->h_chains[0]);
-        hfree(g->h_chains[1]);
+        for (auto& h : g->h_chains) hfree(h);
         g->chains_cap = std::max(n, 2 * g->chains_cap);
         HIPCHK(dalloc(&g->d_chains, (size_t)g->chains_cap));
-        HIPCHK(halloc(&g->h_chains[0], (size_t)g->chains_cap));
-        HIPCHK(halloc(&g->h_chains[1], (size_t)g->chains_cap));
+        for (auto& h : g->h_chains) HIPCHK(halloc(&h, (size_t)g->chains_cap));
     }
     const int64_t nk_max = e->max_block / g->D + 4;
     // Launch shape: each tile group's D phases are split into nseg segments, one 4-wave
@@ -1169,7 +1176,9 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     for (const WfGroup& g : w->groups) nfr += g.nframes;
     e->stats.waterfall_frames += nfr;
     e->stats.waterfall_samples += nfr * w->hop;
-    const int bp = (int)(e->block_index & 1);
+    // the launching block's slot (its previous user, block k - kSlots, has drained; at
+    // owrx_sync every slot has)
+    const int bp = (int)(e->block_index % kSlots);
     memcpy(w->h_groups[bp], w->groups.data(), sizeof(WfGroup) * w->groups.size());
     memcpy(w->h_rows[bp], w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size());
     HIPCHK(kcopy(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(), e->sA));
@@ -1275,7 +1284,9 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
     bool one_shot = false;
     int64_t out_off = 0;
     int np = 0;
-    for (const GroupWork& gw : e->work) {
+    const bool use_steps = e->work.size() <= (size_t)kMaxStepGroups;
+    for (size_t gi = 0; gi < e->work.size(); ++gi) {
+        const GroupWork& gw = e->work[gi];
         const ChainGroup* g = gw.g;
         S.post_groups.push_back(g);
         S.group_post0.push_back(np);
@@ -1285,6 +1296,7 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
             memset(&p, 0, sizeof(p));
             const owrx_chain_params& q = c->prm;
             p.demod = q.demod;
+            p.step_idx = use_steps ? (int)gi : -1;  // nk / k_begin / nseg: post_parallel's table
             p.afc_update = q.afc_update;
             p.afc_sample = q.afc_sample;
             p.output = q.output;
@@ -1447,36 +1459,47 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
             S.h_sel[S.afc_off + S.nafc++] = i;
     S.post_epoch = e->chain_epoch;
     S.post_dirty = one_shot;
+    S.dev_stale = true;
+    return OWRX_OK;
+}
+
+// Wait until block j's stream-A work (which read its input and its staged descriptors) is done.
+static int wait_input_block(owrx_engine* e, int64_t j) {
+    if (j <= e->in_done || j < 0) return OWRX_OK;
+    HIPCHK(hipEventSynchronize(e->evIn[j % kInEv]));
+    e->in_done = j;
     return OWRX_OK;
 }
 
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const double t_enter = now_ms();
-    // Block k's host descriptors and push staging are indexed by block parity, so they need
-    // block k - 2's stream-A work done: the previous call waited for it before returning.  The
-    // wait for block k - 1 (whose input the caller may reuse once this call returns: the
-    // owrx_process_device contract) comes at the end, after block k is built and enqueued, so
-    // stream A runs block k - 1 while the host builds block k.  That order is the A/B option
-    // default since round 3 (+1-2 % at C3 in round 2); OWRX_IN_WAIT=start waits before the
+    // Block k's pinned descriptors are staged per slot (reused by block k + kSlots, after the
+    // slot drained and block k's stream-A work is known done).  The caller's input: blocks
+    // k - retention + 1 .. k may still be read on stream A when this call returns, block
+    // k - retention is done (owrx_set_input_retention; 1 = the owrx_process_device contract:
+    // the caller may reuse block k - 1's buffer).  The wait comes at the end, after block k is enqueued, so stream A
+    // runs earlier blocks while the host builds block k; OWRX_IN_WAIT=start waits before the
     // build (the round-1/2 order, A/B).
     static const bool wait_first = [] {
         const char* v = getenv("OWRX_IN_WAIT");
         return v && strcmp(v, "start") == 0;
     }();
-    if (wait_first && e->in_pending) {
-        HIPCHK(hipEventSynchronize(e->evIn[(e->block_index + 1) & 1]));
-        e->stats.host_ms_wait_input += now_ms() - t_enter;
-        e->in_pending = false;
+    if (wait_first) {
+        const double t = now_ms();
+        RCCHK(wait_input_block(e, e->block_index - e->retention));
+        e->stats.host_ms_wait_input += now_ms() - t;
     }
-    const int bp = (int)(e->block_index & 1);
+    const int bp = (int)(e->block_index % kSlots);
     const int64_t blk_start = e->pos;
     const int64_t blk_end = e->pos + n;
     const int si = (int)(e->block_index % kSlots);
     Slot& S = e->slots[si];
     // the slot's previous block (k - kSlots) must be drained before its buffers are reused
+    // (and its stream-A work done: a block without chain outputs drains without a wait)
     {
         const double t = now_ms();
         RCCHK(drain_slots(e, true, kSlots - 1));
+        RCCHK(wait_input_block(e, e->block_index - kSlots));
         e->stats.host_ms_wait_slots += now_ms() - t;
     }
     const bool timed = e->timing > 0 && e->block_index % e->timing == 0;
@@ -1490,6 +1513,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     e->last_start = blk_start;
     e->last_end = blk_end;
     // ---- chains: DDC per group (A); post_parallel + post_serial_front (B); ADPCM + copies (C)
+    const double t_build = now_ms();
     std::vector<GroupWork>& work = e->work;
     work.clear();
     for (auto& gp : e->groups) {  // descriptors first, so the DDC bracket holds only kernels
@@ -1499,6 +1523,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         const int64_t k_end = (blk_end - g->T) / g->D + 1;
         const int64_t nk64 = k_end - g->k_next;
         if (nk64 <= 0) continue;
+        bool stale = g->chains_stale;
         for (size_t i = 0; i < g->members.size(); ++i) {
             Chain* c = e->chains[g->members[i]].get();
             if (c->rate_pending) {  // retune at output boundary k_next (phase continuous)
@@ -1509,13 +1534,20 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 c->rate_fx = rate_to_fx(c->rate);
                 c->rate_pending = false;
                 RCCHK(fc_build_w(e, c, (int)i));
+                stale = true;
             }
-            DdcChain& d = g->h_chains[bp][i];
-            d.rate_fx = c->rate_fx;
-            d.wD = rate_rotator(c->rate, g->D);
-            d.n0 = c->n0;
-            d.P0 = c->P0;
         }
+        if (stale) {  // the group's DDC descriptors change only with its membership or a retune
+            for (size_t i = 0; i < g->members.size(); ++i) {
+                const Chain* c = e->chains[g->members[i]].get();
+                DdcChain& d = g->h_chains[bp][i];
+                d.rate_fx = c->rate_fx;
+                d.wD = rate_rotator(c->rate, g->D);
+                d.n0 = c->n0;
+                d.P0 = c->P0;
+            }
+        }
+        g->chains_stale = stale;  // consumed by this block's upload below
         work.push_back(GroupWork{g, k_end, (int)nk64,
                                  g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST});
     }
@@ -1524,17 +1556,28 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     bool same_groups = S.post_groups.size() == work.size();
     for (size_t gi = 0; same_groups && gi < work.size(); ++gi) same_groups = S.post_groups[gi] == work[gi].g;
     if (S.post_dirty || S.post_epoch != e->chain_epoch || !same_groups) RCCHK(build_posts(e, S, si));
+    // this block's group fields: post_parallel's StepTable argument (the slot's device posts are
+    // reused as they are), or, past kMaxStepGroups groups, patched into every post
+    StepTable steps;
+    const bool use_steps = work.size() <= (size_t)kMaxStepGroups;
     for (size_t gi = 0; gi < work.size(); ++gi) {
         const GroupWork& gw = work[gi];
-        ChainPost* p = S.h_posts + S.group_post0[gi];
         const int nseg = gw.fast ? 1 : gw.g->nseg;
+        if (use_steps) {
+            steps.g[gi] = GroupStep{gw.g->k_next, gw.nk, nseg};
+            continue;
+        }
+        ChainPost* p = S.h_posts + S.group_post0[gi];
         for (size_t i = 0; i < gw.g->members.size(); ++i) {
             p[i].nk = gw.nk;
             p[i].k_begin = gw.g->k_next;
             p[i].nseg = nseg;
         }
+        S.dev_stale = true;
     }
     const int np = S.np;
+    const double t_launch = now_ms();
+    e->stats.host_ms_build += t_launch - t_build;
     // every descriptor of the block in one upload: the groups' DDC descriptors, the posts, the
     // serial lane lists and the long-bandpass list (stream B / C read them after event evA)
     {
@@ -1554,11 +1597,16 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 nj = 0;
                 maxb = 0;
             }
-            job(gw.g->d_chains, gw.g->h_chains[bp], (int64_t)sizeof(DdcChain) * (int64_t)gw.g->members.size());
+            if (gw.g->chains_stale)
+                job(gw.g->d_chains, gw.g->h_chains[bp], (int64_t)sizeof(DdcChain) * (int64_t)gw.g->members.size());
+            gw.g->chains_stale = false;
         }
-        job(S.d_posts, S.h_posts, (int64_t)sizeof(ChainPost) * np);
-        job(S.d_sel, S.h_sel, (int64_t)sizeof(int) * S.nfill);
-        job(S.d_sel + S.long_off, S.h_sel + S.long_off, (int64_t)sizeof(int) * (S.nlong + S.nafc));
+        if (S.dev_stale) {  // the slot's device posts and lane lists, when rebuilt
+            job(S.d_posts, S.h_posts, (int64_t)sizeof(ChainPost) * np);
+            job(S.d_sel, S.h_sel, (int64_t)sizeof(int) * S.nfill);
+            job(S.d_sel + S.long_off, S.h_sel + S.long_off, (int64_t)sizeof(int) * (S.nlong + S.nafc));
+            S.dev_stale = false;
+        }
         if (nj > 0) {
             hipLaunchKernelGGL(copy_jobs, dim3((unsigned)std::min<int64_t>(64, (maxb + 4095) / 4096), nj),
                                dim3(256), 0, e->sA, S.h_jobs);
@@ -1603,7 +1651,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     if (np > 0) {
         // stream A: post_parallel (wide); stream B: post_serial_front (serial, own CUs)
         if (timed) HIPCHK(hipEventRecord(S.b0, e->sA));
-        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, e->sA));
+        HIPCHK(launch_post_parallel(S.d_posts, np, S.d_counts, steps, e->sA));
         if (S.nlong > 0)  // long bandpass chains: bp_long + post_tail (after post_parallel)
             HIPCHK(launch_post_long(S.d_posts, S.d_counts, S.d_sel + S.long_off, S.nlong, S.long_fd,
                                     S.long_taps, e->sA));
@@ -1669,21 +1717,24 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         HIPCHK(hipEventRecord(S.a3, e->sA));
         S.timed = true;
     }
-    HIPCHK(hipEventRecord(e->evIn[bp], e->sA));
-    if (!wait_first && e->in_pending) {  // block k - 1 (see the top)
+    HIPCHK(hipEventRecord(e->evIn[e->block_index % kInEv], e->sA));
+    e->stats.host_ms_launch += now_ms() - t_launch;
+    if (!wait_first) {  // the oldest input the caller may reuse now (see the top)
         const double t = now_ms();
-        HIPCHK(hipEventSynchronize(e->evIn[bp ^ 1]));
+        RCCHK(wait_input_block(e, e->block_index - e->retention));
         e->stats.host_ms_wait_input += now_ms() - t;
     }
-    e->in_pending = true;
     e->pos = blk_end;
     e->stats.samples_in += n;
     e->stats.host_ms_process += now_ms() - t_enter;
     e->stats.blocks++;
     e->block_index++;
     // collect whatever earlier blocks have finished (B / C / R work overlaps later blocks)
+    const double t_collect = now_ms();
     RCCHK(drain_slots(e, false, 0));
-    return drain_rows(e, false, 0);
+    RCCHK(drain_rows(e, false, 0));
+    e->stats.host_ms_collect += now_ms() - t_collect;
+    return OWRX_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1864,8 +1915,7 @@ int owrx_engine_destroy(owrx_engine* e) {
         prel(e, g->d_fc_w);
         dfree(g->d_chains);
         for (int i = 0; i < kSlots; ++i) dfree(g->d_partial[i]);
-        hfree(g->h_chains[0]);
-        hfree(g->h_chains[1]);
+        for (auto& h : g->h_chains) hfree(h);
     }
     for (auto& kv : e->pool_size) hipFree(kv.first);  // the pool's buffers, in use or not
     hfree(e->h_up);
@@ -1893,6 +1943,16 @@ int owrx_engine_destroy(owrx_engine* e) {
 }
 
 int64_t owrx_engine_history(owrx_engine* e) { return e ? e->history : OWRX_EINVAL; }
+
+int owrx_set_input_retention(owrx_engine* e, int blocks) {
+    ENGINE_GUARD(e);
+    if (blocks < 1 || blocks >= kInEv) {
+        set_last_error("owrx_set_input_retention: blocks must be in [1, %d]", kInEv - 1);
+        return OWRX_EINVAL;
+    }
+    e->retention = blocks;
+    return OWRX_OK;
+}
 int64_t owrx_engine_max_block(owrx_engine* e) { return e ? e->max_block : OWRX_EINVAL; }
 
 int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t n) {
@@ -1946,8 +2006,9 @@ int owrx_push_iq(owrx_engine* e, const float* iq, int64_t n) {
     int64_t done = 0;
     while (done < n) {
         const int64_t m = std::min(n - done, e->max_block);
-        // staging half (block parity) last used two blocks ago: its copy finished before that
-        // block's stream-A work, which process_block waited for at the start of the last block
+        // staging half (block parity) last used two blocks ago: its copy ran before that
+        // block's stream-A work
+        RC_FAIL(e, wait_input_block(e, e->block_index - 2));
         float* hb = e->h_in + 2 * (e->block_index & 1) * e->max_block;
         memcpy(hb, iq + 2 * done, sizeof(float2) * m);
         bool wrapped = false;
@@ -1979,6 +2040,7 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq, int64_t n, float gain) 
     while (done < n) {
         const int64_t m = std::min(n - done, e->max_block);
         // same staging discipline as owrx_push_iq (half the bytes per sample)
+        RC_FAIL(e, wait_input_block(e, e->block_index - 2));
         int16_t* hb = reinterpret_cast<int16_t*>(e->h_in + 2 * (e->block_index & 1) * e->max_block);
         memcpy(hb, iq + 2 * done, 4 * (size_t)m);
         bool wrapped = false;
@@ -2008,7 +2070,9 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq, int64_t n, float gain) 
 int owrx_sync(owrx_engine* e) {
     ENGINE_GUARD(e);
     // batched waterfalls: launch what is pending on the newest block's window (still valid:
-    // owrx_process_device's contract, or the ring)
+    // owrx_process_device's contract, or the ring); every slot drained first (the flush stages
+    // its descriptors in the next block's slot)
+    RC_FAIL(e, drain_all(e));
     if (e->last_blk) RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr));
     RC_FAIL(e, drain_all(e));
     return OWRX_OK;
@@ -2366,6 +2430,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     }
     const int h = e->next_handle++;
     g->members.push_back(h);
+    g->chains_stale = true;
     e->need_out += c->staging_bytes();
     e->need_sm = std::max<int64_t>(e->need_sm, c->sm_cap);
     // squelch / demod debug taps hold up to cap + sq_length samples per step
@@ -2399,6 +2464,7 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     }
     g->members[slot] = g->members[last];
     g->members.pop_back();
+    g->chains_stale = true;
     e->need_out -= it->second->staging_bytes();
     free_chain(e, it->second.get());
     e->chains.erase(it);

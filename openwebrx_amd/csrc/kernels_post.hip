@@ -133,8 +133,14 @@ OWRX_DEV int wfm_audio(const ChainPost& P, ChainStateP& S, int nsq) {
 // 3125-tap complex FIR at 250 kHz) stops after section 1; bp_long then filters it across many
 // workgroups and PHASE 2 (post_tail) runs sections 3-4.
 template <int PHASE>
-OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
-    const ChainPost P = Pin;
+OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable* steps = nullptr) {
+    ChainPost P = Pin;
+    if (PHASE == 0 && P.step_idx >= 0) {  // this block's group fields (StepTable argument)
+        const GroupStep g = steps->g[P.step_idx];
+        P.k_begin = g.k_begin;
+        P.nk = g.nk;
+        P.nseg = g.nseg;
+    }
     const int tid = threadIdx.x;
     constexpr int NT = kPostThreads;
     const int H = P.bp_hist;  // fd_buf[0, H) = bandpass history
@@ -491,8 +497,8 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt) {
 }
 
 __global__ void __launch_bounds__(kPostThreads)
-post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts) {
-    post_body<0>(posts[blockIdx.x], counts[blockIdx.x]);
+post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts, StepTable steps) {
+    post_body<0>(posts[blockIdx.x], counts[blockIdx.x], &steps);
 }
 
 // sections 3-4 of the long-bandpass chains listed in idx (after bp_long)
@@ -1065,9 +1071,9 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
 }
 
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
-                                hipStream_t st) {
+                                const StepTable& steps, hipStream_t st) {
     if (nchains <= 0) return hipSuccess;
-    hipLaunchKernelGGL(post_parallel, dim3(nchains), dim3(kPostThreads), 0, st, posts, counts);
+    hipLaunchKernelGGL(post_parallel, dim3(nchains), dim3(kPostThreads), 0, st, posts, counts, steps);
     return hipGetLastError();
 }
 

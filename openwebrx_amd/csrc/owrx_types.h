@@ -71,6 +71,18 @@ struct NrState {
     int32_t frames;        // frames processed
 };
 
+// The per-block fields of a chain group's posts (post_parallel's argument): the slot's posts
+// stay on the device across blocks and only this table changes.
+struct GroupStep {
+    int64_t k_begin;
+    int32_t nk;
+    int32_t nseg;
+};
+constexpr int kMaxStepGroups = 32;
+struct StepTable {
+    GroupStep g[kMaxStepGroups];
+};
+
 // Static + per-step description of one chain, shared by post_parallel and post_serial.
 struct ChainPost {
     // configuration
@@ -116,7 +128,8 @@ struct ChainPost {
     int32_t nseg;
     int32_t group_chains;
     int32_t chain_in_group;
-    int32_t nk;            // group outputs this step
+    int32_t nk;            // group outputs this step (step_idx < 0; else StepTable)
+    int32_t step_idx;      // the chain's group in this block's StepTable, or -1
     int64_t k_begin;       // absolute output index of partial column 0
     int64_t k_first;       // absolute output index of this chain's output 0
     // outputs

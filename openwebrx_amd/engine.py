@@ -102,6 +102,11 @@ class Engine:
     def sync(self):
         check(lib.owrx_sync(self._h), "owrx_sync")
 
+    def set_input_retention(self, blocks):
+        """process_device callers whose blocks stay valid for `blocks` further calls (e.g. a
+        resident recording): the host may then run that many blocks ahead of the GPU."""
+        check(lib.owrx_set_input_retention(self._h, int(blocks)), "owrx_set_input_retention")
+
     def set_debug(self, on=True):
         check(lib.owrx_set_debug(self._h, 1 if on else 0), "owrx_set_debug")
 

@@ -239,6 +239,41 @@ def test_waterfall_batched_launches(amd):
     assert st2["waterfall_samples"] == st2["waterfall_frames"] * hop
 
 
+def test_input_retention_same_outputs(amd):
+    """owrx_set_input_retention: with a resident recording the host runs up to r blocks ahead of
+    stream A (no wait for block k - 1 before returning); audio, s-meter and waterfall rows are
+    byte-identical to the default contract (r = 1)."""
+    import torch
+    from openwebrx_amd import synth
+    fs, B = 2400000, 1 << 17
+    modes = ["nfm", "usb", "am", "cw"] * 3
+    iq, offs = synth.make_iq(fs, 12 * B, modes)
+    plist = [amd.params.chain_params(fs, o, m) for o, m in zip(offs, modes)]
+    N = 4096
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+
+    def run(r):
+        eng = amd.Engine(fs, max_block=B)
+        eng.set_input_retention(r)
+        wf = eng.waterfall(N, hop, avg, adpcm=True)
+        chains = [eng.chain(p) for p in plist]
+        h = eng.history
+        buf = torch.zeros(h + iq.size, dtype=torch.complex64, device="cuda")
+        buf[h:] = torch.from_numpy(iq).to("cuda")
+        torch.cuda.synchronize()
+        for k in range(12):
+            eng.process_device(buf.data_ptr() + 8 * (h + k * B), B)
+        eng.sync()
+        out = ([c.read_audio() for c in chains], [c.read_smeter().tobytes() for c in chains],
+               wf.read())
+        eng.close()
+        return out
+
+    a, b = run(1), run(8)
+    assert a[0] == b[0] and a[1] == b[1] and a[2] == b[2]
+    assert all(len(x) > 0 for x in a[0]) and len(a[2]) > 0
+
+
 def test_engine_ring_ingest_commit(amd):
     """The caller-written ring slot (owrx_ingest_buffer / owrx_commit, e.g. an RCCL broadcast)
     gives the same rows as owrx_push_iq through the ring's wraps."""
