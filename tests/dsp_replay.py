@@ -70,16 +70,18 @@ def _make(d):
     raise ValueError("replay: no builder for %s" % c)
 
 
-def build(step):
+def build(step, wide=None):
     """(wideband Buffer, modules by graph index, output Buffer by graph index, squelch power
     Buffer).  Modules that feed nothing in the recorded graph write into a Buffer of their own
-    (the client's audio / rows / secondary outputs)."""
+    (the client's audio / rows / secondary outputs).  `wide`: an existing wideband Buffer
+    (several clients on one source)."""
     from openwebrx_amd.pycsdr import modules as M
     from openwebrx_amd.pycsdr.types import Format
     g = step["graph"]
     # the test writes faster than real time: room for the whole stream (a lagging reader of a
     # full ring loses the oldest data, like the reference's Buffer)
-    wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 23)
+    if wide is None:
+        wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 23)
     mods = [None if d["class"] == "PythonReader" else _make(d) for _, d, _ in g]
     outs = {}
 

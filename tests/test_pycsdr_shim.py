@@ -187,6 +187,55 @@ def test_collector_stopped_after_draining_sees_every_byte():
     assert total.startswith(got) and len(got) < len(total)
 
 
+def test_tcp_source_feeds_the_wideband_buffer():
+    """SdrSource.getBuffer (owrx/source/__init__.py:307-314, 325-329): TcpSource(port,
+    COMPLEX_FLOAT) writes whatever the SDR's IQ socket delivers into the wideband Buffer.  A
+    local server sends cf32 in odd-sized pieces (TCP splits samples anywhere): every read of the
+    Buffer returns whole samples, and the bytes are the stream's, in order; stop() ends the pump
+    and closes the socket."""
+    import socket
+    rng = np.random.default_rng(3)
+    iq = (rng.standard_normal(50000) + 1j * rng.standard_normal(50000)).astype(np.complex64)
+    raw = iq.tobytes()
+    srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+    sizes = [1, 7, 13, 4099, 65537, 3]
+
+    def serve():
+        conn, _ = srv.accept()
+        i, k = 0, 0
+        while i < len(raw):
+            n = sizes[k % len(sizes)]
+            conn.sendall(raw[i:i + n])
+            i += n
+            k += 1
+        time.sleep(0.2)
+        conn.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    buf = M.Buffer(Format.COMPLEX_FLOAT)
+    r = buf.getReader()
+    src = M.TcpSource(port, Format.COMPLEX_FLOAT)
+    src.setWriter(buf)
+    got, t0 = [], time.time()
+    while sum(len(g) for g in got) < len(raw) and time.time() - t0 < 20:
+        d = r.read() if r.available() >= 8 else None
+        if d:
+            assert len(d) % 8 == 0
+            got.append(bytes(d))
+        else:
+            time.sleep(0.01)
+    assert b"".join(got) == raw
+    src.stop()
+    t.join(5)
+    srv.close()
+    src._worker.join(5)
+    assert not src._worker.is_alive()
+
+
 def test_format_mismatch_raises_valueerror():
     """setReader / setWriter raise ValueError (callers catch it, csdr/chain/__init__.py:60-84)."""
     with pytest.raises(ValueError):
