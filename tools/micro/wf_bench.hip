@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <map>
 
 using namespace owrx;
 
@@ -58,8 +59,80 @@ wf_mem_only(const float2* __restrict__ blk, const WfGroup* __restrict__ groups,
 
 constexpr int LOGN = 14, N = 1 << LOGN;
 
+__global__ void flush_read(const float4* __restrict__ p, size_t n, float* sink) {
+    float acc = 0.f;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float4 v = p[i];
+        acc += v.x + v.y + v.z + v.w;
+    }
+    if (acc == 12345.f) sink[0] = acc;  // never true for the zeroed buffer: keeps the reads
+}
+// the b2/l32 load pattern alone: 512 threads, 16-B per lane per m1, |x|^2 kept so the loads stay;
+// PF = 1 prefetches the next frame into registers
+template <int PF>
+__global__ void __launch_bounds__(512)
+wf_mem_b2(const float2* __restrict__ blk, const WfGroup* __restrict__ groups, float* __restrict__ partial) {
+    const WfGroup g = groups[blockIdx.x];
+    const int t = threadIdx.x;
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(blk + g.start), 0,
+                                                      (int)(8 * ((int64_t)(g.nframes - 1) * g.hop + 16384)), 0x00020000);
+    float acc[16] = {};
+    float4 nx[16];
+    auto ld = [&](int f, float4* v) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            v[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (t * 2 + f * g.hop) * 8, m * 8192, 0));
+    };
+    if (PF) ld(0, nx);
+    for (int f = 0; f < g.nframes; ++f) {
+        float4 x[16];
+        if (PF) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) x[m] = nx[m];
+            if (f + 1 < g.nframes) ld(f + 1, nx);
+        } else {
+            ld(f, x);
+        }
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            acc[m] = fmaf(x[m].x, x[m].x, fmaf(x[m].y, x[m].y, fmaf(x[m].z, x[m].z, fmaf(x[m].w, x[m].w, acc[m]))));
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) partial[(int64_t)blockIdx.x * 16384 + t + 512 * m] = acc[m];
+}
+// OWRX_WF_FLUSH=1: before every timed launch, write 512 MiB elsewhere so the frames come from HBM
+// (as in the engine, where the DDC's operand streams evict them) instead of the Infinity Cache
+static void* g_flush = nullptr;
+static bool flush_on() {
+    static const bool v = getenv("OWRX_WF_FLUSH") && atoi(getenv("OWRX_WF_FLUSH"));
+    return v;
+}
+template <typename F>
+static double time_us_flushed(F&& launch, int iters = 30) {
+    const size_t fb = (size_t)512 << 20;
+    if (!g_flush) CK(hipMalloc(&g_flush, fb));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    double tot = 0;
+    for (int i = 0; i < iters + 3; ++i) {
+        hipLaunchKernelGGL(flush_read, dim3(4096), dim3(256), 0, 0, (const float4*)g_flush, fb / 16,
+                           (float*)g_flush);
+        CK(hipEventRecord(e0, 0));
+        launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (i >= 3) tot += ms;
+    }
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return tot * 1e3 / iters;
+}
 template <typename F>
 static double time_us(F&& launch, int warm = 50, int iters = 200) {
+    if (flush_on()) return time_us_flushed(launch);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -100,6 +173,23 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dx, x.data(), sizeof(float2) * S, hipMemcpyHostToDevice));
     CK(hipMemcpy(dtw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice));
     CK(hipMemcpy(dwin, win.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    std::vector<float2> tw2(WfB2::kTw2);
+    for (int j = 0; j < 64; ++j)
+        for (int k = 0; k < 16; ++k)
+            tw2[16 * j + k] = float2{(float)cos(2 * M_PI * j * k / 1024), (float)-sin(2 * M_PI * j * k / 1024)};
+    float2* dtw2;
+    CK(hipMalloc(&dtw2, sizeof(float2) * tw2.size()));
+    CK(hipMemcpy(dtw2, tw2.data(), sizeof(float2) * tw2.size(), hipMemcpyHostToDevice));
+    CK(hipFuncSetAttribute((const void*)wf_fft_b2<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfB2::kLds));
+    CK(hipFuncSetAttribute((const void*)wf_fft_b2<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfB2::kLds));
+    CK(hipFuncSetAttribute((const void*)wf_fft_b2<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfB2::kLds));
+    CK(hipFuncSetAttribute((const void*)wf_fft_b2<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfB2::kLds));
+    CK(hipFuncSetAttribute((const void*)wf_fft_b2<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfB2::kLds));
     using KL = WfLean<LOGN>;
     using KR = WfR16<LOGN>;
     CK(hipFuncSetAttribute((const void*)wf_fft_lean<LOGN>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -163,6 +253,26 @@ int main(int argc, char** argv) {
                    hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, (int64_t)0, dg,
                                       dwin, dtw, dpart2, 0, 0);
                }));
+        report("b2", G, F, time_us([&] {
+                   hipLaunchKernelGGL((wf_fft_b2<0, 0>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                      dwin, dtw, dtw2, dpart2);
+               }));
+        report("b2pf", G, F, time_us([&] {
+                   hipLaunchKernelGGL((wf_fft_b2<1, 0>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                      dwin, dtw, dtw2, dpart2);
+               }));
+        report("b2pfnl", G, F, time_us([&] {
+                   hipLaunchKernelGGL((wf_fft_b2<1, 1>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                      dwin, dtw, dtw2, dpart2);
+               }));
+        report("b2nold", G, F, time_us([&] {
+                   hipLaunchKernelGGL((wf_fft_b2<0, 1>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                      dwin, dtw, dtw2, dpart2);
+               }));
+        report("b2nobar", G, F, time_us([&] {
+                   hipLaunchKernelGGL((wf_fft_b2<0, 2>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                      dwin, dtw, dtw2, dpart2);
+               }));
         const int nwg = frame_table(F);
         report("h32", G, F, time_us([&] {
                    hipLaunchKernelGGL(wf_fft_h32, dim3(nwg), dim3(WfH32::NT), WfH32::kLds, 0, dx, (int64_t)0, dfr,
@@ -170,6 +280,12 @@ int main(int argc, char** argv) {
                }));
         report("mem", G, F, time_us([&] {
                    hipLaunchKernelGGL(wf_mem_only<LOGN>, dim3(G), dim3(1024), 0, 0, dx, dg, dwin, dpart2);
+               }));
+        report("memb2", G, F, time_us([&] {
+                   hipLaunchKernelGGL(wf_mem_b2<0>, dim3(G), dim3(512), 0, 0, dx, dg, dpart2);
+               }));
+        report("mempf", G, F, time_us([&] {
+                   hipLaunchKernelGGL(wf_mem_b2<1>, dim3(G), dim3(512), 0, 0, dx, dg, dpart2);
                }));
         // parity of lean vs r16 on the same groups
         hipLaunchKernelGGL(wf_fft_r16<LOGN>, dim3(G), dim3(KR::NT), KR::kLds, 0, dx, (int64_t)0, dg, dwin, dtw,
@@ -201,6 +317,28 @@ int main(int argc, char** argv) {
             rms_d += d * d;
         }
         printf("       l32  vs r16: max rel %.3e, rel-RMS %.3e\n", worst, sqrt(rms_d / rms_a));
+        hipLaunchKernelGGL((wf_fft_b2<0, 0>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg, dwin, dtw,
+                           dtw2, dpart2);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(b.data(), dpart2, sizeof(float) * b.size(), hipMemcpyDeviceToHost));
+        worst = 0; rms_d = 0;
+        for (size_t i = 0; i < a.size(); ++i) {
+            const double d = fabs((double)a[i] - b[i]);
+            worst = std::max(worst, d / std::max((double)fabs(a[i]), 1e-30));
+            rms_d += d * d;
+        }
+        printf("       b2   vs r16: max rel %.3e, rel-RMS %.3e\n", worst, sqrt(rms_d / rms_a));
+        hipLaunchKernelGGL((wf_fft_b2<1, 0>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg, dwin, dtw,
+                           dtw2, dpart2);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(b.data(), dpart2, sizeof(float) * b.size(), hipMemcpyDeviceToHost));
+        worst = 0; rms_d = 0;
+        for (size_t i = 0; i < a.size(); ++i) {
+            const double d = fabs((double)a[i] - b[i]);
+            worst = std::max(worst, d / std::max((double)fabs(a[i]), 1e-30));
+            rms_d += d * d;
+        }
+        printf("       b2pf vs r16: max rel %.3e, rel-RMS %.3e\n", worst, sqrt(rms_d / rms_a));
         hipLaunchKernelGGL(wf_fft_h32, dim3(nwg), dim3(WfH32::NT), WfH32::kLds, 0, dx, (int64_t)0, dfr, dwin, dtw,
                            dmember, dtick, dpart2);
         CK(hipDeviceSynchronize());
@@ -221,6 +359,48 @@ int main(int argc, char** argv) {
             printf("       h32 rerun bit-identical: %s\n", memcmp(c2v.data(), b.data(), 4 * b.size()) ? "NO" : "yes");
         }
 #ifdef OWRX_WF_STAMPS
+        for (int abl = 0; abl < 2; ++abl) {
+            // b2 phase stamps of wave 0, frame 1: medians over workgroups
+            if (F < 2) break;
+            time_us([&] {
+                if (abl)
+                    hipLaunchKernelGGL((wf_fft_b2<0, 1>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                       dwin, dtw, dtw2, dpart2);
+                else
+                    hipLaunchKernelGGL((wf_fft_b2<0, 0>), dim3(G), dim3(WfB2::NT), WfB2::kLds, 0, dx, (int64_t)0, dg,
+                                       dwin, dtw, dtw2, dpart2);
+            });
+            std::vector<unsigned long long> st((size_t)1024 * 16);
+            CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wf_stamp), sizeof(unsigned long long) * st.size()));
+            auto med = [&](int a, int b) {
+                std::vector<long long> d;
+                for (int g = 0; g < std::min(G, 1024); ++g) d.push_back((long long)(st[g * 16 + b] - st[g * 16 + a]));
+                std::sort(d.begin(), d.end());
+                return d[d.size() / 2];
+            };
+            const double clk = (double)med(0, 13) / (double)med(14, 15) * 0.1;
+            {
+                // co-residency: the most workgroups alive at once on one CU (HW_ID: CU, SH, SE; XCC_ID)
+                std::map<unsigned long long, std::vector<std::pair<unsigned long long, int>>> ev;
+                for (int g = 0; g < std::min(G, 1024); ++g) {
+                    const unsigned long long id = st[g * 16 + 12];
+                    const unsigned lo = (unsigned)id, xcc = (unsigned)(id >> 32) & 15;
+                    const unsigned long long cu = ((unsigned long long)xcc << 16) | (lo & 0xff00) | ((lo >> 12) & 0xf) << 20;
+                    ev[cu].push_back({st[g * 16 + 0], +1});
+                    ev[cu].push_back({st[g * 16 + 13], -1});
+                }
+                int best = 0;
+                for (auto& kv : ev) {
+                    std::sort(kv.second.begin(), kv.second.end());
+                    int c = 0;
+                    for (auto& e : kv.second) best = std::max(best, c += e.second);
+                }
+                printf("       b2 CUs used %zu, max workgroups resident on one CU %d\n", ev.size(), best);
+            }
+            printf("       b2%s stamps (median cycles, wave 0): clock %.2f GHz, total %lld, frame0 %lld;"
+                   " frame 1: S1+X1 %lld S2+X2 %lld S3+X3 %lld S4 %lld\n",
+                   abl ? "nold" : "", clk, med(0, 13), med(0, 1), med(1, 2), med(2, 3), med(3, 4), med(4, 5));
+        }
         {
             // l32 phase stamps of wave 0: medians over workgroups
             time_us([&] {

@@ -843,4 +843,281 @@ wf_fft_rx(const float2* __restrict__ blk, int64_t blk_start,
     }
 }
 
+// ---- wf_fft_b2: N = 16384 at two workgroups per CU ------------------------------------------
+// The one-workgroup-per-CU kernels above run a frame's loads, DFTs and LDS exchanges one after
+// the other (the 128 KiB image fills the CU's LDS).  This one keeps the image to 66 KiB so two
+// workgroups share a CU and each one's exchanges run under the other's DFTs, and inside a
+// workgroup it splits every exchange into two rounds whose stores drain under the next stage's
+// arithmetic.
+//
+// n = 1024 m1 + 64 m2 + 4 m3 + 2 n1 + n0, decimation in frequency:
+//   S1: DFT16 over m1 -> k1, * W_16384^(k1 (n mod 1024))
+//   S2: DFT16 over m2 -> k2, * W_1024^(k2 (n mod 64))
+//   S3: DFT16 over m3 -> k3
+//   S4: * W_64^(k3 (2 n1 + n0)), DFT4 over (n1, n0) -> k4;   bin k = k1 + 16 k2 + 256 k3 + 4096 k4.
+// 512 threads hold 32 points each: two batches (n0 = 0, 1) of 16.  n0 stays a register index in
+// every stage, so each exchange moves one batch at a time through a 64 KiB image (66 KiB for the
+// padded X2 layout): W(b0) | R(b0) | W(b1) + the next stage on b0 | R(b1) + the next stage on b1.
+// Thread layouts (t = 64 wave + lane) and images, chosen so every access is one ds_*_b64 with a
+// compile-time offset and no bank conflict (16-lane store groups, 32-lane read groups):
+//   S1 thread t = n1 + 2 m3 + 32 m2 (n mod 1024 = 2 t + n0: one 16-B load per m1 takes both batches)
+//   X1 image [k1][m2][m3 n1] = t + 512 k1;   S2 thread (m3 n1) + 32 k1
+//   X2 image (m3 n1) + 33 k1 + 528 k2;       S3 lane k1 + 16 (k2 & 1) + 32 n1, wave k2 >> 1
+//   X3 image k1 + 16 (k2 & 1) + 32 n1 + 64 k3 + 1024 (k2 >> 1);
+//   S4 lane k1 + 16 (k2 & 3) (the partial row's 64 contiguous bins), wave (k2 >> 2) + 4 (k3 >> 3),
+//      so S4's twiddles are wave-uniform constants.
+struct WfB2 {
+    static constexpr int LOGN = 14, N = 1 << LOGN, NT = 512;
+    static constexpr int kImage = 528 * 16;  // X2's padded image, the largest of the three
+    static constexpr int kTw2 = 64 * 16;     // tw2[16 j + k] = W_1024^(j k)
+    // S2's twiddles stay in LDS behind the image for the whole group, [k][n0][t & 31]: one
+    // conflict-free ds_read_b64 each
+    static constexpr size_t kLds = sizeof(float2) * (kImage + kTw2);
+};
+
+// workgroup barrier with only the LDS counter drained (global loads stay in flight across it);
+// the memory clobber keeps every LDS access on its side
+OWRX_DEV void wf_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// a[k] *= W_16384^(k nr), k = 1..15, from the powers w1 = W^nr, w2 = W^(2 nr), w4, w8
+OWRX_DEV void b2_tw1(float2* a, float2 w1, float2 w2, float2 w4, float2 w8) {
+    // each power is used as soon as it exists (a[k] and a[k + 8]), so few stay live
+    a[8] = f2mul(a[8], w8);
+    a[1] = f2mul(a[1], w1);
+    a[9] = f2mul(a[9], f2mul(w1, w8));
+    a[2] = f2mul(a[2], w2);
+    a[10] = f2mul(a[10], f2mul(w2, w8));
+    const float2 w3 = f2mul(w1, w2);
+    a[3] = f2mul(a[3], w3);
+    a[11] = f2mul(a[11], f2mul(w3, w8));
+    a[4] = f2mul(a[4], w4);
+    a[12] = f2mul(a[12], f2mul(w4, w8));
+    const float2 w5 = f2mul(w1, w4);
+    a[5] = f2mul(a[5], w5);
+    a[13] = f2mul(a[13], f2mul(w5, w8));
+    const float2 w6 = f2mul(w2, w4);
+    a[6] = f2mul(a[6], w6);
+    a[14] = f2mul(a[14], f2mul(w6, w8));
+    const float2 w7 = f2mul(w3, w4);
+    a[7] = f2mul(a[7], w7);
+    a[15] = f2mul(a[15], f2mul(w7, w8));
+}
+
+#ifndef OWRX_B2_ABL
+#define OWRX_B2_ABL 0
+#endif
+// PF = 0: two workgroups per CU (128 VGPRs), each frame's samples loaded when it starts.
+// PF = 1: one workgroup per CU (256 VGPRs): the window stays in registers and the next frame's
+//         samples load while this one transforms.
+// ABL (tools/micro only): 1 = no frame loads, 2 = no barriers.
+template <int PF, int ABL = OWRX_B2_ABL>
+__global__ void __launch_bounds__(WfB2::NT) __attribute__((amdgpu_waves_per_eu(PF ? 2 : 4, PF ? 2 : 4)))
+wf_fft_b2(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+          const float* __restrict__ window, const float2* __restrict__ tw,
+          const float2* __restrict__ tw2, float* __restrict__ partial) {
+    using K = WfB2;
+    constexpr int N = K::N;
+    WF_RSTAMP(14);
+    WF_STAMP(0);
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    {
+        // S2's table into LDS: entry (2 k + n0) 32 + j of W_1024^((2 j + n0) k)
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = t + 512 * i, j = e & 31, kb = e >> 5;
+            sm[K::kImage + e] = tw2[16 * (2 * j + (kb & 1)) + (kb >> 1)];
+        }
+    }
+    // S1's exact powers W_N^(2 t 2^i), i < 4, for the whole group (batch 1 multiplies them by
+    // the constants W_N^(2^i))
+    float2 sb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sb[i] = tw[((int)threadIdx.x << (i + 1)) & (N - 1)];
+    const WfGroup g = groups[blockIdx.x];
+    const int64_t g0 = g.start - blk_start;
+    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
+    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
+        0x00020000);
+    const float2* __restrict__ win2 = reinterpret_cast<const float2*>(window);
+    auto load_x = [&](int f, float4* v) {
+        const int vo = ((int)threadIdx.x * 2 + f * hop) * 8;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (ABL == 1)
+                v[m] = make_float4(vo * 1e-9f + m, m - vo * 1e-9f, 0.5f * m, vo * 2e-9f);
+            else
+                v[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, m * 1024 * 8, 0));
+        }
+    };
+    float4 nx[PF ? 16 : 1];
+    float2 wres[PF ? 16 : 1];
+    if constexpr (PF) {
+        load_x(0, nx);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) wres[m] = win2[threadIdx.x + 512 * m];
+    }
+    float acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.0f;
+    // S4's twiddles W_64^(k3 e), e = 1, 2, 3, k3 = kl + 8 (wave >> 2): wave-uniform, in SGPRs for
+    // the whole group
+    float2 t4[8][3];
+    {
+        const int k3h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+#pragma unroll
+        for (int kl = 0; kl < 8; ++kl)
+#pragma unroll
+            for (int e = 1; e < 4; ++e) t4[kl][e - 1] = tw[(256 * e * (kl + 8 * k3h)) & (N - 1)];
+    }
+#pragma unroll 1
+    for (int f = 0; f < nfr; ++f) {
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        // opaque per frame: otherwise the 30 twiddle products derived from them are hoisted out
+        // of the loop and held in registers (spills)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(sb[i].x), "+v"(sb[i].y));
+        const int lane = t & 63, wv = t >> 6;
+        // ---- S1: both batches' samples, 16 B per m1
+        float2 a0[16], a1[16];
+        if constexpr (PF) {
+            float4 xs[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) xs[m] = nx[m];
+            if (f + 1 < nfr) load_x(f + 1, nx);
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                a0[m] = make_float2(xs[m].x * wres[m].x, xs[m].y * wres[m].x);
+                a1[m] = make_float2(xs[m].z * wres[m].y, xs[m].w * wres[m].y);
+            }
+        } else {
+            float4 xs[16];
+            load_x(f, xs);
+            int wt = t;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float2 wp[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) wp[m] = win2[wt + 512 * (8 * h + m)];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const float4 x = xs[8 * h + m];
+                    a0[8 * h + m] = make_float2(x.x * wp[m].x, x.y * wp[m].x);
+                    a1[8 * h + m] = make_float2(x.z * wp[m].y, x.w * wp[m].y);
+                }
+                // the second half's taps load once the first half is applied (16 VGPRs, not 32)
+                asm volatile("" : "+v"(wt) : "v"(a1[8 * h + 7].x));
+            }
+        }
+        if (f == 1) WF_STAMP(1);
+        f2dft<16>(a0);
+        b2_tw1(a0, sb[0], sb[1], sb[2], sb[3]);
+        if (ABL != 2) wf_bar();  // the previous frame's last reads
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sm[t + 512 * k] = a0[k];
+        f2dft<16>(a1);
+        {
+            // W_N^(2^i) = exp(-2 pi i 2^i / 16384), i < 4
+            const float2 c1 = make_float2(0.99999992646571789f, -0.00038349518757139556f);
+            const float2 c2 = make_float2(0.99999970586288223f, -0.00076699031874270449f);
+            const float2 c4 = make_float2(0.99999882345170188f, -0.0015339801862847655f);
+            const float2 c8 = make_float2(0.99999529380957619f, -0.0030679567629659761f);
+            b2_tw1(a1, f2mul(sb[0], c1), f2mul(sb[1], c2), f2mul(sb[2], c4), f2mul(sb[3], c8));
+        }
+        if (ABL != 2) wf_bar();
+        if (f == 1) WF_STAMP(2);
+        // ---- S2 (thread (m3 n1) + 32 k1, j = n mod 64 = 2 (t & 31) + n0)
+        const int r1 = (t & 31) + 512 * (t >> 5);
+        const float2* T2 = sm + K::kImage + (t & 31);  // [k][n0][t & 31]
+        float2 c0[16], c1[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) c0[m] = sm[r1 + 32 * m];
+        if (ABL != 2) wf_bar();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sm[t + 512 * k] = a1[k];
+        f2dft<16>(c0);
+#pragma unroll
+        for (int k = 1; k < 16; ++k) c0[k] = f2mul(c0[k], T2[64 * k]);
+        if (ABL != 2) wf_bar();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) c1[m] = sm[r1 + 32 * m];
+        if (ABL != 2) wf_bar();
+        const int w2 = (t & 31) + 33 * (t >> 5);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sm[w2 + 528 * k] = c0[k];
+        f2dft<16>(c1);
+#pragma unroll
+        for (int k = 1; k < 16; ++k) c1[k] = f2mul(c1[k], T2[64 * k + 32]);
+        if (ABL != 2) wf_bar();
+        if (f == 1) WF_STAMP(3);
+        // ---- S3 (lane k1 + 16 (k2 & 1) + 32 n1, wave k2 >> 1)
+        const int r2 = (lane >> 5) + 33 * (lane & 15) + 528 * (((lane >> 4) & 1) + 2 * wv);
+        float2 d0[16], d1[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) d0[m] = sm[r2 + 2 * m];
+        if (ABL != 2) wf_bar();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sm[w2 + 528 * k] = c1[k];
+        f2dft<16>(d0);
+        if (ABL != 2) wf_bar();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) d1[m] = sm[r2 + 2 * m];
+        if (ABL != 2) wf_bar();
+        const int w3 = lane + 1024 * wv;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sm[w3 + 64 * k] = d0[k];
+        f2dft<16>(d1);
+        if (ABL != 2) wf_bar();
+        if (f == 1) WF_STAMP(4);
+        // ---- S4 (lane k1 + 16 (k2 & 3), wave (k2 >> 2) + 4 (k3 >> 3)): with e = 2 n1 + n0 and
+        // k4 = ka + 2 kb, X = sum_n0 W_2^(n0 kb) W_4^(n0 ka) y(ka, n0), y(ka, n0) = sum_n1 W_2^(n1 ka)
+        // u(n1, n0), u = W_64^(k3 e) v: batch 0's half of the DFT4 runs before batch 1 arrives.
+        // The twiddles are wave-uniform (k3 = kl + 8 (wave >> 2)): scalar loads of the table.
+        const int r3 = (lane & 31) + 1024 * (lane >> 5) + 2048 * (wv & 3) + 512 * (wv >> 2);
+        float2 y0[8][2];
+#pragma unroll
+        for (int kl = 0; kl < 8; ++kl) {
+            const float2 u0 = sm[r3 + 64 * kl];
+            const float2 u1 = f2mul(sm[r3 + 32 + 64 * kl], t4[kl][1]);
+            y0[kl][0] = f2add(u0, u1);
+            y0[kl][1] = f2sub(u0, u1);
+        }
+        if (ABL != 2) wf_bar();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sm[w3 + 64 * k] = d1[k];
+        if (ABL != 2) wf_bar();
+#pragma unroll
+        for (int kl = 0; kl < 8; ++kl) {
+            const float2 u0 = f2mul(sm[r3 + 64 * kl], t4[kl][0]);
+            const float2 u1 = f2mul(sm[r3 + 32 + 64 * kl], t4[kl][2]);
+            const float2 ya = f2add(u0, u1), yb = f2mi(f2sub(u0, u1));  // ka = 1: * W_4 = -i
+            const float2 x0 = f2add(y0[kl][0], ya), x2 = f2sub(y0[kl][0], ya);
+            const float2 x1 = f2add(y0[kl][1], yb), x3 = f2sub(y0[kl][1], yb);
+            acc[kl][0] = fmaf(x0.y, x0.y, fmaf(x0.x, x0.x, acc[kl][0]));
+            acc[kl][1] = fmaf(x1.y, x1.y, fmaf(x1.x, x1.x, acc[kl][1]));
+            acc[kl][2] = fmaf(x2.y, x2.y, fmaf(x2.x, x2.x, acc[kl][2]));
+            acc[kl][3] = fmaf(x3.y, x3.y, fmaf(x3.x, x3.x, acc[kl][3]));
+        }
+        if (f == 1) WF_STAMP(5);
+    }
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    float* out = partial + (int64_t)blockIdx.x * N + lane + 64 * (wv & 3) + 2048 * (wv >> 2);
+#pragma unroll
+    for (int kl = 0; kl < 8; ++kl)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) out[256 * kl + 4096 * k4] = acc[kl][k4];
+    WF_STAMP(13);
+    WF_RSTAMP(15);
+#ifdef OWRX_WF_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 1024)
+        g_wf_stamp[blockIdx.x][12] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) |
+                                     (unsigned)__builtin_amdgcn_s_getreg(63492);
+#endif
+}
+
 }  // namespace owrx
