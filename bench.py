@@ -8,9 +8,10 @@ Shift -> FirDecimate(833, 22223 taps) -> FractionalDecimator -> Bandpass -> Sque
 Agc -> Convert -> AdpcmEncoder(sync)).  `--config c2|c4|c5` runs the other BASELINE shapes per
 GPU (32 NFM/AM chains; 61.44 Msps with a 65536-bin waterfall and 128 chains; 64 USB chains with
 NoiseFilter).
-A step is one block of `--block` IQ samples (default 2^20) pushed through all of
-it, inputs resident in HBM, outputs (waterfall rows, ADPCM audio, s-meter) copied back to host
-rings and drained.  The waterfall FFT launches once per `--wf-batch` frames (owrx_waterfall_
+A step is `--blocks-per-step` (4) blocks of `--block` IQ samples (2^20, SURVEY.md 8d: the driver's
+20 steps stream 2^26.3 samples in 2^20-sample blocks) pushed through all of it, inputs resident
+in HBM, outputs (waterfall rows, ADPCM audio, s-meter) copied back to host rings and drained
+once per step.  The waterfall FFT launches once per `--wf-batch` frames (owrx_waterfall_
 set_batch; four per stream-A CU by default), not once per block.
 
 N>1 (torchrun, one rank per GPU): rank 0 owns the stream and broadcasts each block over RCCL
@@ -356,6 +357,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--blocks-per-step", type=int, default=4,
+                    help="blocks of --block samples per timed step (SURVEY.md 8d: throughput runs "
+                         "2^26 samples streamed in 2^20-sample blocks; the driver's 20 steps x 4 "
+                         "blocks = 2^26.3 samples, so the pipeline's end-of-run drain is not a "
+                         "fifth of the run)")
     ap.add_argument("--block", type=int, default=1 << 20,
                     help="IQ samples per step (SURVEY.md 8d: 2^20-sample blocks)")
     ap.add_argument("--wf-batch", type=int, default=-1,
@@ -447,9 +453,10 @@ def main():
     # one-off host stalls of ~7 ms (first launches / queue setup on the four streams; measured at
     # global blocks 2-9 on MI355X), so at least 12 untimed blocks precede the timed region
     # whatever W is (12 in all); reported as "priming_blocks"
-    prime = max(0, 12 - args.warmup)
+    bps = max(1, args.blocks_per_step)
+    prime = max(0, -(-(12 - args.warmup * bps) // bps))  # priming steps: >= 12 untimed blocks
     nsteps = prime + args.warmup + args.steps
-    total = nsteps * block
+    total = nsteps * bps * block
     stream = None
     if rank == 0:
         stream = gen_stream_torch(torch, dev, fs, hist + total, modes, offs)
@@ -477,22 +484,24 @@ def main():
         return n
 
     def _step(i):
-        if world == 1:
-            t0 = time.perf_counter()
-            eng.process_device(base + 8 * i * block, block)
-            dt_ = time.perf_counter() - t0
-            host_s["process"] += dt_
-            if i >= prime + args.warmup:
-                host_s["process_t"] += dt_
-        else:  # the one exchange step: rank 0's block to every rank over RCCL
-            t, off = bcast.step(i)
-            # wait for this broadcast only (an event behind it on torch's stream), not for the
-            # device: the engine's own streams keep blocks i-1 .. i-3 in flight meanwhile, and
-            # the next broadcast overlaps block i (its window was released by this call)
-            arrived = torch.cuda.Event()
-            arrived.record()
-            arrived.synchronize()
-            eng.process_device(t.data_ptr() + 8 * off, block)
+        for j in range(i * bps, (i + 1) * bps):
+            if world == 1:
+                t0 = time.perf_counter()
+                eng.process_device(base + 8 * j * block, block)
+                dt_ = time.perf_counter() - t0
+                host_s["process"] += dt_
+                if i >= prime + args.warmup:
+                    host_s["process_t"] += dt_
+            else:  # the one exchange step: rank 0's block to every rank over RCCL
+                t, off = bcast.step(j)
+                # wait for this broadcast only (an event behind it on torch's stream), not for
+                # the device: the engine's own streams keep blocks j-1 .. j-3 in flight
+                # meanwhile, and the next broadcast overlaps block j (its window was released by
+                # this call)
+                arrived = torch.cuda.Event()
+                arrived.record()
+                arrived.synchronize()
+                eng.process_device(t.data_ptr() + 8 * off, block)
         return drain()
 
     for i in range(prime + args.warmup):
@@ -532,7 +541,7 @@ def main():
     print("host seconds over all steps: process_device %.4f, step total %.4f, wall %.4f"
           % (host_s["process"], host_s["drain"], dt), file=sys.stderr)
     print("step marks (ms): " + " ".join("%.2f" % (1e3 * m) for m in marks), file=sys.stderr)
-    samples = args.steps * block
+    samples = args.steps * bps * block
     value = samples / dt / 1e6  # the one ingested stream, at any N (chains scale with N)
     ms_step = dt * 1e3 / args.steps
     # DDC work: the fast-convolution GEMM (fc_mac) is the dominant kernel of the chain path;
@@ -629,7 +638,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "priming_blocks": prime,
+            "priming_blocks": prime * bps,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
@@ -642,6 +651,8 @@ def main():
                             % (avg, hop, D, T, frac),
                 "samp_rate": fs, "fft_size": n_fft, "chains_per_gpu": C,
                 "block_samples": block,
+                "blocks_per_step": bps,
+                "step_samples": bps * block,
                 "parallelism": "1 GPU" if world == 1 else
                 "IQ broadcast over RCCL from rank 0, %d chains per rank" % C,
             },
@@ -713,14 +724,14 @@ def main():
             },
             "ddc": {
                 "form": "fast convolution" if fast else "direct",
-                "gpu_ms_per_step": round(ddc_ms / tsteps, 4),
+                "gpu_ms_per_block": round(ddc_ms / tsteps, 4),
                 "direct_form_equivalent_TFLOPs": round(direct_flops / (ddc_ms / 1e3) / 1e12, 2)
                 if ddc_ms > 0 else None,
                 "note": "the whole DDC (branch DFTs + GEMM + inverse DFTs and rotators) against the "
                         "flop count of the direct form it replaces (C outputs (4T + 6D), SURVEY "
                         "8d): what the same outputs would need at that rate",
             },
-            "kernels_ms_per_step": {
+            "kernels_ms_per_block": {
                 "ddc": round(ddc_ms / tsteps, 3),
                 "ddc_mac": round(mac_ms / tsteps, 3),
                 "waterfall_incl_descriptors": round(wf_ms / tsteps, 3),
@@ -728,13 +739,14 @@ def main():
                 "post_to_encoder_end": round(d["gpu_ms_serial"] / tsteps, 3),
                 "timed_blocks": d["timed_blocks"],
             },
-            "host_ms_per_step": {k[8:]: round(d[k] / args.steps, 3) for k in
+            "host_ms_per_block": {k[8:]: round(d[k] / (args.steps * bps), 3) for k in
                                  ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots",
                                   "host_ms_wait_rows", "host_ms_build", "host_ms_launch",
                                   "host_ms_collect")},
             "host_ms_per_step_python": {
                 "process_device": round(1e3 * host_s["process_t"] / args.steps, 3),
-                "step_total": round(1e3 * host_s["drain_t"] / args.steps, 3)},
+                "step_total": round(1e3 * host_s["drain_t"] / args.steps, 3),
+                "blocks_per_step": bps},
             "realtime": rt,
             "realtime_churn": churn,
             "max_realtime_chains": cap["max_realtime_chains"] if cap else None,

@@ -177,8 +177,10 @@ fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64
 // component s of that float4), the same permutation on both operands.  W of chain slot c at
 // W + c * w_cs + kappa * w_ks.
 constexpr int kFcKSplit = 4;
+// Three waves per SIMD (<= 168 registers): C3's 2^20-sample blocks launch M x 4 = 512
+// workgroups, one more round than stream A's 240 CUs hold at two (480)
 template <int FTT, int CTT, bool NT>
-__global__ void __launch_bounds__(64 * kFcKSplit)
+__global__ void __launch_bounds__(64 * kFcKSplit) __attribute__((amdgpu_waves_per_eu(3)))
 fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs, int64_t w_ks,
        int nchains, int Fs, int F, int Dp, int M, int ncg, int chain_fastest,
        float2* __restrict__ Y) {

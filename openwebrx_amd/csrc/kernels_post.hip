@@ -132,8 +132,35 @@ OWRX_DEV int wfm_audio(const ChainPost& P, ChainStateP& S, int nsq) {
 // PHASE 0 runs a chain whole, except that a chain with a long bandpass (bp_long: WFM's
 // 3125-tap complex FIR at 250 kHz) stops after section 1; bp_long then filters it across many
 // workgroups and PHASE 2 (post_tail) runs sections 3-4.
-template <int PHASE>
-OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable* steps = nullptr) {
+// The workgroup's LDS, declared by each kernel (post_body has two instantiations in post_parallel)
+struct PostLds {
+    ChainStateP S;
+    int n_fd;
+    float2 taps[kBpHist + 1];
+    float2 x[kBpLds];  // the bandpass window; with FUSED the chain-block's whole working set
+    float power[kMaxSqBlocks];
+    uint8_t pass[kMaxSqBlocks];
+};
+
+// FUSED (PHASE 0): the block's DDC outputs, FractionalDecimator output (the bandpass window) and
+// bandpass output stay in LDS -- stages 0-4 read and write the chain's global buffers only for
+// the carried histories and the demodulator output -- when its working set fits x[]
+// (post_fits): x[0, kBpHist + n_fd) = bandpass window, the DDC outputs (+ history) at the top
+// of x[] until the FractionalDecimator consumed them, then the squelch input (pending + this
+// block's) at the top.
+OWRX_DEV bool post_fits(const ChainPost& P, const StepTable* steps) {
+    if (P.bp_long || P.output == OWRX_OUT_IQ || P.bp_hist != kBpHist || P.bp_ntaps > kBpHist + 1)
+        return false;
+    const int64_t nk = P.step_idx >= 0 ? steps->g[P.step_idx].nk : P.nk;
+    const double r = P.frac_enabled ? P.frac_rate : 1.0;
+    if (!(r >= 0.5)) return false;
+    const int64_t nfd = (int64_t)((double)nk / r) + 2;
+    return kBpHist + nfd + kFdHist + nk <= kBpLds && kBpHist + nfd + P.sq_len + nfd <= kBpLds;
+}
+
+template <int PHASE, bool FUSED = false>
+OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
+                        const StepTable* steps = nullptr) {
     ChainPost P = Pin;
     if (PHASE == 0 && P.step_idx >= 0) {  // this block's group fields (StepTable argument)
         const GroupStep g = steps->g[P.step_idx];
@@ -145,17 +172,18 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
     constexpr int NT = kPostThreads;
     const int H = P.bp_hist;  // fd_buf[0, H) = bandpass history
 
-    __shared__ ChainStateP S;
-    __shared__ int sh_n_fd;
-    __shared__ float2 sh_taps[kBpHist + 1];
-    __shared__ float2 sh_x[kBpLds];
-    __shared__ float sh_power[kMaxSqBlocks];
-    __shared__ uint8_t sh_pass[kMaxSqBlocks];
+    static_assert(!FUSED || PHASE == 0, "fused: post_parallel only");
+    ChainStateP& S = Ls.S;
+    int& sh_n_fd = Ls.n_fd;
+    float2* const sh_taps = Ls.taps;
+    float2* const sh_x = Ls.x;
+    float* const sh_power = Ls.power;
+    uint8_t* const sh_pass = Ls.pass;
 
     const auto partial = gp(P.partial);
-    const auto ddc_buf = gp(P.ddc_buf);
+    const auto ddc_g = gp(P.ddc_buf);
     const auto fd_buf = gp(P.fd_buf);
-    const auto sq_buf = gp(P.sq_buf);
+    const auto sq_g = gp(P.sq_buf);
     const auto dem = gp(P.dem);
     const auto bp_taps = gp(P.bp_taps);
     const auto smeter = gp(P.smeter);
@@ -170,6 +198,17 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
     const int64_t nn = P.k_begin + P.nk - kb;
     n_new = nn > 0 ? (int)nn : 0;
     const int col0 = (int)(kb - P.k_begin);
+    // FUSED: the DDC outputs (with their kFdHist history) at the top of x[], the bandpass
+    // window's history at its bottom
+    float2* const ddc_l = sh_x + (kBpLds - kFdHist - (n_new > 0 ? n_new : 0));
+    const auto ddc_buf = [&]() {
+        if constexpr (FUSED) return ddc_l;
+        else return ddc_g;
+    }();
+    if constexpr (FUSED) {
+        if (tid < kFdHist) ddc_l[tid] = ddc_g[tid];
+        sh_x[tid] = fd_buf[tid];  // kBpHist == NT
+    }
     {   // segment partials: 8 independent loads in flight per thread, summed in segment order
         const int64_t sstride = (int64_t)P.group_chains * P.nk;
         const int nseg = P.nseg;
@@ -257,19 +296,23 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
                 acc.x = fmaf(L, xi.x, acc.x);
                 acc.y = fmaf(L, xi.y, acc.y);
             }
-            fd_buf[H + j] = acc;
+            if constexpr (FUSED) sh_x[kBpHist + j] = acc;
+            else fd_buf[H + j] = acc;
         }
     } else {
         if (tid == 0) sh_n_fd = n_new;
-        for (int j = tid; j < n_new; j += NT) fd_buf[H + j] = ddc_buf[kFdHist + j];
+        for (int j = tid; j < n_new; j += NT) {
+            if constexpr (FUSED) sh_x[kBpHist + j] = ddc_buf[kFdHist + j];
+            else fd_buf[H + j] = ddc_buf[kFdHist + j];
+        }
     }
     __syncthreads();
     n_fd = sh_n_fd;
     {   // keep the last kFdHist DDC outputs as interpolator history
         float2 t = make_float2(0.0f, 0.0f);
         if (tid < kFdHist) t = ddc_buf[n_new + tid];
-        __syncthreads();
-        if (tid < kFdHist) ddc_buf[tid] = t;
+        if constexpr (!FUSED) __syncthreads();
+        if (tid < kFdHist) ddc_g[tid] = t;
     }
     if (P.bp_long) {  // the bandpass and everything after it run in bp_long / post_tail
         if (tid == 0) {
@@ -307,13 +350,29 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
     const int pend = S.sq_pending;
     const int nbt = P.bp_ntaps;
     const bool lds_bp = !P.bp_long && nbt > 0 && (kBpHist + n_fd) <= kBpLds;
-    if (lds_bp) {
+    // FUSED: the squelch input (the pending samples, then this block's bandpass output) at the
+    // top of x[], where the DDC outputs were
+    float2* const sq_l = sh_x + (kBpLds - pend - n_fd);
+    const auto sq_buf = [&]() {
+        if constexpr (FUSED) return sq_l;
+        else return sq_g;
+    }();
+    if constexpr (FUSED) {
+        __syncthreads();  // every read of the DDC outputs (interpolator history) is done
+        for (int j = tid; j < pend; j += NT) sq_l[j] = sq_g[j];
+        for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
+        __syncthreads();
+    } else if (lds_bp) {
         for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[j] = fd_buf[j];
         for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
         __syncthreads();
     }
+    const auto fd_win = [&]() {
+        if constexpr (FUSED) return sh_x;
+        else return fd_buf;
+    }();
     for (int j = tid; j < (P.bp_long ? 0 : n_fd); j += NT) {
-        const auto x = fd_buf + kBpHist + j;
+        const auto x = fd_win + kBpHist + j;
         float2 y;
         if (lds_bp) {
             const float2* xs = sh_x + kBpHist + j;
@@ -362,7 +421,9 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
         }
     }
     __syncthreads();
-    if (P.bp_long) {  // keep the last H bandpass inputs
+    if constexpr (FUSED) {
+        fd_buf[tid] = sh_x[n_fd + tid];  // keep the last kBpHist bandpass inputs
+    } else if (P.bp_long) {  // keep the last H bandpass inputs
         move_front<float2>(fd_buf, n_fd, H);
     } else {  // keep the last kBpHist bandpass inputs
         const float2 t = fd_buf[n_fd + tid];  // kBpHist == NT
@@ -456,7 +517,9 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
         const int rem = total - nsq;
         float2 last = S.fm_last;
         if (nsq > 0) last = sh_pass[nb - 1] ? sq_buf[nsq - 1] : make_float2(0.0f, 0.0f);
-        if (P.sq_len > kMaxSqLen) {  // WFM: 15625-sample squelch blocks
+        if constexpr (FUSED) {
+            for (int i = tid; i < rem; i += NT) sq_g[i] = sq_buf[nsq + i];
+        } else if (P.sq_len > kMaxSqLen) {  // WFM: 15625-sample squelch blocks
             __syncthreads();
             move_front<float2>(sq_buf, nsq, rem);
         } else {
@@ -498,15 +561,21 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, const StepTable*
 
 __global__ void __launch_bounds__(kPostThreads)
 post_parallel(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts, StepTable steps) {
-    post_body<0>(posts[blockIdx.x], counts[blockIdx.x], &steps);
+    __shared__ PostLds Ls;
+    const ChainPost& P = posts[blockIdx.x];
+    if (post_fits(P, &steps))
+        post_body<0, true>(P, counts[blockIdx.x], Ls, &steps);
+    else
+        post_body<0, false>(P, counts[blockIdx.x], Ls, &steps);
 }
 
 // sections 3-4 of the long-bandpass chains listed in idx (after bp_long)
 __global__ void __launch_bounds__(kPostThreads)
 post_tail(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
           const int* __restrict__ idx) {
+    __shared__ PostLds Ls;
     const int i = idx[blockIdx.x];
-    post_body<2>(posts[i], counts[i]);
+    post_body<2>(posts[i], counts[i], Ls);
 }
 
 // Bandpass(transition=320/IF, use_fft=True) (csdr/chain/selector.py:115-117) for chains whose
