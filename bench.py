@@ -440,7 +440,10 @@ def main():
     if world == 1:
         # the stream is a resident recording: every block stays valid, so the host may run
         # ahead of stream A (owrx_set_input_retention); the N>1 windows alternate two buffers
-        eng.set_input_retention(int(os.environ.get("OWRX_BENCH_RETENTION", "4")))
+        eng.set_input_retention(int(os.environ.get("OWRX_BENCH_RETENTION", "8")))
+    # 16 blocks in flight for the headline engine (256 chains: a few MB of staging per block);
+    # the capacity ladder's engines keep the default 8 (their staging grows with the chains)
+    eng.set_pipeline_depth(int(os.environ.get("OWRX_BENCH_DEPTH", "16")))
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:

@@ -102,6 +102,12 @@ int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t nsamples);
  * engine waits only for block k - r + 1's stream-A work before returning from block k, so the
  * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 15. */
 int owrx_set_input_retention(owrx_engine* e, int blocks);
+/* Blocks of chain work in flight (streams A -> B -> C -> host rings), 1..16, default 8; only
+ * before the first chain and block.  Each one holds pinned and device staging for every chain
+ * (at 98 304 chains ~0.5 GB pinned per block), so deeper pipelines are for few-chain, high-rate
+ * engines.  No reference counterpart: csdr runs each module in its own thread with its own
+ * buffer (owrx/dsp.py:846-863 pumps); this is the engine's equivalent of that slack. */
+int owrx_set_pipeline_depth(owrx_engine* e, int blocks);
 /* Device window slot for the next block (write there, e.g. with ncclBroadcast), then commit. */
 int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity);
 int owrx_commit(owrx_engine* e, int64_t nsamples);

@@ -137,6 +137,7 @@ PROTOTYPES = {
     "owrx_waterfall_set": (_i32, [_vp, _i32, _i32, _i32, _i32]),
     "owrx_waterfall_set_batch": (_i32, [_vp, _i32, _i32, _i64]),
     "owrx_set_input_retention": (_i32, [_vp, _i32]),
+    "owrx_set_pipeline_depth": (_i32, [_vp, _i32]),
     "owrx_waterfall_destroy": (_i32, [_vp, _i32]),
     "owrx_waterfall_row_bytes": (_i64, [_vp, _i32]),
     "owrx_waterfall_read": (_i64, [_vp, _i32, _vp, _i64]),

@@ -122,9 +122,10 @@ constexpr int kSelPad = 64 * 4 * 6;    // serial lane lists: 64-lane padding per
 constexpr int64_t kDefaultHistory = 1 << 18;
 constexpr int kDebugStages = 6;
 #ifndef OWRX_SLOTS
-#define OWRX_SLOTS 8
+#define OWRX_SLOTS 16
 #endif
-constexpr int kSlots = OWRX_SLOTS;  // blocks of chain work in flight (streams A -> B -> C)
+constexpr int kSlots = OWRX_SLOTS;  // the most blocks of chain work in flight (A -> B -> C)
+constexpr int kDefaultSlots = 8;    // owrx_set_pipeline_depth: the engine's own (e->nslots)
 constexpr int kInEv = 16;          // stream-A completion events kept (block index mod kInEv)
 constexpr int kRowSlots = 4;  // waterfall row blocks in flight (each on its own stream, R CUs)
 
@@ -567,6 +568,9 @@ struct owrx_engine {
     hipEvent_t evIn[kInEv] = {};
     int64_t in_done = -1;
     int retention = 1;
+    // blocks of chain work in flight (owrx_set_pipeline_depth, <= kSlots): every slot holds
+    // pinned and device staging for all chains, so the depth is the caller's memory trade
+    int nslots = kDefaultSlots;
     std::map<int, std::unique_ptr<Waterfall>> wfs;
     // hashed: the per-block loops and the batched reads look every chain up (a tree of 65 536
     // chains costs ~16 cache misses per lookup)
@@ -848,7 +852,7 @@ static int drain_rows(owrx_engine* e, bool block, int keep) {
 // Drain finished chain slots in block order; with `block` wait until `keep` remain in flight.
 static int drain_slots(owrx_engine* e, bool block, int keep) {
     while (e->slot_tail < e->block_index) {
-        const int si = (int)(e->slot_tail % kSlots);
+        const int si = (int)(e->slot_tail % e->nslots);
         Slot& s = e->slots[si];
         const bool must = block && (e->block_index - e->slot_tail) > keep;
         if (!must) {
@@ -934,7 +938,7 @@ static int ensure_post_capacity(owrx_engine* e) {
     e->out_total = need_out + need_out / 2;  // headroom: adding a chain rarely reallocates
     e->sm_stride = need_sm;
     e->dbg_stride = e->debug ? (need_dbg + 255) & ~(int64_t)255 : 0;
-    for (int si = 0; si < kSlots; ++si) {
+    for (int si = 0; si < e->nslots; ++si) {
         Slot& s = e->slots[si];
         free_slot_staging(s);
         HIPCHK(dalloc(&s.d_posts, cap));
@@ -1178,7 +1182,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     e->stats.waterfall_samples += nfr * w->hop;
     // the launching block's slot (its previous user, block k - kSlots, has drained; at
     // owrx_sync every slot has)
-    const int bp = (int)(e->block_index % kSlots);
+    const int bp = (int)(e->block_index % e->nslots);
     memcpy(w->h_groups[bp], w->groups.data(), sizeof(WfGroup) * w->groups.size());
     memcpy(w->h_rows[bp], w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size());
     HIPCHK(kcopy(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(), e->sA));
@@ -1489,17 +1493,17 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         RCCHK(wait_input_block(e, e->block_index - e->retention));
         e->stats.host_ms_wait_input += now_ms() - t;
     }
-    const int bp = (int)(e->block_index % kSlots);
+    const int bp = (int)(e->block_index % e->nslots);
     const int64_t blk_start = e->pos;
     const int64_t blk_end = e->pos + n;
-    const int si = (int)(e->block_index % kSlots);
+    const int si = (int)(e->block_index % e->nslots);
     Slot& S = e->slots[si];
     // the slot's previous block (k - kSlots) must be drained before its buffers are reused
     // (and its stream-A work done: a block without chain outputs drains without a wait)
     {
         const double t = now_ms();
-        RCCHK(drain_slots(e, true, kSlots - 1));
-        RCCHK(wait_input_block(e, e->block_index - kSlots));
+        RCCHK(drain_slots(e, true, e->nslots - 1));
+        RCCHK(wait_input_block(e, e->block_index - e->nslots));
         e->stats.host_ms_wait_slots += now_ms() - t;
     }
     const bool timed = e->timing > 0 && e->block_index % e->timing == 0;
@@ -1778,8 +1782,10 @@ int owrx_device_count(void) {
 
 // Streams B, C and R run per-chain / per-row recurrences: a handful of waves whose speed is
 // their own instruction issue, which halves when DDC waves share their SIMDs.  They get
-// dedicated CUs (OWRX_SERIAL_CUS = "B,C,R" counts, default "4,4,4"; "0" = no masks) and
-// stream A (FFT, DDC, post_parallel) the rest of the chip.
+// dedicated CUs (OWRX_SERIAL_CUS = "B,C,R,W" counts, default "4,4,4,4"; "0" = no masks) and
+// stream A (FFT, DDC, post_parallel) the rest of the chip.  W: the waterfall row encoders'
+// own CUs -- sharing R's, a batch of row encoders (one ~120 KiB-LDS workgroup per row, more
+// rows than CUs) held the output gathers back by ~0.5 ms, and with them every slot's release.
 static hipError_t create_streams(owrx_engine* e) {
     int ncu = 0;
     hipError_t err = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device);
@@ -1791,12 +1797,14 @@ static hipError_t create_streams(owrx_engine* e) {
     // R (8 CUs) holds the output gathers and the waterfall row encoders: one stream per row
     // slot, so the rows of consecutive blocks (independent: FftAdpcm restarts every row)
     // encode concurrently instead of queueing behind each other
-    int nb = 4, nc = 4, nr = 8;
+    int nb = 4, nc = 4, nr = 4, nw = 4;
     if (const char* v = getenv("OWRX_SERIAL_CUS")) {
-        if (sscanf(v, "%d,%d,%d", &nb, &nc, &nr) != 3) nb = nc = nr = 0;
+        const int k = sscanf(v, "%d,%d,%d,%d", &nb, &nc, &nr, &nw);
+        if (k == 3) nw = 0;  // the row encoders share R's CUs (the round-2 layout)
+        else if (k != 4) nb = nc = nr = 0;
     }
     e->cus_a = ncu;
-    if (nb <= 0 || nc <= 0 || nr <= 0 || nb + nc + nr > ncu / 2) {
+    if (nb <= 0 || nc <= 0 || nr <= 0 || nw < 0 || nb + nc + nr + nw > ncu / 2) {
         for (hipStream_t* st : {&e->sA, &e->sB, &e->sC, &e->sR}) {
             err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
             if (err != hipSuccess) return err;
@@ -1813,12 +1821,13 @@ static hipError_t create_streams(owrx_engine* e) {
         for (int c = lo; c < hi; ++c) m[(size_t)c / 32] |= 1u << (c % 32);
         return m;
     };
-    const int a_end = ncu - nb - nc - nr;
+    const int a_end = ncu - nb - nc - nr - nw;
     e->cus_a = a_end;
     const std::vector<uint32_t> mA = mask_range(0, a_end);
     const std::vector<uint32_t> mB = mask_range(a_end, a_end + nb);
     const std::vector<uint32_t> mC = mask_range(a_end + nb, a_end + nb + nc);
-    const std::vector<uint32_t> mR = mask_range(a_end + nb + nc, ncu);
+    const std::vector<uint32_t> mR = mask_range(a_end + nb + nc, a_end + nb + nc + nr);
+    const std::vector<uint32_t> mW = nw > 0 ? mask_range(a_end + nb + nc + nr, ncu) : mR;
     const std::pair<hipStream_t*, const std::vector<uint32_t>*> sm[] = {
         {&e->sA, &mA}, {&e->sB, &mB}, {&e->sC, &mC}, {&e->sR, &mR}};
     for (auto& x : sm) {
@@ -1826,7 +1835,7 @@ static hipError_t create_streams(owrx_engine* e) {
         if (err != hipSuccess) return err;
     }
     for (auto& r : e->rslots) {
-        err = hipExtStreamCreateWithCUMask(&r.stream, (uint32_t)words, mR.data());
+        err = hipExtStreamCreateWithCUMask(&r.stream, (uint32_t)words, mW.data());
         if (err != hipSuccess) return err;
     }
     return hipSuccess;
@@ -1943,6 +1952,17 @@ int owrx_engine_destroy(owrx_engine* e) {
 }
 
 int64_t owrx_engine_history(owrx_engine* e) { return e ? e->history : OWRX_EINVAL; }
+
+int owrx_set_pipeline_depth(owrx_engine* e, int blocks) {
+    ENGINE_GUARD(e);
+    if (blocks < 1 || blocks > kSlots || e->block_index != 0 || !e->chains.empty()) {
+        set_last_error("owrx_set_pipeline_depth: blocks must be in [1, %d], before the first "
+                       "chain and block", kSlots);
+        return OWRX_EINVAL;
+    }
+    e->nslots = blocks;
+    return OWRX_OK;
+}
 
 int owrx_set_input_retention(owrx_engine* e, int blocks) {
     ENGINE_GUARD(e);
@@ -2411,9 +2431,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     // slack: the serial kernels read whole 64-sample chunks / 8-sample prefetches unguarded
     // (SAm: the Selector output, cf32, until chain_afc leaves the RealPart in place)
     const size_t dem_n = (p->demod == OWRX_DEMOD_SAM ? 2 : 1) * ((size_t)scap + 160);
-    for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_dem[i], dem_n));
+    for (int i = 0; i < e->nslots; ++i) HIPCHK(palloc(e, &c->d_dem[i], dem_n));
     // + kNrN: a NoiseFilter emits up to one frame more than its input per step
-    for (int i = 0; i < kSlots; ++i) HIPCHK(palloc(e, &c->d_s16[i], (size_t)scap + 160 + kNrN));
+    for (int i = 0; i < e->nslots; ++i) HIPCHK(palloc(e, &c->d_s16[i], (size_t)scap + 160 + kNrN));
     int rc = chain_set_bandpass_taps(e, c.get());
     if (!rc && p->nr_enabled && p->output != OWRX_OUT_IQ) rc = chain_nr_alloc(e, c.get());
     if (rc) {

@@ -107,6 +107,10 @@ class Engine:
         resident recording): the host may then run that many blocks ahead of the GPU."""
         check(lib.owrx_set_input_retention(self._h, int(blocks)), "owrx_set_input_retention")
 
+    def set_pipeline_depth(self, blocks):
+        """Blocks of chain work in flight (1..16, default 8), before the first chain and block."""
+        check(lib.owrx_set_pipeline_depth(self._h, int(blocks)), "owrx_set_pipeline_depth")
+
     def set_debug(self, on=True):
         check(lib.owrx_set_debug(self._h, 1 if on else 0), "owrx_set_debug")
 

@@ -112,6 +112,35 @@ def test_engine_cs16_ingest_equals_float_ingest(amd):
     assert outs[0] == outs[1]
 
 
+def test_pipeline_depth_outputs_identical(amd):
+    """owrx_set_pipeline_depth: 1, 8 (default) and 16 blocks in flight give byte-identical
+    waterfall rows, chain audio and s-meter values; the depth is refused once a chain exists."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    n = 1 << 20
+    iq, offs = synth.make_iq(fs, n, ["nfm", "usb", "am"], amp=0.02)
+    avg, hop = amd.params.fft_parameters(fs, 4096, 9, 0.3)
+    outs = []
+    for depth in (1, None, 16):
+        eng = amd.Engine(fs, max_block=1 << 16)
+        if depth is not None:
+            eng.set_pipeline_depth(depth)
+        wf = eng.waterfall(4096, hop, avg, adpcm=True)
+        chs = [eng.chain(amd.params.chain_params(fs, o, m))
+               for o, m in zip(offs, ["nfm", "usb", "am"])]
+        if depth == 16:
+            with pytest.raises(Exception):
+                eng.set_pipeline_depth(8)
+        for i in range(0, n, 1 << 16):
+            eng.push(iq[i:i + (1 << 16)])
+        eng.sync()
+        audio, _, sm, _ = eng.read_chains(chs)
+        outs.append((wf.read(), audio.tobytes(), np.asarray(sm).tobytes()))
+        eng.close()
+    assert len(outs[0][0]) > 0 and len(outs[0][1]) > 0
+    assert outs[0] == outs[1] == outs[2]
+
+
 def test_dcblock_deemph_bit_exact(amd):
     f = (RNG.standard_normal(25000) * 0.2 + 0.1).astype(np.float32)
     g = np.frombuffer(run_module(amd, amd._lib.MOD_DCBLOCK, f, 4 * f.size), np.float32)
