@@ -352,6 +352,47 @@ def pmc_traffic(prefix, config):
     return None, "kernel absent from " + os.path.relpath(files[-1], ROOT)
 
 
+def extra_block_run(Engine, fs, n_fft, hop, avg, wf_batch, plist, stream, total, xb, no_wf,
+                    warm=3, timed=8):
+    """The same workload on a fresh engine at `xb`-sample blocks (8 timed after 3 untimed),
+    from the same resident recording: the block granularity's effect on the rate."""
+    hist = (wf_batch + 16) * hop + 2 * n_fft + xb if wf_batch > 1 else 0
+    eng = Engine(fs, max_block=xb, history=hist)
+    eng.set_input_retention(8)
+    eng.set_pipeline_depth(16)
+    h = eng.history
+    if h + (warm + timed) * xb > stream.numel():
+        eng.close()
+        return None
+    wf = None
+    if not no_wf:
+        wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
+        if wf_batch > 1:
+            wf.set_batch(wf_batch)
+    chains = [eng.chain(p) for p in plist]
+    base = stream.data_ptr() + 8 * h
+
+    def one(i):
+        eng.process_device(base + 8 * i * xb, xb)
+        eng.read_chains(chains)
+        if wf is not None:
+            wf.read()
+    for i in range(warm):
+        one(i)
+    eng.sync()
+    t0 = time.perf_counter()
+    for i in range(warm, warm + timed):
+        one(i)
+    eng.sync()
+    dt = time.perf_counter() - t0
+    eng.close()
+    return {"block_samples": xb, "blocks": timed, "msps": round(timed * xb / dt / 1e6, 2),
+            "ms_per_block": round(dt * 1e3 / timed, 3),
+            "note": "a fresh engine (16 blocks in flight, retention 8) on the same recording, %d "
+                    "untimed then %d timed blocks, outputs drained per block, final sync inside "
+                    "the timed region" % (warm, timed)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -362,6 +403,9 @@ def main():
                          "2^26 samples streamed in 2^20-sample blocks; the driver's 20 steps x 4 "
                          "blocks = 2^26.3 samples, so the pipeline's end-of-run drain is not a "
                          "fifth of the run)")
+    ap.add_argument("--extra-block", type=int, default=1 << 22,
+                    help="a second, shorter run at this block size reported beside the headline "
+                         "(block_2p22: the round-2 headline granularity; 0 = skip)")
     ap.add_argument("--block", type=int, default=1 << 20,
                     help="IQ samples per step (SURVEY.md 8d: 2^20-sample blocks)")
     ap.add_argument("--wf-batch", type=int, default=-1,
@@ -534,8 +578,12 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    gc.enable()
     s1 = eng.stats()
+    xblock = None
+    if world == 1 and args.extra_block and args.extra_block != block:
+        xblock = extra_block_run(Engine, fs, n_fft, hop, avg, wf_batch, plist, stream, total,
+                                 args.extra_block, args.no_waterfall)
+    gc.enable()
     if dist:
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -750,6 +798,7 @@ def main():
                 "process_device": round(1e3 * host_s["process_t"] / args.steps, 3),
                 "step_total": round(1e3 * host_s["drain_t"] / args.steps, 3),
                 "blocks_per_step": bps},
+            "block_2p22": xblock,
             "realtime": rt,
             "realtime_churn": churn,
             "max_realtime_chains": cap["max_realtime_chains"] if cap else None,
