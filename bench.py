@@ -353,8 +353,8 @@ def pmc_traffic(prefix, config):
 
 
 def extra_block_run(Engine, fs, n_fft, hop, avg, wf_batch, plist, stream, total, xb, no_wf,
-                    warm=3, timed=8):
-    """The same workload on a fresh engine at `xb`-sample blocks (8 timed after 3 untimed),
+                    warm=3, timed=16):
+    """The same workload on a fresh engine at `xb`-sample blocks (16 timed after 3 untimed),
     from the same resident recording: the block granularity's effect on the rate."""
     hist = (wf_batch + 16) * hop + 2 * n_fft + xb if wf_batch > 1 else 0
     eng = Engine(fs, max_block=xb, history=hist)
