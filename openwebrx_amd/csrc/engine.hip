@@ -93,6 +93,8 @@ int ddc_blocks_per_cu(int P, int nchains);
 int fc_frame_supported(int m);  // kernels_fcddc.hip
 hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
                             uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st);
+hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int dst, hipStream_t st);
+int64_t fc_w_chain_offset(int c, int Dp);  // chain c's first entry in a bin's row of the tiled W
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
@@ -1053,16 +1055,17 @@ static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
     ChainGroup* g = c->group;
     if (!g->fc_M) return OWRX_OK;
     HIPCHK(launch_fc_make_w(g->fc_M, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P, c->rate_fx,
-                            g->d_fc_w + (int64_t)slot * g->fc_Dp, g->fc_w_ks(), e->sA));
+                            g->d_fc_w + fc_w_chain_offset(slot, g->fc_Dp), g->fc_w_ks(), e->sA));
     return OWRX_OK;
 }
 
-// Room for `slots` members' spectra: grows W[kappa][slot][Dp] by
-// doubling, moving the existing rows with one strided copy.
+// Room for `slots` members' spectra: grows W[kappa][slot tiles] (kernels_fcddc.hip: 8-chain
+// tiles, so capacities are multiples of 8 and a bin's first cap Dp entries hold its first cap
+// slots) by doubling, moving the existing rows with one strided copy.
 static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
     if (!g->fc_M || slots <= g->fc_w_cap) return OWRX_OK;
     const int M = g->fc_M;
-    const int cap = std::max(std::max(32, 2 * g->fc_w_cap), slots);
+    const int cap = (std::max(std::max(32, 2 * g->fc_w_cap), slots) + 7) & ~7;
     float2* nw = nullptr;
     // on stream A behind the blocks that read the old spectra (those release it when drained)
     HIPCHK(palloc(e, &nw, (size_t)M * cap * g->fc_Dp));
@@ -2474,14 +2477,8 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     // swap-remove: the last member takes the slot (and its filter spectra move with it)
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
     const int last = (int)g->members.size() - 1;
-    if (slot != last && g->fc_M) {
-        const int M = g->fc_M;
-        const size_t pitch = sizeof(float2) * (size_t)g->fc_w_ks();
-        HIPCHK(hipMemcpy2DAsync(g->d_fc_w + (int64_t)slot * g->fc_Dp, pitch,
-                                g->d_fc_w + (int64_t)last * g->fc_Dp, pitch,
-                                sizeof(float2) * (size_t)g->fc_Dp, (size_t)M,
-                                hipMemcpyDeviceToDevice, e->sA));
-    }
+    if (slot != last && g->fc_M)
+        HIPCHK(launch_fc_move_w(g->fc_M, g->d_fc_w, g->fc_w_ks(), g->fc_Dp, last, slot, e->sA));
     g->members[slot] = g->members[last];
     g->members.pop_back();
     g->chains_stale = true;

@@ -42,6 +42,17 @@ typedef __attribute__((address_space(1))) const fc_f4 gf4;  // global (not flat)
     } while (0)
 
 constexpr int kFcRT = 16;   // branches (r) per fc_fwd / fc_make_w workgroup
+// W's layout per bin kappa: [chain / 8][K-block of 8 branches][chain % 8][8 branches] (cf32):
+// fc_mac's load instruction for one 8-chain tile and K-block reads 512 contiguous bytes and the
+// K-blocks follow each other (its load pattern alone: 54 -> 48 us per C3 launch from HBM,
+// tools/micro/fc_floor.hip).  Element (kappa, chain c, branch r) at
+// kappa w_ks + fc_w_chain(c, Dp) + fc_w_branch(r).
+constexpr int kFcTile = 8;
+#define OWRX_DEV_HOST_INLINE __host__ __device__ __forceinline__
+OWRX_DEV_HOST_INLINE int64_t fc_w_chain(int c, int Dp) {
+    return (int64_t)(c / kFcTile) * kFcTile * Dp + (c % kFcTile) * 8;
+}
+OWRX_DEV_HOST_INLINE int64_t fc_w_branch(int r) { return (int64_t)(r >> 3) * kFcTile * 8 + (r & 7); }
 constexpr int kFcDpAlign = 96;  // Dp: a multiple of kFcRT and of 4 (K split) x 3 K-blocks of 8
 
 // Frame lengths: powers of two (64, 128, 256) and three times one (192, 384).  A row of
@@ -133,7 +144,8 @@ fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rat
             re += a.x * b.x - a.y * b.y;
             im += a.x * b.y + a.y * b.x;
         }
-        W[(int64_t)kap * w_ks + r0 + j] = make_float2((float)re, (float)im);  // zero for r >= D
+        const int r = r0 + j;  // tiled: the chain's K-block of 8 branches every 64 entries
+        W[(int64_t)kap * w_ks + (r >> 3) * kFcTile * 8 + (r & 7)] = make_float2((float)re, (float)im);  // zero for r >= D
     }
 }
 
@@ -230,7 +242,8 @@ fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs,
 #pragma unroll
     for (int t = 0; t < CTT; ++t) {
         const int c = cg * 8 * CTT + t * 8 + cc;
-        wp[t] = (const gf4*)(W + (c < nchains ? c : 0) * w_cs + (int64_t)kap * w_ks + 8 * kb0 + 2 * g);
+        wp[t] = (const gf4*)(W + (int64_t)kap * w_ks + fc_w_chain(c < nchains ? c : 0, (int)w_cs) +
+                             fc_w_branch(8 * kb0 + 2 * g));
     }
     fc_f4 acc[FTT][CTT];
 #pragma unroll
@@ -246,9 +259,9 @@ fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs,
 #pragma unroll
         for (int ft = 0; ft < FTT; ++ft) ua[ft] = up[ft][o];
 #pragma unroll
-        for (int t = 0; t < CTT; ++t) {
-            if constexpr (NT) wa[t] = __builtin_nontemporal_load(wp[t] + o);
-            else wa[t] = wp[t][o];
+        for (int t = 0; t < CTT; ++t) {  // tiled W: K-blocks kFcTile * 8 cf32 = 4 kFcTile float4 apart
+            if constexpr (NT) wa[t] = __builtin_nontemporal_load(wp[t] + o * kFcTile);
+            else wa[t] = wp[t][o * kFcTile];
         }
     };
     auto block = [&](const fc_f4* ua, const fc_f4* wa) {
@@ -328,6 +341,22 @@ fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs,
             if (fb + 1 < F) yc[(int64_t)(fb + 1) * M] = y1;
         }
 }
+
+// ---- a member's spectra to another slot of the tiled W (swap-remove on a chain's leave) ------
+// grid M (one bin each), block 256
+__global__ void __launch_bounds__(256)
+fc_move_w(float2* __restrict__ W, int64_t w_ks, int Dp, int src, int dst) {
+    float2* row = W + (int64_t)blockIdx.x * w_ks;
+    for (int r = threadIdx.x; r < Dp; r += 256)
+        row[fc_w_chain(dst, Dp) + fc_w_branch(r)] = row[fc_w_chain(src, Dp) + fc_w_branch(r)];
+}
+
+hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int dst, hipStream_t st) {
+    hipLaunchKernelGGL(fc_move_w, dim3(M), dim3(256), 0, st, W, w_ks, Dp, src, dst);
+    return hipGetLastError();
+}
+
+int64_t fc_w_chain_offset(int c, int Dp) { return fc_w_chain(c, Dp); }
 
 // ---- y_c[k0 + m] = rot_c(k0 + m) IDFT_M(Y_c[f])[m] into the group's output rows ------------
 // grid: ceil(nchains F / RW) workgroups of RW = 1024 / M rows; block 256.
