@@ -95,6 +95,7 @@ hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
                             uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st);
 hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int dst, hipStream_t st);
 int64_t fc_w_chain_offset(int c, int Dp);  // chain c's first entry in a bin's row of the tiled W
+int fc_w_tile();                           // chains per W tile: capacities are multiples of it
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
@@ -1059,13 +1060,14 @@ static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
     return OWRX_OK;
 }
 
-// Room for `slots` members' spectra: grows W[kappa][slot tiles] (kernels_fcddc.hip: 8-chain
-// tiles, so capacities are multiples of 8 and a bin's first cap Dp entries hold its first cap
-// slots) by doubling, moving the existing rows with one strided copy.
+// Room for `slots` members' spectra: grows W[kappa][slot tiles] (kernels_fcddc.hip: tiles of
+// fc_w_tile() chains, so capacities are multiples of it and a bin's first cap Dp entries hold its
+// first cap slots) by doubling, moving the existing rows with one strided copy.
 static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
     if (!g->fc_M || slots <= g->fc_w_cap) return OWRX_OK;
     const int M = g->fc_M;
-    const int cap = (std::max(std::max(32, 2 * g->fc_w_cap), slots) + 7) & ~7;
+    const int tile = fc_w_tile();
+    const int cap = (std::max(std::max(32, 2 * g->fc_w_cap), slots) + tile - 1) / tile * tile;
     float2* nw = nullptr;
     // on stream A behind the blocks that read the old spectra (those release it when drained)
     HIPCHK(palloc(e, &nw, (size_t)M * cap * g->fc_Dp));

@@ -42,12 +42,20 @@ typedef __attribute__((address_space(1))) const fc_f4 gf4;  // global (not flat)
     } while (0)
 
 constexpr int kFcRT = 16;   // branches (r) per fc_fwd / fc_make_w workgroup
-// W's layout per bin kappa: [chain / 8][K-block of 8 branches][chain % 8][8 branches] (cf32):
-// fc_mac's load instruction for one 8-chain tile and K-block reads 512 contiguous bytes and the
-// K-blocks follow each other (its load pattern alone: 54 -> 48 us per C3 launch from HBM,
+// W's layout per bin kappa: [chain / T][K-block of 8 branches][chain % T][8 branches] (cf32),
+// T = kFcTile chains: fc_mac's load instruction for 8 chains and one K-block reads 512
+// contiguous bytes, the CTT loads of a wave tile are adjacent when T >= 8 CTT, and the K-blocks
+// follow each other (its load pattern alone, T = 8: 54 -> 48 us per C3 launch from HBM,
 // tools/micro/fc_floor.hip).  Element (kappa, chain c, branch r) at
-// kappa w_ks + fc_w_chain(c, Dp) + fc_w_branch(r).
-constexpr int kFcTile = 8;
+// kappa w_ks + fc_w_chain(c, Dp) + fc_w_branch(r).  Capacities are multiples of T.  T = 32 (a
+// wave's four tiles of 8 chains in 2 KB runs): fc_mac 0.467-0.468 of HBM at C3 vs 0.443-0.460
+// for T = 8 and 0.467-0.471 for T = 64, same box (profiles/r03aj_ab_w_tile_c3.txt); 32 is
+// already the smallest capacity, so small engines allocate nothing extra.
+#ifndef OWRX_FC_TILE
+#define OWRX_FC_TILE 32
+#endif
+constexpr int kFcTile = OWRX_FC_TILE;
+static_assert(kFcTile >= 8 && (kFcTile & (kFcTile - 1)) == 0, "W tile: a power of two >= 8 chains");
 #define OWRX_DEV_HOST_INLINE __host__ __device__ __forceinline__
 OWRX_DEV_HOST_INLINE int64_t fc_w_chain(int c, int Dp) {
     return (int64_t)(c / kFcTile) * kFcTile * Dp + (c % kFcTile) * 8;
@@ -357,6 +365,7 @@ hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int
 }
 
 int64_t fc_w_chain_offset(int c, int Dp) { return fc_w_chain(c, Dp); }
+int fc_w_tile() { return kFcTile; }
 
 // ---- y_c[k0 + m] = rot_c(k0 + m) IDFT_M(Y_c[f])[m] into the group's output rows ------------
 // grid: ceil(nchains F / RW) workgroups of RW = 1024 / M rows; block 256.
