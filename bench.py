@@ -639,7 +639,8 @@ def main():
         wf_traffic_src.append(src)
     wf_traffic_src = "; ".join(sorted(set(wf_traffic_src)))
 
-    traffic, traffic_src = pmc_traffic("fc_mac<" if fast else "ddc_lds<", args.config)
+    mac_name = "fc_mac<" if os.environ.get("OWRX_FC_MAC") == "reg" else "fc_mac_lds<"
+    traffic, traffic_src = pmc_traffic(mac_name if fast else "ddc_lds<", args.config)
     rt = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
@@ -718,8 +719,8 @@ def main():
             "chains_total": C * world,
             "roofline": {
                 "bound": mac_bound,
-                "kernel": ("fc_mac: the fast-convolution DDC's per-bin complex GEMM (frames x "
-                           "chains x branches) on v_mfma_f32_16x16x4_f32" if fast else
+                "kernel": ("fc_mac (%s): the fast-convolution DDC's per-bin complex GEMM (frames x "
+                           "chains x branches) on v_mfma_f32_16x16x4_f32" % mac_name.rstrip("<") if fast else
                            "ddc_lds (direct polyphase Shift + FirDecimate)"),
                 "achieved": round(mac_gbs, 1) if mac_bound == "hbm" else round(achieved_tf, 3),
                 "peak": HBM_PEAK_GBS if mac_bound == "hbm" else FP32_PEAK_TFLOPS,

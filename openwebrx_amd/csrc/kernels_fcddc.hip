@@ -350,6 +350,157 @@ fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs,
         }
 }
 
+// ---- fc_mac with the operand stream through an LDS ring (LDS-DMA; the default form) ---------
+// Same workgroup decode, K split, MFMA order and epilogue as fc_mac (bit-identical Y).  Each wave
+// streams its own K-blocks into a private ring of NR slots with global_load_lds_dwordx4 (1 KiB per
+// instruction, no VGPR destination, no duplicate lanes): per K-block CTT/2 instructions of W
+// (two 8-chain runs of 512 B each) and FTT of U (16 frames x 64 B), NR - 1 blocks in flight.
+// Only the issuing wave reads a slot, so its counted vmcnt orders the reads (no barrier).
+// Slot image: [t][chain % 8][branch pair] then [ft][frame][branch pair], 16 B entries.
+template <int FTT, int CTT, int NR>
+__global__ void __launch_bounds__(64 * kFcKSplit)
+fc_mac_lds(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs, int64_t w_ks,
+           int nchains, int Fs, int F, int Dp, int M, int ncg, int chain_fastest,
+           float2* __restrict__ Y) {
+    constexpr int P = CTT / 2 + FTT;  // DMA instructions per K-block
+    constexpr int kSlot = P * 1024;
+    constexpr int kRing = NR * kSlot;
+    constexpr int kRed = (kFcKSplit - 1) * FTT * CTT * 64 * 16;
+    constexpr int kLds = kFcKSplit * kRing > kRed ? kFcKSplit * kRing : kRed;
+    static_assert((NR - 1) * P <= 63, "vmcnt holds 6 bits");
+    __shared__ __attribute__((aligned(1024))) char lds[kLds];
+    const int w = blockIdx.x;
+    const int xcd = w & 7;
+    const int q = w >> 3;
+    const int mper = M >> 3;
+    int kap, cg, fg;
+    if (chain_fastest) {
+        cg = q % ncg;
+        const int r1 = q / ncg;
+        kap = xcd * mper + r1 % mper;
+        fg = r1 / mper;
+    } else {
+        kap = xcd * mper + q % mper;
+        const int rest = q / mper;
+        cg = rest % ncg;
+        fg = rest / ncg;
+    }
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int g = lane >> 4;
+    const int col = lane & 15;
+    const int cc = col >> 1;
+    const bool bim = col & 1;
+    const int nkb = (Dp >> 3) / kFcKSplit;
+    const int kb0 = wave * nkb;
+    char* ring = lds + wave * kRing;
+
+    // DMA sources (per lane): W instruction i covers tiles 2i, 2i + 1 (lanes 0-31, 32-63), lane
+    // (l & 31) = chain (l & 31) >> 2, branch pair l & 3; U instruction ft: frame l >> 2, pair l & 3
+    const float2* ws[CTT / 2];
+#pragma unroll
+    for (int i = 0; i < CTT / 2; ++i) {
+        const int c = cg * 8 * CTT + (2 * i + (lane >> 5)) * 8 + ((lane & 31) >> 2);
+        ws[i] = W + (int64_t)kap * w_ks + fc_w_chain(c < nchains ? c : 0, (int)w_cs) +
+                fc_w_branch(8 * kb0 + 2 * (lane & 3));
+    }
+    const float2* us[FTT];
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft) {
+        const int f = fg * 16 * FTT + ft * 16 + (lane >> 2);
+        us[ft] = U + ((int64_t)kap * Fs + (f < F ? f : 0)) * Dp + 8 * kb0 + 2 * (lane & 3);
+    }
+    auto issue = [&](int kb) {
+        const int k = kb < nkb ? kb : nkb - 1;
+        char* s = ring + (kb % NR) * kSlot;
+#pragma unroll
+        for (int i = 0; i < CTT / 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(ws[i] + (int64_t)k * kFcTile * 8),
+                                             (__attribute__((address_space(3))) void*)(s + i * 1024), 16, 0, 0);
+#pragma unroll
+        for (int ft = 0; ft < FTT; ++ft)
+            __builtin_amdgcn_global_load_lds((const void*)(us[ft] + 8 * k),
+                                             (__attribute__((address_space(3))) void*)(s + (CTT / 2 + ft) * 1024), 16, 0, 0);
+    };
+    fc_f4 acc[FTT][CTT];
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) acc[ft][t] = fc_f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < NR - 1; ++j) issue(j);
+    constexpr int kWait = (NR - 1) * P;  // vmcnt once block kb has landed
+    constexpr int kEnc = (kWait & 15) | ((kWait >> 4) << 14) | (7 << 4) | (15 << 8);
+    for (int kb = 0; kb < nkb; ++kb) {
+        issue(kb + NR - 1);  // into the slot block kb - 1 left (its reads retired before its MFMAs)
+        __builtin_amdgcn_s_waitcnt(kEnc);
+        __builtin_amdgcn_sched_barrier(0);
+        const char* s = ring + (kb % NR) * kSlot;
+        fc_f4 ua[FTT], wa[CTT];
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) wa[t] = *(const fc_f4*)(s + t * 512 + cc * 64 + g * 16);
+#pragma unroll
+        for (int ft = 0; ft < FTT; ++ft) ua[ft] = *(const fc_f4*)(s + (CTT / 2 + ft) * 1024 + col * 64 + g * 16);
+        __builtin_amdgcn_sched_barrier(0);  // all reads of the slot issued back to back
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            float bsel[CTT];
+#pragma unroll
+            for (int t = 0; t < CTT; ++t) {
+                const float wr = (st < 2) ? wa[t].x : wa[t].z;
+                const float wi = (st < 2) ? wa[t].y : wa[t].w;
+                bsel[t] = (st & 1) ? (bim ? wr : -wi) : (bim ? wi : wr);
+            }
+#pragma unroll
+            for (int ft = 0; ft < FTT; ++ft) {
+                const float a = ua[ft][st];
+#pragma unroll
+                for (int t = 0; t < CTT; ++t)
+                    acc[ft][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bsel[t], acc[ft][t], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // the clamped tail blocks land before the ring is reused
+    __syncthreads();
+    fc_f4* red = (fc_f4*)lds;  // [kFcKSplit - 1][FTT * CTT][64]
+    if (wave > 0) {
+#pragma unroll
+        for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+            for (int t = 0; t < CTT; ++t) red[((wave - 1) * FTT * CTT + ft * CTT + t) * 64 + lane] = acc[ft][t];
+    }
+    __syncthreads();
+    if (wave > 0) return;
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) {
+            const int i = ft * CTT + t;
+            acc[ft][t] = (acc[ft][t] + red[i * 64 + lane]) +
+                         (red[(FTT * CTT + i) * 64 + lane] + red[(2 * FTT * CTT + i) * 64 + lane]);
+        }
+#pragma unroll
+    for (int ft = 0; ft < FTT; ++ft)
+#pragma unroll
+        for (int t = 0; t < CTT; ++t) {
+            const fc_f4 o = acc[ft][t];
+            fc_f4 p;
+            p.x = __shfl_xor(o.x, 1);
+            p.y = __shfl_xor(o.y, 1);
+            p.z = __shfl_xor(o.z, 1);
+            p.w = __shfl_xor(o.w, 1);
+            const int c = cg * 8 * CTT + t * 8 + cc;
+            if (c >= nchains) continue;
+            const int fb = fg * 16 * FTT + ft * 16 + 4 * g + (bim ? 2 : 0);
+            const float2 y0 = bim ? make_float2(p.z, o.z) : make_float2(o.x, p.x);
+            const float2 y1 = bim ? make_float2(p.w, o.w) : make_float2(o.y, p.y);
+            float2* yc = Y + ((int64_t)c * Fs) * M + kap;
+            if (fb < F) yc[(int64_t)fb * M] = y0;
+            if (fb + 1 < F) yc[(int64_t)(fb + 1) * M] = y1;
+        }
+}
+
 // ---- a member's spectra to another slot of the tiled W (swap-remove on a chain's leave) ------
 // grid M (one bin each), block 256
 __global__ void __launch_bounds__(256)
@@ -466,8 +617,19 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
         const char* v = getenv("OWRX_FC_ORDER");
         return (v && strcmp(v, "kappa") == 0) ? 0 : 1;
     }();
+    // the LDS-DMA ring form by default: C3 fc_mac 0.469-0.495 of HBM vs 0.455-0.465 with register
+    // operands, 5 815-5 899 vs 5 712-5 788 Msps, same box (profiles/r03al_ab_fc_mac_lds_c3.txt);
+    // OWRX_FC_MAC=reg: the register form (A/B)
+    static const bool lds_ring = [] {
+        const char* v = getenv("OWRX_FC_MAC");
+        return !(v && strcmp(v, "reg") == 0);
+    }();
     if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
-    if (wide)
+    if (lds_ring && wide)
+        hipLaunchKernelGGL((fc_mac_lds<2, 4, 2>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
+    else if (lds_ring)
+        hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
+    else if (wide)
         hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     else
         hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);

@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace owrx;
@@ -141,8 +142,48 @@ int main() {
         return tot * 1e3 / 20;
     };
     const double wb = nw * 8.0;
+    {  // LDS-ring variants: Y identical to fc_mac<1, 8>
+        std::vector<float2> y0(ny), y1(ny);
+        hipMemset(Y, 0, ny * 8);
+        hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        hipMemcpy(y0.data(), Y, ny * 8, hipMemcpyDeviceToHost);
+        auto cmp = [&](const char* name) {
+            hipMemcpy(y1.data(), Y, ny * 8, hipMemcpyDeviceToHost);
+            size_t bad = 0;
+            for (int c = 0; c < C; ++c)
+                for (int f = 0; f < F; ++f)
+                    for (int k = 0; k < M; ++k) {
+                        const size_t i = ((size_t)c * Fs + f) * M + k;
+                        bad += memcmp(&y0[i], &y1[i], 8) != 0;
+                    }
+            printf("%s: %zu of %d outputs differ from fc_mac<1,8>\n", name, bad, C * F * M);
+        };
+        hipMemset(Y, 0, ny * 8);
+        hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        cmp("fc_mac_lds<1,8,2>");
+        hipMemset(Y, 0, ny * 8);
+        hipLaunchKernelGGL((fc_mac_lds<1, 8, 3>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        cmp("fc_mac_lds<1,8,3>");
+        hipMemset(Y, 0, ny * 8);
+        hipLaunchKernelGGL((fc_mac_lds<1, 8, 4>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        cmp("fc_mac_lds<1,8,4>");
+    }
     for (int rep = 0; rep < 2; ++rep) {
-        double us = timed([&] {
+        double us;
+        us = timed([&] {
+            hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        });
+        printf("fc_mac_lds NR=2  %7.1f us  W %6.0f GB/s (%.3f of 8 TB/s)\n", us, wb / us / 1e3, wb / us / 8e6);
+        us = timed([&] {
+            hipLaunchKernelGGL((fc_mac_lds<1, 8, 3>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        });
+        printf("fc_mac_lds NR=3  %7.1f us  W %6.0f GB/s (%.3f of 8 TB/s)\n", us, wb / us / 1e3, wb / us / 8e6);
+        us = timed([&] {
+            hipLaunchKernelGGL((fc_mac_lds<1, 8, 4>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
+        });
+        printf("fc_mac_lds NR=4  %7.1f us  W %6.0f GB/s (%.3f of 8 TB/s)\n", us, wb / us / 1e3, wb / us / 8e6);
+
+        us = timed([&] {
             hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(256), 0, 0, U, W, (int64_t)Dp, (int64_t)C * Dp, C, Fs, F, Dp, M, ncg, 1, Y);
         });
         printf("fc_mac<1,8>      %7.1f us  W %6.0f GB/s (%.3f of 8 TB/s)\n", us, wb / us / 1e3, wb / us / 8e6);
