@@ -639,8 +639,15 @@ def main():
         wf_traffic_src.append(src)
     wf_traffic_src = "; ".join(sorted(set(wf_traffic_src)))
 
-    mac_name = "fc_mac<" if os.environ.get("OWRX_FC_MAC") == "reg" else "fc_mac_lds<"
-    traffic, traffic_src = pmc_traffic(mac_name if fast else "ddc_lds<", args.config)
+    # fc_mac_lds (LDS-DMA ring) where the GEMM grid takes more than one workgroup per CU, fc_mac
+    # (register operands) otherwise or with OWRX_FC_MAC=reg: the newest PMC summary names which ran
+    mac_name = "fc_mac"
+    traffic, traffic_src = None, "direct-form DDC"
+    for pref in (("fc_mac_lds<", "fc_mac<") if fast else ("ddc_lds<",)):
+        traffic, traffic_src = pmc_traffic(pref, args.config)
+        if traffic is not None:
+            mac_name = pref.rstrip("<")
+            break
     rt = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
@@ -720,7 +727,7 @@ def main():
             "roofline": {
                 "bound": mac_bound,
                 "kernel": ("fc_mac (%s): the fast-convolution DDC's per-bin complex GEMM (frames x "
-                           "chains x branches) on v_mfma_f32_16x16x4_f32" % mac_name.rstrip("<") if fast else
+                           "chains x branches) on v_mfma_f32_16x16x4_f32" % mac_name if fast else
                            "ddc_lds (direct polyphase Shift + FirDecimate)"),
                 "achieved": round(mac_gbs, 1) if mac_bound == "hbm" else round(achieved_tf, 3),
                 "peak": HBM_PEAK_GBS if mac_bound == "hbm" else FP32_PEAK_TFLOPS,

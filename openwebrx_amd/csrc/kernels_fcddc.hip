@@ -624,10 +624,21 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
         const char* v = getenv("OWRX_FC_MAC");
         return !(v && strcmp(v, "reg") == 0);
     }();
+    // the ring where the grid needs two or more workgroups per CU (C3: 512); a grid one round of
+    // single workgroups holds (C4's per-GPU share: 128, long K) keeps register operands, which
+    // measured 6 % faster there than the ring at 2 or 4 slots (profiles/r03ap_ab_fc_mac_c4.txt)
+    static const int ncu = [] {
+        int d = 0, n = 0;
+        if (hipGetDevice(&d) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+            return 256;
+        return n;
+    }();
+    const bool ring = lds_ring && (int)gm.x > ncu;
     if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
-    if (lds_ring && wide)
+    if (ring && wide)
         hipLaunchKernelGGL((fc_mac_lds<2, 4, 2>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
-    else if (lds_ring)
+    else if (ring)
         hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     else if (wide)
         hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
