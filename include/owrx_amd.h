@@ -32,6 +32,7 @@ extern "C" {
 #define OWRX_EINVAL (-22)
 #define OWRX_ENOSPC (-28)   /* output ring overrun (oldest data dropped) */
 #define OWRX_ENODEV (-19)   /* no gfx950 device */
+#define OWRX_ETIMEDOUT (-110) /* a wait on the GPU exceeded the stall timeout (engine marked failed) */
 
 #define OWRX_DEMOD_NFM 0
 #define OWRX_DEMOD_AM 1
@@ -108,6 +109,21 @@ int owrx_set_input_retention(owrx_engine* e, int blocks);
  * engines.  No reference counterpart: csdr runs each module in its own thread with its own
  * buffer (owrx/dsp.py:846-863 pumps); this is the engine's equivalent of that slack. */
 int owrx_set_pipeline_depth(owrx_engine* e, int blocks);
+/* Stall bound (default 20 000 ms): no call blocks longer than this waiting for the GPU.  When a
+ * wait expires the engine is marked failed and the call, and every later one, returns
+ * OWRX_ETIMEDOUT -- the engine-side counterpart of the reference's source failure
+ * (owrx/source/__init__.py:432-448 fail() -> onFail, owrx/connection.py:292-295), which the
+ * pycsdr shim turns into a FAILED driver with every output buffer ended.  owrx_engine_destroy
+ * waits one more bound for the streams and then leaks the engine's buffers rather than free them
+ * under a running kernel. */
+int owrx_set_stall_timeout(owrx_engine* e, int64_t ms);
+/* Test hook: enqueues a kernel that occupies stream 0 (A: FFT / DDC), 1 (B) or 2 (C) for `us`
+ * microseconds and then exits (stall injection for the bounded-wait path). */
+int owrx_debug_stall(owrx_engine* e, int stream, int64_t us);
+/* Host self-test (no GPU needed): the fast-convolution DDC's tiled filter-spectrum layout maps
+ * every (member slot < cap, branch < Dp) inside its bin's row of cap * Dp entries, one entry per
+ * element.  OWRX_OK, or OWRX_EINVAL (the reason in owrx_last_error). */
+int owrx_selftest_w_layout(int Dp, int cap);
 /* Device window slot for the next block (write there, e.g. with ncclBroadcast), then commit. */
 int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity);
 int owrx_commit(owrx_engine* e, int64_t nsamples);

@@ -18,6 +18,7 @@ OWRX_ENOMEM = -12
 OWRX_EINVAL = -22
 OWRX_ENOSPC = -28
 OWRX_ENODEV = -19
+OWRX_ETIMEDOUT = -110  # a GPU wait exceeded the stall timeout (engine failed)
 
 DEMOD_NFM, DEMOD_AM, DEMOD_SSB, DEMOD_WFM, DEMOD_SAM = 0, 1, 2, 3, 4
 OUT_S16, OUT_ADPCM, OUT_F32, OUT_IQ, OUT_SEL = 0, 1, 2, 3, 4
@@ -138,6 +139,9 @@ PROTOTYPES = {
     "owrx_waterfall_set_batch": (_i32, [_vp, _i32, _i32, _i64]),
     "owrx_set_input_retention": (_i32, [_vp, _i32]),
     "owrx_set_pipeline_depth": (_i32, [_vp, _i32]),
+    "owrx_set_stall_timeout": (_i32, [_vp, _i64]),
+    "owrx_debug_stall": (_i32, [_vp, _i32, _i64]),
+    "owrx_selftest_w_layout": (_i32, [_i32, _i32]),
     "owrx_waterfall_destroy": (_i32, [_vp, _i32]),
     "owrx_waterfall_row_bytes": (_i64, [_vp, _i32]),
     "owrx_waterfall_read": (_i64, [_vp, _i32, _vp, _i64]),
@@ -200,4 +204,6 @@ def check(rc, what=""):
         raise ValueError(msg)
     if rc == OWRX_ENOMEM:
         raise MemoryError(msg)
+    if rc == OWRX_ETIMEDOUT:
+        raise TimeoutError(-rc, msg)  # an OSError subclass: the shim's failure path catches it
     raise OSError(-rc, msg)

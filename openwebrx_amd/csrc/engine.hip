@@ -24,6 +24,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <dlfcn.h>
@@ -74,6 +75,7 @@ void set_last_error(const char* fmt, ...) {
 }
 
 // kernel launchers (kernels_*.hip)
+hipError_t launch_debug_sleep(int64_t us, hipStream_t st);  // synth.hip (stall injection)
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, int fpg, const float* window, const float* ones,
                          const float2* tw, float* partial, float2* scratch, hipStream_t st);
@@ -96,6 +98,7 @@ hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
 hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int dst, hipStream_t st);
 int64_t fc_w_chain_offset(int c, int Dp);  // chain c's first entry in a bin's row of the tiled W
 int fc_w_tile();                           // chains per W tile: capacities are multiples of it
+int fc_w_layout_check(int Dp, int cap);    // host self-test of the tiled W layout
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
@@ -549,6 +552,9 @@ struct owrx_engine {
     int64_t block_index = 0;
     int64_t slot_tail = 0;  // oldest block whose outputs are not yet in the host rings
     bool failed = false;
+    bool stalled = false;            // a bounded wait expired (owrx_set_stall_timeout)
+    int64_t stall_ms = 20000;        // the longest any host-side wait blocks before failing
+    hipEvent_t evSync = nullptr;     // marker for bounded stream synchronisation
     bool debug = false;
     int timing = 0;                  // timing events every `timing` blocks (0: off)
     std::vector<GroupWork> work;     // per-block scratch: the groups with outputs
@@ -614,6 +620,41 @@ struct owrx_engine {
 // helpers
 // ------------------------------------------------------------------------------------------
 
+// Bounded waits.  The reference turns a source that stops producing into fail() -> every
+// client's onFail (owrx/source/__init__.py:432-448, owrx/connection.py:292-295); here a GPU
+// that stops completing work must do the same instead of blocking the OpenWebRX process in a
+// HIP synchronisation call forever.  Every host-side wait polls its event against a deadline
+// (e->stall_ms); an expired wait marks the engine failed (`stalled`) and returns
+// OWRX_ETIMEDOUT, which the pycsdr shim turns into FAILED and ended outputs.
+static int wait_ev(owrx_engine* e, hipEvent_t ev) {
+    hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return OWRX_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    int polls = 0;
+    while (q == hipErrorNotReady) {
+        const double ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > (double)e->stall_ms) {
+            e->failed = true;
+            e->stalled = true;
+            set_last_error("GPU stalled: no progress for %lld ms (owrx_set_stall_timeout)",
+                           (long long)e->stall_ms);
+            return OWRX_ETIMEDOUT;
+        }
+        // spin briefly (a block's tail is typically tens of microseconds), then sleep
+        if (++polls > 64) std::this_thread::sleep_for(std::chrono::microseconds(polls > 4096 ? 200 : 20));
+        q = hipEventQuery(ev);
+    }
+    HIPCHK(q);
+    return OWRX_OK;
+}
+
+// everything enqueued on `st` so far, within the stall bound
+static int sync_stream(owrx_engine* e, hipStream_t st) {
+    HIPCHK(hipEventRecord(e->evSync, st));
+    return wait_ev(e, e->evSync);
+}
+
 static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
     int64_t nk = e->max_block / D + 4;
     if (frac > 0 && frac < 1.0) nk = (int64_t)std::ceil(nk / frac) + 4;
@@ -663,14 +704,14 @@ static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
     if (n == 0) return OWRX_OK;
     const size_t a = (n + 255) & ~(size_t)255;
     if (a > e->up_cap) {
-        if (e->h_up) HIPCHK(hipStreamSynchronize(e->sA));
+        if (e->h_up) RCCHK(sync_stream(e, e->sA));
         hfree(e->h_up);
         e->up_cap = std::max<size_t>(4u << 20, a);
         HIPCHK(halloc(&e->h_up, e->up_cap));
         e->up_head = 0;
     }
     if (e->up_head + a > e->up_cap) {  // wrap: the ring's earlier copies must have run
-        HIPCHK(hipStreamSynchronize(e->sA));
+        RCCHK(sync_stream(e, e->sA));
         e->up_head = 0;
     }
     memcpy(e->h_up + e->up_head, src, n);
@@ -742,7 +783,7 @@ static void free_slot_staging(Slot& s) {
 static int drain_slot(owrx_engine* e, int si) {
     Slot& s = e->slots[si];
     if (s.chains_pending) {
-        HIPCHK(hipEventSynchronize(s.evB));
+        RCCHK(wait_ev(e, s.evB));
         s.chains_pending = false;
         if (s.timed) {
             float ms = 0;
@@ -801,7 +842,7 @@ static int drain_slot(owrx_engine* e, int si) {
         }
     } else if (s.timed) {
         float ms = 0;
-        HIPCHK(hipEventSynchronize(s.a3));
+        RCCHK(wait_ev(e, s.a3));
         if (hipEventElapsedTime(&ms, s.a1, s.a2) == hipSuccess) e->stats.gpu_ms_ddc += ms;
         if (s.timed_mac && hipEventElapsedTime(&ms, s.m0, s.m1) == hipSuccess)
             e->stats.gpu_ms_ddc_mac += ms;
@@ -810,13 +851,13 @@ static int drain_slot(owrx_engine* e, int si) {
     }
     if (s.timed_wf) {
         float ms = 0;
-        HIPCHK(hipEventSynchronize(s.a1));
+        RCCHK(wait_ev(e, s.a1));
         if (hipEventElapsedTime(&ms, s.a0, s.a1) == hipSuccess) e->stats.gpu_ms_waterfall += ms;
         s.timed_wf = false;
     }
     if (s.timed_wff) {
         float ms = 0;
-        HIPCHK(hipEventSynchronize(s.w1));
+        RCCHK(wait_ev(e, s.w1));
         if (hipEventElapsedTime(&ms, s.w0, s.w1) == hipSuccess) e->stats.gpu_ms_waterfall_fft += ms;
         s.timed_wff = false;
     }
@@ -834,7 +875,7 @@ static int drain_rows(owrx_engine* e, bool block, int keep) {
             if (q == hipErrorNotReady) break;
             HIPCHK(q);
         } else {
-            HIPCHK(hipEventSynchronize(r.evC));
+            RCCHK(wait_ev(e, r.evC));
         }
         for (auto& kv : e->wfs) {
             Waterfall* w = kv.second.get();
@@ -875,7 +916,7 @@ static int drain_slots(owrx_engine* e, bool block, int keep) {
 
 static int drain_all(owrx_engine* e) {
     e->stats.pipeline_drains++;
-    HIPCHK(hipStreamSynchronize(e->sA));
+    RCCHK(sync_stream(e, e->sA));
     e->in_done = e->block_index - 1;
     RCCHK(drain_rows(e, true, 0));
     return drain_slots(e, true, 0);
@@ -1475,7 +1516,7 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
 // Wait until block j's stream-A work (which read its input and its staged descriptors) is done.
 static int wait_input_block(owrx_engine* e, int64_t j) {
     if (j <= e->in_done || j < 0) return OWRX_OK;
-    HIPCHK(hipEventSynchronize(e->evIn[j % kInEv]));
+    RCCHK(wait_ev(e, e->evIn[j % kInEv]));
     e->in_done = j;
     return OWRX_OK;
 }
@@ -1602,7 +1643,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 hipLaunchKernelGGL(copy_jobs, dim3((unsigned)std::min<int64_t>(64, (maxb + 4095) / 4096), nj),
                                    dim3(256), 0, e->sA, S.h_jobs);
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipStreamSynchronize(e->sA));  // the table is reused right away
+                RCCHK(sync_stream(e, e->sA));  // the table is reused right away
                 nj = 0;
                 maxb = 0;
             }
@@ -1757,8 +1798,9 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     }                                                                \
     std::lock_guard<std::recursive_mutex> _lk((e)->mu);              \
     if ((e)->failed) {                                               \
-        set_last_error("engine failed earlier (HIP error)");         \
-        return OWRX_EIO;                                             \
+        set_last_error((e)->stalled ? "engine failed earlier (GPU stalled)" \
+                                    : "engine failed earlier (HIP error)"); \
+        return (e)->stalled ? OWRX_ETIMEDOUT : OWRX_EIO;             \
     }                                                                \
     hipSetDevice((e)->device);
 
@@ -1766,7 +1808,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     do {                                             \
         int _rc = (expr);                            \
         if (_rc < 0) {                               \
-            if (_rc == OWRX_EIO) (e)->failed = true; \
+            if (_rc == OWRX_EIO || _rc == OWRX_ETIMEDOUT) (e)->failed = true; \
             return _rc;                              \
         }                                            \
     } while (0)
@@ -1874,6 +1916,7 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
         return OWRX_EIO;
     };
     if (create_streams(e) != hipSuccess) return fail("stream");
+    if (hipEventCreateWithFlags(&e->evSync, hipEventDisableTiming) != hipSuccess) return fail("event");
     for (auto& r : e->rslots) {
         if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
@@ -1914,10 +1957,16 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
 int owrx_engine_destroy(owrx_engine* e) {
     if (!e) return OWRX_EINVAL;
     hipSetDevice(e->device);
+    // every stream drained, within the stall bound (a stalled engine gets one more bound to
+    // finish; if its work still has not completed, its buffers are leaked rather than freed
+    // under a running kernel, and the process keeps going)
+    if (e->stalled) e->failed = false;
+    bool stuck = false;
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
-        if (st) hipStreamSynchronize(st);
+        if (st && e->evSync && sync_stream(e, st) == OWRX_ETIMEDOUT) stuck = true;
     for (auto& r : e->rslots)
-        if (r.stream) hipStreamSynchronize(r.stream);
+        if (r.stream && e->evSync && sync_stream(e, r.stream) == OWRX_ETIMEDOUT) stuck = true;
+    if (stuck) return OWRX_ETIMEDOUT;
     for (auto& kv : e->chains) free_chain(e, kv.second.get());
     for (auto& kv : e->wfs) free_wf(kv.second.get());
     for (auto& g : e->groups) {
@@ -1952,6 +2001,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     }
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamDestroy(st);
+    if (e->evSync) hipEventDestroy(e->evSync);
     delete e;
     return OWRX_OK;
 }
@@ -1979,6 +2029,35 @@ int owrx_set_input_retention(owrx_engine* e, int blocks) {
     return OWRX_OK;
 }
 int64_t owrx_engine_max_block(owrx_engine* e) { return e ? e->max_block : OWRX_EINVAL; }
+
+int owrx_selftest_w_layout(int Dp, int cap) {
+    const int rc = fc_w_layout_check(Dp, cap);
+    if (rc) set_last_error("owrx_selftest_w_layout(Dp=%d, cap=%d): %s", Dp, cap,
+                           rc == -1 ? "not an engine geometry" : rc == -2 ? "entry outside the row"
+                                                                          : "two entries on one element");
+    return rc ? OWRX_EINVAL : OWRX_OK;
+}
+
+int owrx_set_stall_timeout(owrx_engine* e, int64_t ms) {
+    ENGINE_GUARD(e);
+    if (ms < 1) {
+        set_last_error("owrx_set_stall_timeout: ms must be >= 1");
+        return OWRX_EINVAL;
+    }
+    e->stall_ms = ms;
+    return OWRX_OK;
+}
+
+int owrx_debug_stall(owrx_engine* e, int stream, int64_t us) {
+    ENGINE_GUARD(e);
+    hipStream_t st = stream == 0 ? e->sA : stream == 1 ? e->sB : stream == 2 ? e->sC : nullptr;
+    if (!st || us < 0 || us > 60000000) {
+        set_last_error("owrx_debug_stall: stream 0..2, 0 <= us <= 60 s");
+        return OWRX_EINVAL;
+    }
+    HIPCHK(launch_debug_sleep(us, st));
+    return OWRX_OK;
+}
 
 int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t n) {
     ENGINE_GUARD(e);
@@ -2010,7 +2089,7 @@ int owrx_ingest_buffer(owrx_engine* e, float** dev_ptr, int64_t* capacity) {
     bool wrapped = false;
     RC_FAIL(e, ring_room(e, e->max_block, &wrapped));
     // the caller writes on a stream of its own: the move must be done first
-    if (wrapped) RC_FAIL(e, hipStreamSynchronize(e->sA) == hipSuccess ? OWRX_OK : OWRX_EIO);
+    if (wrapped) RC_FAIL(e, sync_stream(e, e->sA));
     *dev_ptr = (float*)(e->d_ring + e->wp);
     *capacity = e->max_block;
     return OWRX_OK;

@@ -24,6 +24,7 @@
 // f32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 products and sums; the complex product is the
 // real GEMM [Ur Ui] x [[Wr Wi] [-Wi Wr]]).  Its operands stream once per block: W (C M Dp 8 B,
 // unique per chain) from HBM, U from L2, so fc_mac sits between the HBM and the f32 MFMA roof.
+#include <vector>
 #include <stdlib.h>
 #include <string.h>
 
@@ -516,6 +517,24 @@ hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int
 }
 
 int64_t fc_w_chain_offset(int c, int Dp) { return fc_w_chain(c, Dp); }
+
+// Host self-test of the tiled W layout (owrx_selftest_w_layout): for a group of `cap` member
+// slots and Dp branches, every (slot, branch) entry that fc_make_w / fc_move_w write and fc_mac /
+// fc_mac_lds read lies inside the bin's row of cap * Dp entries, and no two share one.  0 if so;
+// -1 for a geometry the engine never allocates (cap not a multiple of the tile, Dp not of 8);
+// -2 for an entry outside the row; -3 for two entries on one element.
+int fc_w_layout_check(int Dp, int cap) {
+    if (Dp <= 0 || cap <= 0 || Dp % 8 || cap % kFcTile) return -1;
+    const int64_t row = (int64_t)cap * Dp;
+    std::vector<uint8_t> seen((size_t)row, 0);
+    for (int c = 0; c < cap; ++c)
+        for (int r = 0; r < Dp; ++r) {
+            const int64_t o = fc_w_chain(c, Dp) + fc_w_branch(r);
+            if (o < 0 || o >= row) return -2;
+            if (seen[(size_t)o]++) return -3;
+        }
+    return 0;
+}
 int fc_w_tile() { return kFcTile; }
 
 // ---- y_c[k0 + m] = rot_c(k0 + m) IDFT_M(Y_c[f])[m] into the group's output rows ------------

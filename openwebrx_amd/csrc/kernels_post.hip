@@ -54,6 +54,9 @@ OWRX_DEV void move_front(PTR buf, int64_t off, int n) {
     __syncthreads();
 }
 
+// Output-count searches step at most this far from their estimate (normally 0-2 steps).
+constexpr int kSearchMax = 64;
+
 // WFM audio: FractionalDecimator(FLOAT, IF/audio, prefilter=True) (csdr/chain/analog.py:69)
 // on the FmDemod + Limit output the block appended at wf_buf[kWfHist, +nsq): a causal lowpass
 // prefilter, then the 12-point Lagrange interpolator of the Selector's FractionalDecimator at
@@ -83,8 +86,11 @@ OWRX_DEV int wfm_audio(const ChainPost& P, ChainStateP& S, int nsq) {
         auto valid = [&](int64_t k) { return (int64_t)ceil(6.0 + (double)k * r) + 5 < total; };
         int64_t ke = (int64_t)floor(((double)total - 12.0) / r);
         if (ke < S.wf_next) ke = S.wf_next;
-        while (valid(ke)) ++ke;
-        while (ke > S.wf_next && !valid(ke - 1)) --ke;
+        // the estimate is within a sample or two; a bounded search (a descriptor with a
+        // non-positive or non-finite rate must not spin stream A forever)
+        for (int it = 0; it < kSearchMax && valid(ke); ++it) ++ke;
+        for (int it = 0; it < kSearchMax && ke > S.wf_next && !valid(ke - 1); ++it) --ke;
+        if (!(r > 0.0) || valid(ke) || (ke > S.wf_next && !valid(ke - 1))) ke = S.wf_next;
         sh_n = (int)(ke - S.wf_next);
     }
     __syncthreads();
@@ -265,8 +271,9 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
             };
             int64_t ke = (int64_t)floor(((double)ddc_total - 12.0) / r);
             if (ke < S.fd_next) ke = S.fd_next;
-            while (valid(ke)) ++ke;
-            while (ke > S.fd_next && !valid(ke - 1)) --ke;
+            for (int it = 0; it < kSearchMax && valid(ke); ++it) ++ke;  // bounded (see wfm_audio)
+            for (int it = 0; it < kSearchMax && ke > S.fd_next && !valid(ke - 1); ++it) --ke;
+            if (!(r > 0.0) || valid(ke) || (ke > S.fd_next && !valid(ke - 1))) ke = S.fd_next;
             sh_n_fd = (int)(ke - S.fd_next);
         }
         __syncthreads();

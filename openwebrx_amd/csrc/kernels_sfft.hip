@@ -36,6 +36,7 @@ chain_sfft(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts
     constexpr int PPT = N / kSfThreads;
     const ChainPost& P = posts[blockIdx.x];
     if (P.sf_n != N) return;  // chains without (or with another size of) secondary FFT
+    if (P.sf_hop <= 0 || P.sf_avg <= 0) return;  // never a frame loop that does not advance
     extern __shared__ __align__(16) uint8_t smem[];
     SfLds<LOGN>& S = *reinterpret_cast<SfLds<LOGN>*>(smem);
     const int tid = threadIdx.x;

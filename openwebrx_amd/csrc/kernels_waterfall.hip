@@ -27,6 +27,10 @@ namespace owrx {
 
 OWRX_DEV float2 ld2(const float2* p) { return *p; }
 
+// A buffer-load offset past every waterfall descriptor's range (num_records < 2^30 bytes): such
+// loads return zeros and never touch memory, so a prefetch can be issued unconditionally.
+constexpr int kWfOob = 1 << 30;
+
 template <int LOGN>
 __global__ void __launch_bounds__(1024)
 wf_fft_power(const float2* __restrict__ blk, int64_t blk_start,
@@ -353,12 +357,13 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
     const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
                                                       (int)(sizeof(float) * N), 0x00020000);
     auto load_x = [&](int f, c2* v) {
+        const int fo = f < nfr ? f * hop * 8 : kWfOob;  // f == nfr: zeros (see wf_fft_l32)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             // two dword loads the compiler pairs into one dwordx2 (this hipcc's vector-returning
             // raw_buffer_load_b64 / _b128 builtins load one dword and splat it); the frame offset
             // in the one VGPR, the tap offset r NT in the SGPR soffset
-            const int vo = tid0 * 8 + f * hop * 8;
+            const int vo = tid0 * 8 + fo;
             v[r] = c2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
                       __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0))};
         }
@@ -425,7 +430,7 @@ wf_fft_r16(const float2* __restrict__ blk, int64_t blk_start,
                 const int d = ((tid / ns) * ns * 16) + k;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) sm[wf_pad(d + r * ns)] = f2_of(a[r]);
-                if (pass == 0 && f + 1 < nfr) load_x(f + 1, nx);
+                if (pass == 0) load_x(f + 1, nx);
             }
             ns *= 16;
             WF_STAMP(st0 + 2 + pass);
@@ -594,6 +599,22 @@ OWRX_DEV void f2dft32(float2* a) {
     for (int k1 = 0; k1 < 8; ++k1) f2dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
 }
 
+// W_64^m = exp(-2 pi i m / 64), m a compile-time constant after unrolling
+OWRX_DEV float2 w64c(int m) {
+    constexpr float q[17] = {1.00000000000000000f, 0.99518472667219693f, 0.98078528040323043f,
+                             0.95694033573220882f, 0.92387953251128674f, 0.88192126434835505f,
+                             0.83146961230254524f, 0.77301045336273699f, 0.70710678118654757f,
+                             0.63439328416364549f, 0.55557023301960229f, 0.47139673682599781f,
+                             0.38268343236508984f, 0.29028467725446233f, 0.19509032201612833f,
+                             0.09801714032956077f, 0.0f};
+    // cos(2 pi m / 64) over the whole turn from the first quadrant's table
+    auto cs = [&](int v) {
+        v &= 63;
+        return v <= 16 ? q[v] : v <= 32 ? -q[32 - v] : v <= 48 ? -q[v - 32] : q[64 - v];
+    };
+    return make_float2(cs(m), -cs(m - 16));  // sin(2 pi m / 64) = cos(2 pi (m - 16) / 64)
+}
+
 // ---- wf_fft_l32: N = 16384 as 32 x 32 x 16, two LDS exchanges ------------------------------
 // 512 threads of 32 points (two waves per SIMD, up to 256 VGPRs each), one workgroup per CU.
 // LDS stores are the scarcest resource of the exchange (~85 B/clk/CU for any store width), so
@@ -640,10 +661,15 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         0x00020000);
     const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
                                                       (int)(sizeof(float) * N), 0x00020000);
+    // frame f's samples; f == nfr (the prefetch after the last frame) is offset past the
+    // descriptor's range, so those loads return zeros without touching memory.  The prefetch is
+    // unconditional: behind an `if (f + 1 < nfr)` the wait-count pass merged the two paths at
+    // vmcnt(0) before the window products, so every frame waited for its successor's samples.
     auto load_x = [&](int f, float2* v) {
+        const int fo = f < nfr ? f * hop * 8 : kWfOob;
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
-            const int vo = t0 * 8 + f * hop * 8;
+            const int vo = t0 * 8 + fo;
             v[r] = make_float2(
                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, r * NT * 8, 0)),
                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, r * NT * 8, 0)));
@@ -686,7 +712,7 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 #pragma unroll
             for (int r = 0; r < 32; ++r) a[r] = make_float2(nx[r].x * wv[r], nx[r].y * wv[r]);
         }
-        if (f + 1 < nfr) load_x(f + 1, nx);
+        load_x(f + 1, nx);
         f2dft32(a);
         if (f < 2) WF_STAMP(sb + 1);
         __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
@@ -746,6 +772,192 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         if (f < 2) WF_STAMP(sb + 5);
     }
     float* out = partial + (int64_t)blockIdx.x * N;  // = group * (N << qlog) + j * N
+#pragma unroll
+    for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
+    WF_STAMP(13);
+    WF_RSTAMP(15);
+}
+
+// ---- wf_fft_h2: N = 16384 as two 8192-point halves, two workgroups per CU ------------------
+// wf_fft_l32 holds a whole frame's image (128 KiB) in one CU's LDS, so one 512-thread workgroup
+// per CU runs its passes in lockstep: while its waves wait at a barrier, for the LDS or for the
+// window loads, nothing else issues (measured: ~20 k cycles per frame against ~6.6 k of VALU).
+// Here one decimation-in-frequency step splits the frame, X[2k + h] = DFT_8192(y_h)[k] with
+//   y_h[n] = (w[n] x[n] + (-1)^h w[n + 8192] x[n + 8192]) W_16384^(h n),   n < 8192,
+// and a 256-thread workgroup transforms one half h of its group's frames through a 64 KiB image,
+// so two independent workgroups share each CU and one's exchanges and barriers run under the
+// other's arithmetic.  Each reads the whole frame (the pair's second read of a frame is an L2
+// hit: the halves of group g are blocks b and b + 8, one XCD under round-robin placement).
+// The 8192-point transform is Stockham radix 32 x 16 x 16, 32 points per thread:
+//  P1 (Ns = 1):   a[r] = y[t + 256 r] (h = 1: times W_64^r) -> DFT32 (h = 1: times W_N^t)
+//                 -> image[32 t + k]
+//  P2 (Ns = 32):  j = t + 256 b (b < 2): image[j + 512 r] * W_512^(r (t & 31)) (LDS table
+//                 [15][32]) -> DFT16 -> image[(j >> 5) 512 + (j & 31) + 32 r]
+//  P3 (Ns = 512): j = t + 256 b: image[j + 512 r] * W_8192^(r j) (bases W_8192^(r t) from four
+//                 exact powers, W_32^(r b)) -> DFT16 -> |Y|^2 of half-bins j + 512 r, summed in
+//                 registers over the group's frames
+// The image uses wf_fft_l32's XOR swizzle (every store and read bank-conflict-free).  The
+// window taps of the thread's 64 samples stay in registers for the whole group.  The partial
+// row is written half-major (bin 2k + h at h 8192 + k), as the DIF-split path's rows are, and
+// wf_finalize reads it back in bin order.
+struct WfH2 {
+    static constexpr int N = 16384, M = 8192, NT = 256;
+    static constexpr int TW2 = M;  // [15][32]: W_512^(r k), r = 1..15
+    static constexpr size_t kLds = sizeof(float2) * (M + 15 * 32);
+};
+
+__global__ void __launch_bounds__(WfH2::NT, 2)
+wf_fft_h2(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+          int ngroups, const float* __restrict__ window, const float2* __restrict__ tw,
+          float* __restrict__ partial) {
+    using K = WfH2;
+    constexpr int N = K::N, M = K::M, NT = K::NT;
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    const int b0 = blockIdx.x;
+    const int gi = (b0 >> 4) * 8 + (b0 & 7);  // groups in runs of 8 workgroups, halves 8 apart
+    const int h = (b0 >> 3) & 1;
+    if (gi >= ngroups) return;
+    const int t0 = threadIdx.x;
+    WF_RSTAMP(14);
+    WF_STAMP(0);
+    const WfGroup g = groups[gi];
+    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
+    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
+    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
+        0x00020000);
+    // samples t + 256 r and their partners + 8192 of frame f, in batches of kB values of r
+    constexpr int kB = 8;
+    auto load_x = [&](int f, int rb, float2* va, float2* vb) {
+        const int vo = t0 * 8 + f * hop * 8;
+#pragma unroll
+        for (int r = 0; r < kB; ++r) {
+            const int so = (rb * kB + r) * NT * 8;
+            va[r] = make_float2(
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, so, 0)),
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, so, 0)));
+            vb[r] = make_float2(
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + M * 8, so, 0)),
+                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + M * 8 + 4, so, 0)));
+        }
+    };
+    // tables (L2-resident) first: vmcnt retires in order
+    float wa[32], wb[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        wa[r] = window[t0 + NT * r];
+        wb[r] = window[t0 + NT * r + M];
+    }
+    float2 tp[4];  // W_8192^(2^i t) = W_N^(2^(i+1) t): P3's bases W_8192^(r t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tp[i] = tw[(t0 << (i + 1)) & (N - 1)];
+    const float2 wt = tw[t0];  // W_N^t (h = 1)
+    float2 t2v[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int e = t0 + NT * i;  // 480 entries: (r - 1) * 32 + k, W_512^(r k) = W_N^(32 r k)
+        t2v[i] = e < 15 * 32 ? tw[((((e >> 5) + 1) * (e & 31)) << 5) & (N - 1)] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        if (t0 + NT * i < 15 * 32) sm[K::TW2 + t0 + NT * i] = t2v[i];
+    if (h) {
+#pragma unroll
+        for (int r = 0; r < 32; ++r) wb[r] = -wb[r];  // y_1: the partner sample subtracted
+    }
+    float acc[32];
+#pragma unroll
+    for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
+#pragma unroll 1
+    for (int f = 0; f < nfr; ++f) {
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        const int sb = 1 + 6 * f;
+        if (f < 2) WF_STAMP(sb);
+        float2 a[32];
+#pragma unroll
+        for (int rb = 0; rb < 32 / kB; ++rb) {
+            float2 va[kB], vb[kB];
+            load_x(f, rb, va, vb);
+#pragma unroll
+            for (int i = 0; i < kB; ++i) {
+                const int r = rb * kB + i;
+                a[r] = make_float2(fmaf(wb[r], vb[i].x, va[i].x * wa[r]),
+                                   fmaf(wb[r], vb[i].y, va[i].y * wa[r]));
+            }
+        }
+        if (h) {  // y_1[n] = (...) W_N^n, n = t + 256 r: W_64^r here, W_N^t after the DFT
+#pragma unroll
+            for (int r = 1; r < 32; ++r) a[r] = (r & 1) ? f2mul(a[r], w64c(r)) : f2mul32(a[r], r >> 1);
+        }
+        f2dft32(a);
+        if (h) {
+#pragma unroll
+            for (int k = 0; k < 32; ++k) a[k] = f2mul(a[k], wt);
+        }
+        if (f < 2) WF_STAMP(sb + 1);
+        __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
+#pragma unroll
+        for (int k = 0; k < 32; ++k) sm[32 * t + (k ^ (t & 15))] = a[l32_at(k)];
+        if (f < 2) WF_STAMP(sb + 2);
+        __syncthreads();
+        // P2: two radix-16 butterflies j = t + 256 b, twiddle W_512^(r (t & 31))
+        {
+            const int k = t & 31;
+            const float2* T = sm + K::TW2 + k;
+            float2 c[2][16];
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) c[b][r] = sm[wf_swz32(t + NT * b + 512 * r)];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) {
+                const float2 w = T[(r - 1) * 32];
+                c[0][r] = f2mul(c[0][r], w);
+                c[1][r] = f2mul(c[1][r], w);
+                if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 twiddles live
+            }
+            f2dft<16>(c[0]);
+            f2dft<16>(c[1]);
+            __syncthreads();  // every P2 read before any P2 store
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int base = ((t >> 5) + 8 * b) * 512 + k;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sm[wf_swz32(base + 32 * r)] = c[b][r];
+            }
+        }
+        if (f < 2) WF_STAMP(sb + 3);
+        __syncthreads();
+        // P3: j = t + 256 b, W_8192^(r j) = W_8192^(r t) W_32^(r b)
+        if (f < 2) WF_STAMP(sb + 4);
+        float2 tb[16];
+        tb[1] = tp[0];
+        tb[2] = tp[1];
+        tb[4] = tp[2];
+        tb[8] = tp[3];
+        tb[3] = f2mul(tp[0], tp[1]);
+        tb[5] = f2mul(tp[0], tp[2]);
+        tb[6] = f2mul(tp[1], tp[2]);
+        tb[7] = f2mul(tb[3], tp[2]);
+#pragma unroll
+        for (int r = 9; r < 16; ++r) tb[r] = f2mul(tb[r - 8], tp[3]);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            float2 c[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) c[r] = sm[wf_swz32(t + NT * b + 512 * r)];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) c[r] = f2mul(c[r], b ? f2mul32(tb[r], r) : tb[r]);
+            f2dft<16>(c);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                acc[b + 2 * r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b + 2 * r]));
+        }
+        if (f < 2) WF_STAMP(sb + 5);
+    }
+    float* out = partial + (int64_t)gi * N + h * M;  // half-major: bin 2k + h at h M + k
 #pragma unroll
     for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
     WF_STAMP(13);

@@ -53,6 +53,19 @@ synth_iq(float2* __restrict__ out, int64_t n, int64_t start, double fs, int nc,
     out[i] = make_float2(re, im);
 }
 
+// Stall injection for the bounded-wait test (owrx_debug_stall): one wave that sleeps for `us`
+// microseconds of the 100 MHz real-time counter and exits -- a stream that stops completing
+// work for a known time, ended by the kernel itself.
+__global__ void __launch_bounds__(64) debug_sleep(int64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+hipError_t launch_debug_sleep(int64_t us, hipStream_t st) {
+    hipLaunchKernelGGL(debug_sleep, dim3(1), dim3(64), 0, st, us * 100);
+    return hipGetLastError();
+}
+
 }  // namespace owrx
 
 using namespace owrx;

@@ -102,6 +102,15 @@ class Engine:
     def sync(self):
         check(lib.owrx_sync(self._h), "owrx_sync")
 
+    def set_stall_timeout(self, ms):
+        """Longest any call waits on the GPU before the engine fails with TimeoutError
+        (owrx_set_stall_timeout; default 20 s)."""
+        check(lib.owrx_set_stall_timeout(self._h, int(ms)), "owrx_set_stall_timeout")
+
+    def debug_stall(self, stream, us):
+        """Test hook: occupy stream 0 (A), 1 (B) or 2 (C) for `us` microseconds."""
+        check(lib.owrx_debug_stall(self._h, int(stream), int(us)), "owrx_debug_stall")
+
     def set_input_retention(self, blocks):
         """process_device callers whose blocks stay valid for `blocks` further calls (e.g. a
         resident recording): the host may then run that many blocks ahead of the GPU."""

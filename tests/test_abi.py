@@ -66,3 +66,18 @@ def test_chain_params_struct_layout_matches_header():
                                               check=True).stdout.split()]
     want = [getattr(_lib.ChainParams, n).offset for n in names] + [ctypes.sizeof(_lib.ChainParams)]
     assert got == want
+
+
+def test_w_layout_selftest_every_capacity():
+    """The fast-convolution DDC's tiled filter spectra (kernels_fcddc.hip fc_w_chain /
+    fc_w_branch): for C4's design (D = 5120 -> Dp = 5184) and C3's (D = 833 -> Dp = 864), every
+    member slot's entries lie inside its bin's row and no two overlap, at every capacity the
+    engine allocates (multiples of the tile up to 4096 members); geometries it never allocates
+    are rejected.  Host code: no GPU needed."""
+    from openwebrx_amd import _lib
+    L = _lib.lib
+    for dp in (864, 5184):
+        for cap in list(range(32, 1025, 32)) + [2048, 4096]:
+            assert L.owrx_selftest_w_layout(dp, cap) == 0, (dp, cap, _lib.last_error())
+    assert L.owrx_selftest_w_layout(5184, 130) == _lib.OWRX_EINVAL
+    assert L.owrx_selftest_w_layout(5180, 128) == _lib.OWRX_EINVAL

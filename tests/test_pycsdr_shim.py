@@ -599,6 +599,57 @@ def test_engine_failure_ends_outputs(monkeypatch):
 
 
 @pytest.mark.gpu
+def test_stalled_gpu_fails_driver_and_ends_outputs():
+    """A GPU that stops completing work must fail like a dead SDR source, not hang the server
+    (owrx/source/__init__.py:432-448 fail() -> onFail; owrx/dsp.py:858-861 pumps end on None):
+    a stream-A kernel that sleeps 3 s (owrx_debug_stall) against a 300 ms stall bound makes the
+    engine's bounded wait expire -> TimeoutError -> the driver is FAILED, the on_failure callback
+    runs once with that error and the client's audio reader returns None within seconds."""
+    import time
+    fs = 2400000
+    wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 23)
+    mods = selector(fs, 1000, "nfm") + demodulator("nfm") + client_audio()
+    ch = Chain(mods)
+    out = M.Buffer(Format.CHAR, size=1 << 22)
+    ch.setWriter(out)
+    ch.setReader(wide.getReader())
+    r = out.getReader()
+    failed = []
+    _graph.on_failure(wide, failed.append)
+    blk = np.zeros(_graph.BLOCK, np.complex64).tobytes()
+    wide.write(blk)  # the driver plans the chain, creates its engine and pushes
+    drv, deadline = None, time.time() + 60
+    while time.time() < deadline:
+        drv = _graph._drivers.get(id(wide))
+        if drv is not None and drv.engines:
+            break
+        time.sleep(0.05)
+    assert drv is not None and drv.engines
+    with _graph._lock:
+        drv.engine.set_stall_timeout(300)
+        drv.engine.debug_stall(0, 3000000)
+        t_stall = time.time()
+    for _ in range(8):
+        wide.write(blk)
+    got = []
+
+    def pump():
+        while r.read() is not None:
+            pass
+        got.append(time.time())
+
+    t = threading.Thread(target=pump, daemon=True)
+    t.start()
+    t.join(20)
+    assert got, "the audio reader did not end"
+    assert got[0] - t_stall < 10.0
+    assert _graph.state(wide) == "FAILED"
+    assert len(failed) == 1 and isinstance(failed[0], TimeoutError), failed
+    time.sleep(max(0.0, t_stall + 3.5 - time.time()))  # the injected kernel has exited
+    _graph.finish(wide)
+
+
+@pytest.mark.gpu
 def test_pycsdr_sharded_engines_equal_single(monkeypatch):
     """The drop-in over several engines in one process (OWRX_AMD_DEVICES="0,0,0": three
     engines on the test box's one GPU -- the code path of one engine per GPU) writes

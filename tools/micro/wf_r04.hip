@@ -1,0 +1,239 @@
+// Waterfall FFT kernels in isolation (diagnostic, not part of the product), round 4: C3's
+// geometry (10 Msps, N = 16384, hop 11454), FT frames per launch in groups of F, frames read
+// from HBM (OWRX_WF_FLUSH=1, default: 512 MiB streamed between launches, as the DDC's operand
+// streams evict them in the engine) or from the Infinity Cache (OWRX_WF_FLUSH=0).
+// Prints us per launch and the rate on the algorithmic bytes (the frames' span of cf32 IQ,
+// 8 B per sample read once), for the production kernel(s) and the load pattern alone, and the
+// relative difference of each kernel's partial rows from wf_fft_r16<14> (the radix-16 kernel).
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt
+//        -fno-slp-vectorize wf_r04.hip -o wf_r04
+// Run:   ./wf_r04 [FT ...]
+#include "../../openwebrx_amd/csrc/kernels_waterfall.hip"
+#include "wf_l32x.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+using namespace owrx;
+
+#define CK(x)                                                                                \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) {                                                              \
+            printf("%s: %s\n", #x, hipGetErrorString(e_));                                   \
+            exit(1);                                                                         \
+        }                                                                                    \
+    } while (0)
+
+constexpr int N = 16384;
+
+// the frame loads (16 B per lane, 512 threads) and partial-row stores alone, the next frame in
+// flight while the current one is summed: the memory floor of the access pattern
+__global__ void __launch_bounds__(512)
+wf_mem_pf(const float2* __restrict__ blk, const WfGroup* __restrict__ groups, float* __restrict__ partial) {
+    const WfGroup g = groups[blockIdx.x];
+    const int t = threadIdx.x;
+    const int nfr = g.nframes;
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(blk + g.start), 0,
+                                                      (int)(8 * ((int64_t)(nfr - 1) * g.hop + N)), 0x00020000);
+    float acc[16] = {};
+    float4 nx[16];
+    auto ld = [&](int f, float4* v) {
+        const int fo = f < nfr ? f * g.hop * 8 : (1 << 30);
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            v[m] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, t * 16 + fo, m * 8192, 0));
+    };
+    ld(0, nx);
+    for (int f = 0; f < nfr; ++f) {
+        float4 x[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) x[m] = nx[m];
+        ld(f + 1, nx);
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            acc[m] = fmaf(x[m].x, x[m].x, fmaf(x[m].y, x[m].y, fmaf(x[m].z, x[m].z, fmaf(x[m].w, x[m].w, acc[m]))));
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m)
+        for (int u = 0; u < 2; ++u) partial[(int64_t)blockIdx.x * N + 2 * (t + 512 * m) + u] = acc[m];
+}
+
+__global__ void flush_read(const float4* __restrict__ p, size_t n, float* sink) {
+    float acc = 0.f;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float4 v = p[i];
+        acc += v.x + v.y + v.z + v.w;
+    }
+    if (acc == 12345.f) sink[0] = acc;
+}
+
+static void* g_flush = nullptr;
+static bool flush_on() {
+    static const bool v = !getenv("OWRX_WF_FLUSH") || atoi(getenv("OWRX_WF_FLUSH"));
+    return v;
+}
+static double time_us(const std::function<void()>& launch) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const size_t fb = (size_t)512 << 20;
+    if (!g_flush) {
+        CK(hipMalloc(&g_flush, fb));
+        CK(hipMemset(g_flush, 0, fb));
+    }
+    const int iters = 40;
+    std::vector<float> t;
+    for (int i = 0; i < iters + 5; ++i) {
+        if (flush_on())
+            hipLaunchKernelGGL(flush_read, dim3(4096), dim3(256), 0, 0, (const float4*)g_flush, fb / 16,
+                               (float*)g_flush);
+        CK(hipEventRecord(e0, 0));
+        launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (i >= 5) t.push_back(ms * 1e3f);
+    }
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main(int argc, char** argv) {
+    const int hop = 11454;
+    std::vector<int> fts;
+    for (int i = 1; i < argc; ++i) fts.push_back(atoi(argv[i]));
+    if (fts.empty()) fts = {960, 1920};
+    const int FTmax = *std::max_element(fts.begin(), fts.end());
+    const int64_t S = (int64_t)FTmax * hop + N;
+    std::vector<float2> x(S);
+    srand(1);
+    for (auto& v : x) v = float2{rand() / (float)RAND_MAX - 0.5f, rand() / (float)RAND_MAX - 0.5f};
+    std::vector<float> win(N);
+    for (int i = 0; i < N; ++i) win[i] = (float)(0.54 - 0.46 * cos(2 * M_PI * i / (N - 1)));
+    std::vector<float2> tw(N);
+    for (int k = 0; k < N; ++k) tw[k] = float2{(float)cos(2 * M_PI * k / N), (float)-sin(2 * M_PI * k / N)};
+    float2 *dx, *dtw;
+    float *dwin, *dref, *dpart;
+    WfGroup* dg;
+    CK(hipMalloc(&dx, sizeof(float2) * S));
+    CK(hipMalloc(&dtw, sizeof(float2) * N));
+    CK(hipMalloc(&dwin, sizeof(float) * N));
+    CK(hipMalloc(&dref, sizeof(float) * (size_t)FTmax * N));
+    CK(hipMalloc(&dpart, sizeof(float) * (size_t)FTmax * N));
+    CK(hipMalloc(&dg, sizeof(WfGroup) * FTmax));
+    CK(hipMemcpy(dx, x.data(), sizeof(float2) * S, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dtw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dwin, win.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    CK(hipFuncSetAttribute((const void*)wf_fft_r16<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfR16<14>::kLds));
+    CK(hipFuncSetAttribute((const void*)wf_fft_l32, hipFuncAttributeMaxDynamicSharedMemorySize,
+                           (int)WfL32::kLds));
+#define SETX(v) CK(hipFuncSetAttribute((const void*)wf_fft_l32x<v>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WfL32::kLds))
+    SETX(0); SETX(1); SETX(2); SETX(3); SETX(4); SETX(5); SETX(6);
+    CK(hipFuncSetAttribute((const void*)wf_fft_h2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WfH2::kLds));
+    printf("N=%d hop=%d, frames from %s\n", N, hop, flush_on() ? "HBM (512 MiB flushed between launches)" : "cache");
+    for (int FT : fts) {
+        const double alg = 8.0 * ((double)(FT - 1) * hop + N);
+        for (int F : {2, 4, 8}) {
+            const int G = (FT + F - 1) / F;
+            std::vector<WfGroup> grp(G);
+            for (int g = 0; g < G; ++g) grp[g] = WfGroup{(int64_t)g * F * hop, std::min(F, FT - g * F), hop};
+            CK(hipMemcpy(dg, grp.data(), sizeof(WfGroup) * G, hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(wf_fft_r16<14>, dim3(G), dim3(WfR16<14>::NT), WfR16<14>::kLds, 0, dx, (int64_t)0,
+                               dg, dwin, dtw, dref);
+            CK(hipDeviceSynchronize());
+            std::vector<float> a((size_t)G * N), b((size_t)G * N);
+            CK(hipMemcpy(a.data(), dref, sizeof(float) * a.size(), hipMemcpyDeviceToHost));
+            struct V {
+                const char* name;
+                std::function<void()> run;
+                bool check;
+                bool half_major = false;  // partial rows bin 2k + h at h N/2 + k
+            };
+            std::vector<V> vs = {
+                {"l32", [&] {
+                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, (int64_t)0,
+                                        dg, dwin, dtw, dpart, 0, 0);
+                 }, true},
+                {"r16", [&] {
+                     hipLaunchKernelGGL(wf_fft_r16<14>, dim3(G), dim3(WfR16<14>::NT), WfR16<14>::kLds, 0, dx,
+                                        (int64_t)0, dg, dwin, dtw, dpart);
+                 }, true},
+                {"h2", [&] {
+                     hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx,
+                                        (int64_t)0, dg, G, dwin, dtw, dpart);
+                 }, true, true},
+#define XV(v, nm) {nm, [&] { hipLaunchKernelGGL(wf_fft_l32x<v>, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, dg, dwin, dtw, dpart); }, v == 0}
+                XV(0, "x0"), XV(1, "x-load"), XV(2, "x-lds"), XV(3, "x-ld-lds"), XV(4, "x-math"), XV(5, "x-ld-mth"), XV(6, "x-lds-mth"),
+                {"mem", [&] {
+                     hipLaunchKernelGGL(wf_mem_pf, dim3(G), dim3(512), 0, 0, dx, dg, dpart);
+                 }, false},
+            };
+            for (auto& v : vs) {
+                const double us = time_us(v.run);
+                printf("FT=%5d F=%d G=%4d %-8s %8.2f us  %7.1f GB/s  %5.1f %% of 8 TB/s", FT, F, G, v.name, us,
+                       alg / us * 1e-3, alg / us * 1e-3 / 80.0);
+                if (v.check) {
+                    v.run();
+                    CK(hipDeviceSynchronize());
+                    CK(hipMemcpy(b.data(), dpart, sizeof(float) * b.size(), hipMemcpyDeviceToHost));
+                    double d2 = 0, a2 = 0, worst = 0;
+                    if (v.half_major) {  // back to bin order
+                        std::vector<float> nb(b.size());
+                        for (int q = 0; q < G; ++q)
+                            for (int k = 0; k < N; ++k)
+                                nb[(size_t)q * N + k] = b[(size_t)q * N + (k & 1) * (N / 2) + (k >> 1)];
+                        b.swap(nb);
+                    }
+                    for (size_t i = 0; i < a.size(); ++i) {
+                        const double d = fabs((double)a[i] - b[i]);
+                        d2 += d * d;
+                        a2 += (double)a[i] * a[i];
+                        worst = std::max(worst, d / std::max((double)fabs(a[i]), 1e-30));
+                    }
+                    printf("  vs r16: rel-RMS %.2e max rel %.2e", sqrt(d2 / a2), worst);
+                }
+                printf("\n");
+                fflush(stdout);
+            }
+#ifdef OWRX_WF_STAMPS
+            if (F == 4) {
+                auto stamps = [&](const char* nmk, int nwg, const std::function<void()>& run) {
+                    time_us(run);
+                    std::vector<unsigned long long> st((size_t)1024 * 16);
+                    CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wf_stamp), sizeof(unsigned long long) * st.size()));
+                    auto med = [&](int a0, int b0) {
+                        std::vector<long long> d;
+                        for (int q = 0; q < std::min(nwg, 1024); ++q) d.push_back((long long)(st[q * 16 + b0] - st[q * 16 + a0]));
+                        std::sort(d.begin(), d.end());
+                        return d[d.size() / 2];
+                    };
+                    const double clk = (double)med(0, 13) / (double)med(14, 15) * 0.1;
+                    printf("   stamps %s (median cycles, wave 0): clock %.2f GHz, total %lld\n", nmk, clk, med(0, 13));
+                    const char* nm[] = {"load+dft32", "P1 bar+store", "bar+P2", "bar+P3 reads", "P3 math"};
+                    for (int f = 0; f < 2; ++f) {
+                        const int b0 = 1 + 6 * f;
+                        printf("   frame %d starts at %lld:", f, med(0, b0));
+                        for (int p = 0; p < 5; ++p) printf("  %s %lld", nm[p], med(b0 + p, b0 + p + 1));
+                        printf("\n");
+                    }
+                    printf("   frame 2.. to end: %lld\n", med(12, 13));
+                };
+                stamps("x0", G, [&] { hipLaunchKernelGGL(wf_fft_l32x<0>, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, dg, dwin, dtw, dpart); });
+                stamps("h2", 2 * G, [&] { hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx, (int64_t)0, dg, G, dwin, dtw, dpart); });
+            }
+#endif
+        }
+    }
+    return 0;
+}
