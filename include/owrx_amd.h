@@ -141,14 +141,23 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
 /* FftChain._setBlockSize / setFftAverages / setCompression (fft.py:51-55, 11-16, 87-96) */
 int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_number,
                        int adpcm);
-/* Launch granularity of the waterfall FFT (an engine-side choice; the rows, bit for bit, and
- * their order do not depend on it).  Complete frame groups are launched when at least
+/* Launch granularity of the waterfall FFT (an engine-side choice; for a fixed batch setting the
+ * rows, bit for bit, and their order do not depend on how the stream is cut into blocks -- the
+ * setting picks the frames summed per workgroup, so rows under different settings may differ in
+ * the last ulp of the dB value).  Complete frame groups are launched when at least
  * `min_frames` are ready, or when the oldest pending frame starts `max_lag` or more samples
  * before the end of the newest block, or before it would leave the engine history, and on
  * owrx_sync.  min_frames <= 1 (the default): every block's frames in that block.  max_lag <= 0:
  * as far as the history allows.  Rows then reach the reader up to max_lag samples later than
  * with per-block launches (the throughput / latency trade of Fft(every_n_samples) batching). */
 int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t max_lag);
+/* Wall-clock bound on that batching (the row latency a client sees): pending frames are also
+ * launched at the first block call at which waiting for one more block (the engine's running
+ * estimate of the interval between block calls) would leave the oldest pending frame unlaunched
+ * for more than `max_wall_ms` after the call that made it ready.  At the stream's real-time rate
+ * this launches every block or two; fed faster than real time (a throughput run) the frame
+ * count bound applies.  max_wall_ms <= 0: no wall-clock bound (the default). */
+int owrx_waterfall_set_latency(owrx_engine* e, int handle, double max_wall_ms);
 int owrx_waterfall_destroy(owrx_engine* e, int handle);
 /* bytes of one output row: (fft_size+10)/2 with ADPCM, 4*fft_size without */
 int64_t owrx_waterfall_row_bytes(owrx_engine* e, int handle);
@@ -284,6 +293,12 @@ typedef struct {
     double  host_ms_build;     /* host time building a block's chain descriptors (of process) */
     double  host_ms_launch;    /* host time enqueueing its kernels, copies and events */
     double  host_ms_collect;   /* host time moving finished blocks into the output rings */
+    /* waterfall row latency (wall clock): from the owrx_push_iq / owrx_process_device /
+     * owrx_commit call that completed a row's last frame to the row being readable
+     * (owrx_waterfall_read) */
+    double  wf_row_latency_ms_max;
+    double  wf_row_latency_ms_sum;
+    int64_t wf_rows_latency_n;
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

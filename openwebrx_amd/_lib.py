@@ -107,6 +107,9 @@ class Stats(ctypes.Structure):
         ("host_ms_build", ctypes.c_double),
         ("host_ms_launch", ctypes.c_double),
         ("host_ms_collect", ctypes.c_double),
+        ("wf_row_latency_ms_max", ctypes.c_double),
+        ("wf_row_latency_ms_sum", ctypes.c_double),
+        ("wf_rows_latency_n", ctypes.c_int64),
     ]
 
 
@@ -137,6 +140,7 @@ PROTOTYPES = {
     "owrx_waterfall_create": (_i32, [_vp, _i32, _i32, _i32, _f32, _i32, _pi32]),
     "owrx_waterfall_set": (_i32, [_vp, _i32, _i32, _i32, _i32]),
     "owrx_waterfall_set_batch": (_i32, [_vp, _i32, _i32, _i64]),
+    "owrx_waterfall_set_latency": (_i32, [_vp, _i32, _f64]),
     "owrx_set_input_retention": (_i32, [_vp, _i32]),
     "owrx_set_pipeline_depth": (_i32, [_vp, _i32]),
     "owrx_set_stall_timeout": (_i32, [_vp, _i64]),

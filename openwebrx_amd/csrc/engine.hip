@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <deque>
 #include <map>
 #include <unordered_map>
 #include <memory>
@@ -216,6 +217,11 @@ struct Waterfall {
     int fpg = 1;             // frames per group (fixed per configuration: rows are bit-stable)
     int batch_min = 0;       // owrx_waterfall_set_batch: launch once this many frames are ready
     int64_t batch_lag = 0;   //   ... or the oldest pending frame is this far behind (0: history)
+    double batch_wall_ms = 0;  // owrx_waterfall_set_latency: ... or it would wait longer than this
+    double t_pending = -1;     // wall time (ms) of the block call that made the oldest pending frame ready
+    // (stream end of a block, wall time of its call) for the blocks whose frames are not all
+    // launched: a row's readiness time is the first block that covered its last frame
+    std::deque<std::pair<int64_t, double>> blk_times;
     bool carry_valid = false;
     int carry_idx = 0;
     int64_t rows = 0;
@@ -239,6 +245,7 @@ struct Waterfall {
     uint8_t* h_bytes[kRowSlots] = {};
     int pend_rows[kRowSlots] = {};
     int pend_adpcm[kRowSlots] = {};
+    std::vector<double> pend_t[kRowSlots];  // readiness time of each row in the slot
     ByteRing ring;
     std::vector<WfGroup> groups;
     std::vector<WfRow> rowdesc;
@@ -553,6 +560,9 @@ struct owrx_engine {
     int64_t slot_tail = 0;  // oldest block whose outputs are not yet in the host rings
     bool failed = false;
     bool stalled = false;            // a bounded wait expired (owrx_set_stall_timeout)
+    double t_block = 0;              // wall time (ms) of the current block call
+    double t_last_block = -1;        // ... of the previous one
+    double block_interval_ms = 0;    // running estimate of the interval between block calls
     int64_t stall_ms = 20000;        // the longest any host-side wait blocks before failing
     hipEvent_t evSync = nullptr;     // marker for bounded stream synchronisation
     bool debug = false;
@@ -619,6 +629,11 @@ struct owrx_engine {
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // Bounded waits.  The reference turns a source that stops producing into fail() -> every
 // client's onFail (owrx/source/__init__.py:432-448, owrx/connection.py:292-295); here a GPU
@@ -886,6 +901,15 @@ static int drain_rows(owrx_engine* e, bool block, int keep) {
             w->rows += nr;
             e->stats.waterfall_rows += nr;
             w->pend_rows[ri] = 0;
+            const double tnow = now_ms();
+            for (double tr : w->pend_t[ri]) {
+                if (tr < 0) continue;
+                const double lat = tnow - tr;
+                e->stats.wf_row_latency_ms_max = std::max(e->stats.wf_row_latency_ms_max, lat);
+                e->stats.wf_row_latency_ms_sum += lat;
+                e->stats.wf_rows_latency_n++;
+            }
+            w->pend_t[ri].clear();
         }
         r.pending = false;
         e->row_tail++;
@@ -1128,28 +1152,31 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
 // ------------------------------------------------------------------------------------------
 
 // Frames summed by one FFT workgroup (one partial |X|^2 row per group).  Fixed per waterfall
-// configuration (engine geometry, hop, batching) and groups start at fixed frame offsets of a
-// row, so the summation order -- hence every row, bit for bit -- does not depend on how the
-// stream is cut into blocks or launches.  `frames` is the launch size expected: a block's
-// frames, or the batch.
-//  - wf_fft_l32 (N = 16384): 2, or 4 for launches of >= 3 frames per CU (micro-benchmark, C3
-//    geometry: 366 frames F=2 21.3 us vs F=1 24.6 / F=3 27.6; 960 frames F=4 41.4 us vs F=2
-//    45.5; profiles/r03a_wf_micro_*.txt);
-//  - wf_fft_r16: enough that a launch's frames occupy stream A's CUs about once;
-//  - the DIF split (N = 16384 Q): wf_fft_l32's rule on the Q sub-frames of each frame;
-//  - the four-step FFT (OWRX_WF_KERNEL=fourstep): one frame per group.
+// configuration (engine geometry and hop -- not the launch batching) and groups start at fixed
+// frame offsets of a row, so the summation order -- hence every row, bit for bit -- depends
+// neither on how the stream is cut into blocks nor on how frames are batched into launches:
+//  - N = 16384 and the DIF split (N = 16384 Q): 4 (micro-benchmark, C3 geometry, 960 frames
+//    from HBM: F = 4 49 us vs F = 2 55 us, profiles/r04*_wf_micro.txt);
+//  - wf_fft_r16: enough that a block's frames occupy stream A's CUs about once;
+//  - the four-step FFT (OWRX_WF_KERNEL=fourstep): one frame per group;
+// always clamped so that a group still open at a block's end fits the next block's history.
 static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
     const int64_t hop = std::max(1, w->hop);
-    const int64_t frames = std::max<int64_t>(w->batch_min, e->max_block / hop);
+    const int64_t frames = e->max_block / hop;  // not the batch: rows must not depend on it
     const int64_t cus = std::max(1, e->cus_a);
+    // a group still open at the end of a block is read again from the next block's window, so
+    // its span (fpg - 1) hop + N must fit the history (every kernel)
+    const int64_t fit = std::max<int64_t>(1, (e->history - w->N) / hop + 1);
+    int64_t fpg;
     if (w->N > kWfLdsMaxN) {
         if (!wf_uses_split(w->logn)) return 1;
-        return frames * (w->N / kWfLdsMaxN) >= 3 * cus ? kWfSplitMaxFpg : 2;
+        fpg = kWfSplitMaxFpg;
+    } else if (wf_uses_l32(w->logn)) {
+        fpg = 4;
+    } else {
+        fpg = std::min<int64_t>((frames + cus - 1) / cus, kWfMaxFramesPerGroup);
     }
-    if (wf_uses_l32(w->logn)) return frames >= 3 * cus ? 4 : 2;
-    int64_t fpg = (frames + cus - 1) / cus;
-    fpg = std::min(fpg, (e->history - w->N) / hop);
-    return (int)std::max<int64_t>(1, std::min<int64_t>(fpg, kWfMaxFramesPerGroup));
+    return (int)std::max<int64_t>(1, std::min(fpg, fit));
 }
 
 // Schedules and launches one FftChain's ready frames on stream A (when the batching rule says
@@ -1162,15 +1189,20 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     w->groups.clear();
     w->rowdesc.clear();
     if (w->next_start + w->N > blk_end) return OWRX_OK;  // no frame complete
+    if (w->t_pending < 0) w->t_pending = e->t_block;
     if (w->batch_min > 1 && !force) {
         // launch once enough frames are ready, or the oldest pending one is max_lag behind, or
-        // it would leave the window of the next block (which starts at blk_end - history)
+        // it would leave the window of the next block (which starts at blk_end - history), or
+        // waiting for the next block call would hold it past the wall-clock bound
         const int64_t ready = (blk_end - w->N - w->next_start) / std::max(1, w->hop) + 1;
         const int64_t lag = blk_end - w->next_start;
         const int64_t max_lag = w->batch_lag > 0 ? w->batch_lag : e->history;
         const bool leaving = w->next_start < blk_end + w->hop - e->history;
-        if (ready < w->batch_min && lag < max_lag && !leaving) return OWRX_OK;
+        const bool late = w->batch_wall_ms > 0 &&
+                          e->t_block - w->t_pending + e->block_interval_ms >= w->batch_wall_ms;
+        if (ready < w->batch_min && lag < max_lag && !leaving && !late) return OWRX_OK;
     }
+    w->pend_t[ri].clear();
     int cur_row_first_group = 0;
     bool row_open = false;
     const int adpcm_now = w->adpcm;
@@ -1188,6 +1220,14 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         w->next_start += (int64_t)gf * w->hop;
         w->row_frame += gf;
         if (w->row_frame == w->avg) {
+            // readiness: the first block call whose stream end covered the row's last frame
+            double tr = -1;
+            for (const auto& bt : w->blk_times)
+                if (bt.first >= last + w->N) {
+                    tr = bt.second;
+                    break;
+                }
+            w->pend_t[ri].push_back(tr);
             WfRow r;
             r.first_group = cur_row_first_group;
             r.ngroups = (int)w->groups.size() - cur_row_first_group;
@@ -1211,6 +1251,10 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         }
     }
     const int ncomplete = (int)w->rowdesc.size();
+    // frames still ready after this launch keep the pending time; blocks wholly launched go
+    while (!w->blk_times.empty() && w->blk_times.front().first < w->next_start + w->N)
+        w->blk_times.pop_front();
+    w->t_pending = w->next_start + w->N <= blk_end ? e->t_block : -1;
     if (row_open) {  // partially accumulated row: sum into the carry
         WfRow r;
         r.first_group = cur_row_first_group;
@@ -1260,10 +1304,6 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     return OWRX_OK;
 }
 
-static double now_ms() {
-    return std::chrono::duration<double, std::milli>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 
 // Every waterfall's ready frames (batching rule, or all of them with `force`) on stream A, then
 // the completed rows' FftAdpcm + copy on a row slot's stream.
@@ -1542,6 +1582,14 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const int bp = (int)(e->block_index % e->nslots);
     const int64_t blk_start = e->pos;
     const int64_t blk_end = e->pos + n;
+    // wall-clock bookkeeping of the waterfall batching bound and row latency
+    e->t_block = t_enter;
+    if (e->t_last_block >= 0) {
+        const double d = t_enter - e->t_last_block;
+        e->block_interval_ms = e->block_interval_ms > 0 ? 0.75 * e->block_interval_ms + 0.25 * d : d;
+    }
+    e->t_last_block = t_enter;
+    for (auto& kv : e->wfs) kv.second->blk_times.emplace_back(blk_end, t_enter);
     const int si = (int)(e->block_index % e->nslots);
     Slot& S = e->slots[si];
     // the slot's previous block (k - kSlots) must be drained before its buffers are reused
@@ -2010,7 +2058,8 @@ int64_t owrx_engine_history(owrx_engine* e) { return e ? e->history : OWRX_EINVA
 
 int owrx_set_pipeline_depth(owrx_engine* e, int blocks) {
     ENGINE_GUARD(e);
-    if (blocks < 1 || blocks > kSlots || e->block_index != 0 || !e->chains.empty()) {
+    // a chain created (and destroyed) before sized the per-slot staging for the old depth
+    if (blocks < 1 || blocks > kSlots || e->block_index != 0 || !e->chains.empty() || e->post_cap > 0) {
         set_last_error("owrx_set_pipeline_depth: blocks must be in [1, %d], before the first "
                        "chain and block", kSlots);
         return OWRX_EINVAL;
@@ -2282,6 +2331,14 @@ int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t
         return OWRX_EINVAL;
     }
     RC_FAIL(e, wf_alloc_buffers(e, w));
+    return OWRX_OK;
+}
+
+int owrx_waterfall_set_latency(owrx_engine* e, int handle, double max_wall_ms) {
+    ENGINE_GUARD(e);
+    auto it = e->wfs.find(handle);
+    if (it == e->wfs.end()) return OWRX_EINVAL;
+    it->second->batch_wall_ms = max_wall_ms > 0 ? max_wall_ms : 0;
     return OWRX_OK;
 }
 

@@ -203,6 +203,12 @@ class Waterfall:
         check(lib.owrx_waterfall_set_batch(self.engine.handle, self.id, int(min_frames),
                                            int(max_lag)), "owrx_waterfall_set_batch")
 
+    def set_latency(self, max_wall_ms):
+        """Wall-clock bound on the batching: pending frames launch before they would wait more
+        than `max_wall_ms` (owrx_waterfall_set_latency; <= 0: none)."""
+        check(lib.owrx_waterfall_set_latency(self.engine.handle, self.id, float(max_wall_ms)),
+              "owrx_waterfall_set_latency")
+
     def row_bytes(self):
         return check(lib.owrx_waterfall_row_bytes(self.engine.handle, self.id), "row_bytes")
 

@@ -33,6 +33,18 @@ _drivers = weakref.WeakValueDictionary()  # id(source buffer) -> EngineDriver
 _lock = threading.RLock()
 
 BLOCK = 1 << 18  # IQ samples per engine block (26 ms at 10 Msps)
+# Engine history (samples of the stream kept readable before each block): room for a waterfall
+# batch of up to ~HISTORY / hop frames.  32 MiB of cf32 (two of them in the push ring).
+HISTORY = 1 << 22
+# Waterfall launch batching: frames per FFT launch (four per CU of a 256-CU MI355X) and the
+# wall-clock bound on how long a ready frame may wait for its batch (OWRX_AMD_WF_LATENCY_MS).
+# At the stream's real-time rate the bound launches every block or two (rows within ~50 ms);
+# fed faster than real time (a recording, a backlog) the frame bound gives chip-filling launches.
+WF_BATCH_FRAMES = 960
+
+
+def wf_latency_ms():
+    return float(os.environ.get("OWRX_AMD_WF_LATENCY_MS", "50"))
 
 _failure_callbacks = {}  # id(source buffer) -> [callable(exception)]
 
@@ -374,6 +386,7 @@ class EngineDriver:
         self.error = None
         self._dirty = True
         self._closing = False
+        self._pool = None
         self.reader = source.getReader()  # before any further write: nothing is missed
         self._thread = threading.Thread(target=self._run, name="owrx-engine", daemon=True)
         self._thread.start()
@@ -402,7 +415,7 @@ class EngineDriver:
         from ..engine import Engine
         eng = self.engines.get(slot)
         if eng is None:
-            eng = Engine(1.0, max_block=BLOCK, device=self.devices[slot])
+            eng = Engine(1.0, max_block=BLOCK, device=self.devices[slot], history=HISTORY)
             self.engines[slot] = eng
         return eng
 
@@ -432,6 +445,13 @@ class EngineDriver:
             if kind == "waterfall":
                 obj = eng.waterfall(p["fft_size"], p["hop"], max(1, p["avg"]), p["add_db"],
                                     p["adpcm"])
+                lat = wf_latency_ms()
+                if lat > 0:  # batched launches, bounded in wall-clock time
+                    try:
+                        obj.set_batch(WF_BATCH_FRAMES)
+                        obj.set_latency(lat)
+                    except ValueError:  # a hop the history cannot batch: per-block launches
+                        pass
             else:
                 obj = eng.chain(chain_params_struct(p))
                 if p.get("secondary_fft") is not None:
@@ -474,39 +494,57 @@ class EngineDriver:
         self.segments[hid] = (kind, p, mods, obj, slot)
 
     def _drain(self):
+        """Every segment's new output into its writer: chain audio and s-meter values of each
+        engine with two batched native calls (Engine.read_chains), waterfall rows, secondary
+        FFT rows and taps per object."""
+        by_slot = {}
         for kind, p, mods, obj, slot in list(self.segments.values()):
             out = mods[-1].writer
             if kind == "waterfall":
                 data = obj.read()
                 if data and out is not None:
                     out.write(data)
-            else:
-                data = obj.read_audio()
-                if data and out is not None:
-                    out.write(data)
-                sm = obj.read_smeter()
+                continue
+            by_slot.setdefault(slot, []).append((p, out, obj))
+            sw = p.get("secondary_writer")
+            if p.get("secondary_fft") and sw is not None:
+                rows = obj.read_secondary_fft()
+                if rows.size:
+                    sw.write(rows.tobytes())
+            # taps: the Selector output into selectorBuffer, the demodulator chain's audio
+            # into audioBuffer, for their secondary readers
+            for key, which in (("tap_selector", "selector"), ("tap_audio", "audio")):
+                buf = p.get(key)
+                if buf is not None:
+                    t = obj.read_tap(which)
+                    if t.size:
+                        buf.write(t.tobytes())
+        for slot, segs in by_slot.items():
+            eng = self.engines[slot]
+            audio, alens, sm, scounts = eng.read_chains([obj for _, _, obj in segs])
+            ao = np.concatenate(([0], np.cumsum(alens)))
+            so = np.concatenate(([0], np.cumsum(scounts)))
+            for i, (p, out, obj) in enumerate(segs):
+                if alens[i] and out is not None:
+                    out.write(audio[ao[i]:ao[i + 1]].tobytes())
                 pw = p.get("power_writer")
-                if sm.size and pw is not None:
-                    pw.write(sm.astype(np.float32).tobytes())
-                sw = p.get("secondary_writer")
-                if p.get("secondary_fft") and sw is not None:
-                    rows = obj.read_secondary_fft()
-                    if rows.size:
-                        sw.write(rows.tobytes())
-                # taps: the Selector output into selectorBuffer, the demodulator chain's audio
-                # into audioBuffer, for their secondary readers
-                for key, which in (("tap_selector", "selector"), ("tap_audio", "audio")):
-                    buf = p.get(key)
-                    if buf is not None:
-                        t = obj.read_tap(which)
-                        if t.size:
-                            buf.write(t.tobytes())
+                if scounts[i] and pw is not None:
+                    pw.write(sm[so[i]:so[i + 1]].tobytes())
 
     def _push(self, blk):
         # every engine gets the block from host memory over its own PCIe link (8 B per
-        # sample: 0.5 GB/s per GPU at 61.44 Msps), then all run concurrently
-        for eng in self.engines.values():
-            eng.push(blk)
+        # sample: 0.5 GB/s per GPU at 61.44 Msps); with several engines the pushes run in
+        # parallel threads (the native call releases the GIL), so the engines' host-side block
+        # work overlaps instead of adding up
+        engs = list(self.engines.values())
+        if len(engs) == 1:
+            engs[0].push(blk)
+            return
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="owrx-push")
+        for f in [self._pool.submit(e.push, blk) for e in engs]:
+            f.result()  # re-raises an engine's error in the driver thread
 
     def close(self):
         """Stop reading the source; the thread pushes what it holds, syncs and drains."""

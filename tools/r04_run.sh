@@ -8,6 +8,7 @@ for st in "$@"; do
     micro) timeout -k 10 180 ./tools/micro/wf_r04 ${FT:-960} > gpurun_out/${TAG}_wf_micro.txt 2>&1 || exit $? ;;
     stamps) timeout -k 10 180 ./tools/micro/wf_r04s ${FT:-960} > gpurun_out/${TAG}_wf_stamps.txt 2>&1 || exit $? ;;
     wftest) timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "waterfall" > gpurun_out/${TAG}_pytest_wf.log 2>&1 || exit $? ;;
+    sel) timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "${SEL}" > gpurun_out/${TAG}_pytest_sel.log 2>&1 || exit $? ;;
     test) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_pytest.log 2>&1 || exit $? ;;
     bench) timeout -k 10 300 python -u bench.py --config ${CFG:-c3} --realtime-seconds 0 --capacity-ladder "" --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $? ;;
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o bench \
