@@ -81,7 +81,7 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
                          int ngroups, int fpg, const float* window, const float* ones,
                          const float2* tw, float* partial, float2* scratch, hipStream_t st);
 bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
-bool wf_uses_l32(int logn);  // kernels_waterfall.hip: the N = 16384 kernel in use
+bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_h2 / wf_fft_l32 (not r16)
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st);
@@ -103,8 +103,9 @@ int fc_w_layout_check(int Dp, int cap);    // host self-test of the tiled W layo
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
-                         const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
-                         hipEvent_t mac0, hipEvent_t mac1);
+                         const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
+                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1);
+int fc_kslices_max(int M, int nchains, int Dp, int ncu);  // Y slices a group may need
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
                                 const StepTable& steps, hipStream_t st);
 hipError_t launch_post_long(const ChainPost* posts, ChainCounts* counts, const int* idx,
@@ -1078,7 +1079,9 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     }
     g->nseg = nseg;
     if (g->fc_M) {  // fast-convolution product rows Y[chains][Fs][M]
-        const size_t ny = (size_t)std::max(1, n) * g->fc_Fs * (size_t)g->fc_M;
+        // times the K slices its smallest tile grid may be split into (fc_kslices)
+        const size_t ny = (size_t)std::max(1, n) * g->fc_Fs * (size_t)g->fc_M *
+                          (size_t)fc_kslices_max(g->fc_M, std::max(1, n), g->fc_Dp, e->cus_a);
         if (ny > g->fc_y_elems) {
             RCCHK(drain_all(e));
             dfree(g->d_fc_y);
@@ -1725,7 +1728,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, blk_end, g->d_chains, g->d_fc_w,
                                  g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
                                  g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
-                                 g->d_fc_y, g->d_partial[si], e->sA, tm ? S.m0 : nullptr,
+                                 g->d_fc_y, (int64_t)g->fc_y_elems, g->d_partial[si], e->sA,
+                                 tm ? S.m0 : nullptr,
                                  tm ? S.m1 : nullptr));
             if (tm) {
                 // algorithmic work of that GEMM: 8 flop per complex MAC over the frames that

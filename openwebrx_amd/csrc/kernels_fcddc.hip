@@ -198,6 +198,7 @@ fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64
 // component s of that float4), the same permutation on both operands.  W of chain slot c at
 // W + c * w_cs + kappa * w_ks.
 constexpr int kFcKSplit = 4;
+constexpr int kFcMaxKSlices = 16;  // K slices across workgroups (fc_kslices): Y holds this many
 // Three waves per SIMD (<= 168 registers): C3's 2^20-sample blocks launch M x 4 = 512
 // workgroups, one more round than stream A's 240 CUs hold at two (480)
 template <int FTT, int CTT, bool NT>
@@ -362,7 +363,7 @@ template <int FTT, int CTT, int NR>
 __global__ void __launch_bounds__(64 * kFcKSplit)
 fc_mac_lds(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs, int64_t w_ks,
            int nchains, int Fs, int F, int Dp, int M, int ncg, int chain_fastest,
-           float2* __restrict__ Y) {
+           float2* __restrict__ Y, int ks, int64_t y_slice) {
     constexpr int P = CTT / 2 + FTT;  // DMA instructions per K-block
     constexpr int kSlot = P * 1024;
     constexpr int kRing = NR * kSlot;
@@ -370,7 +371,14 @@ fc_mac_lds(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w
     constexpr int kLds = kFcKSplit * kRing > kRed ? kFcKSplit * kRing : kRed;
     static_assert((NR - 1) * P <= 63, "vmcnt holds 6 bits");
     __shared__ __attribute__((aligned(1024))) char lds[kLds];
-    const int w = blockIdx.x;
+    // K slices across workgroups (ks > 1: grids too small to fill the chip, e.g. C4's per-GPU
+    // share of 128 chains): slice sl of tile w holds K-blocks [sl KB / ks, (sl + 1) KB / ks) and
+    // writes its partial Y to Y + sl y_slice; fc_out sums the slices in slice order.  The tile
+    // count is a multiple of 8, so a tile's slices share its XCD (and its U tile in L2).
+    const int tiles = M * ncg * (int)(gridDim.x / (unsigned)(M * ncg * ks));
+    const int sl = blockIdx.x / tiles;
+    const int w = blockIdx.x - sl * tiles;
+    Y += sl * y_slice;
     const int xcd = w & 7;
     const int q = w >> 3;
     const int mper = M >> 3;
@@ -392,8 +400,8 @@ fc_mac_lds(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w
     const int col = lane & 15;
     const int cc = col >> 1;
     const bool bim = col & 1;
-    const int nkb = (Dp >> 3) / kFcKSplit;
-    const int kb0 = wave * nkb;
+    const int nkb = (Dp >> 3) / (kFcKSplit * ks);
+    const int kb0 = (sl * kFcKSplit + wave) * nkb;
     char* ring = lds + wave * kRing;
 
     // DMA sources (per lane): W instruction i covers tiles 2i, 2i + 1 (lanes 0-31, 32-63), lane
@@ -552,7 +560,7 @@ template <int M>
 __global__ void __launch_bounds__(256)
 fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nchains, int Fs,
        int F, int V, int D, int64_t k_begin, int nk, const float2* __restrict__ tw,
-       float2* __restrict__ out) {
+       float2* __restrict__ out, int ks, int64_t y_slice) {
     using FM = FcM<M>;
     constexpr int RW = FM::R3 ? 3072 / M : 1024 / M;
     constexpr int RS = FM::RS;
@@ -567,7 +575,12 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
         float2 v = make_float2(0.0f, 0.0f);
         if (row < nrows) {
             const int c = row / F, f = row % F;
-            v = Y[((int64_t)c * Fs + f) * M + kap];
+            const float2* y = Y + ((int64_t)c * Fs + f) * M + kap;
+            v = y[0];
+            for (int sl = 1; sl < ks; ++sl) {  // K slices in slice order (fixed)
+                const float2 u = y[sl * y_slice];
+                v = make_float2(v.x + u.x, v.y + u.y);
+            }
         }
         sm[rr * RS + FM::tpos(kap)] = make_float2(v.x, -v.y);
     }
@@ -589,6 +602,34 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
 }
 
 // ---- host launchers ----------------------------------------------------------------------
+
+// K slices across workgroups for a tile grid of `tiles` workgroups: 1 when the tiles alone give
+// every CU of the chip three or more workgroups; otherwise the smallest count that does (each
+// wave of a slice must keep a whole number of the Dp / 8 K-blocks), at most kFcMaxKSlices.
+// OWRX_FC_KSLICES=n forces n (A/B; 1 = the unsliced form).
+int fc_kslices(int tiles, int Dp, int ncu) {
+    static const int forced = [] {
+        const char* v = getenv("OWRX_FC_KSLICES");
+        return v ? atoi(v) : 0;
+    }();
+    const int per_wave = (Dp >> 3) / kFcKSplit;  // K-blocks per wave, unsliced
+    auto ok = [&](int k) { return k >= 1 && k <= kFcMaxKSlices && per_wave % k == 0; };
+    if (forced > 0) return ok(forced) ? forced : 1;
+    if (tiles >= 3 * ncu) return 1;
+    int best = 1;
+    for (int k = 2; k <= kFcMaxKSlices; ++k) {
+        if (!ok(k)) continue;
+        best = k;
+        if (tiles * k >= 3 * ncu) break;
+    }
+    return best;
+}
+
+// the most slices a group of nchains may use: its smallest tile grid (64-chain tiles, one frame
+// tile) against the CU count of its stream
+int fc_kslices_max(int M, int nchains, int Dp, int ncu) {
+    return fc_kslices(M * ((nchains + 63) / 64), Dp, ncu);
+}
 
 #define OWRX_FC_SWITCH(m, CALL)          \
     switch (m) {                         \
@@ -615,8 +656,8 @@ hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
-                         const float2* tw, float2* U, float2* Y, float2* out, hipStream_t st,
-                         hipEvent_t mac0, hipEvent_t mac1) {
+                         const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
+                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1) {
     const int F = (nk + V - 1) / V;
     if (F > Fs || nk <= 0 || nchains <= 0) return hipErrorInvalidValue;
     const dim3 gf(Dp / kFcRT, F);
@@ -653,12 +694,18 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
             return 256;
         return n;
     }();
-    const bool ring = lds_ring && (int)gm.x > ncu;
+    // K slices across workgroups where the tile grid leaves CUs idle (fc_kslices)
+    const int64_t y_slice = (int64_t)nchains * Fs * M;
+    int ks = lds_ring ? fc_kslices((int)gm.x, Dp, ncu) : 1;
+    while (ks > 1 && ks * y_slice > y_cap) --ks;  // within the group's Y (fc_kslices_max)
+    while (ks > 1 && ((Dp >> 3) / kFcKSplit) % ks) --ks;
+    const dim3 gk(gm.x * ks);
+    const bool ring = lds_ring && (int)gk.x > ncu;
     if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
     if (ring && wide)
-        hipLaunchKernelGGL((fc_mac_lds<2, 4, 2>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
+        hipLaunchKernelGGL((fc_mac_lds<2, 4, 2>), gk, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y, ks, y_slice);
     else if (ring)
-        hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
+        hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gk, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y, ks, y_slice);
     else if (wide)
         hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     else
@@ -667,7 +714,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
     if (mac1) HIPCHK_RET(hipEventRecord(mac1, st));
     const int rw = (M % 3 == 0) ? 3072 / M : 1024 / M;
     const dim3 go((nchains * F + rw - 1) / rw);
-#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out)
+#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out, ring ? ks : 1, y_slice)
     OWRX_FC_SWITCH(M, OWRX_FC_O)
 #undef OWRX_FC_O
     return hipGetLastError();

@@ -1213,17 +1213,21 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
-// N = 16384: the radix-32 two-exchange kernel (OWRX_WF_KERNEL=r16 keeps the radix-16 one, A/B);
-// 1024 <= N <= 8192: radix 16
-static bool wf_force_r16() {
-    static const bool v = [] {
+// N = 16384: the half-frame kernel wf_fft_h2 (two workgroups per CU); OWRX_WF_KERNEL=l32 keeps
+// the whole-frame radix-32 kernel and =r16 the radix-16 one (A/B); 1024 <= N <= 8192: radix 16
+static int wf_n16k_kernel() {  // 0: h2, 1: l32, 2: r16
+    static const int v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
-        return s && strcmp(s, "r16") == 0;
+        if (s && strcmp(s, "r16") == 0) return 2;
+        if (s && strcmp(s, "l32") == 0) return 1;
+        return 0;
     }();
     return v;
 }
+static bool wf_force_r16() { return wf_n16k_kernel() == 2; }
 
-bool wf_uses_l32(int logn) { return logn == 14 && !wf_force_r16(); }
+bool wf_uses_l32(int logn) { return logn == 14 && wf_n16k_kernel() != 2; }
+bool wf_uses_h2(int logn) { return logn == 14 && wf_n16k_kernel() == 0; }
 
 // N = 32768, 65536: the DIF split onto wf_fft_l32 (OWRX_WF_KERNEL=fourstep: the four-step, A/B)
 bool wf_uses_split(int logn) {
@@ -1262,13 +1266,33 @@ static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const W
     return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, st, QLOG, fpg);
 }
 
+static hipError_t launch_fft_h2(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                int ngroups, const float* window, const float2* tw,
+                                float* partial, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_h2,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)WfH2::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    // runs of 8 groups: blocks 16 q + 8 h + i hold half h of group 8 q + i
+    hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((ngroups + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, st,
+                       blk, blk_start, groups, ngroups, window, tw, partial);
+    return hipGetLastError();
+}
+
 template <int LOGN>
 static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw, float* partial,
                                  hipStream_t st) {
-    if constexpr (LOGN == 14)
+    if constexpr (LOGN == 14) {
+        if (wf_uses_h2(LOGN))
+            return launch_fft_h2(blk, blk_start, groups, ngroups, window, tw, partial, st);
         if (!wf_force_r16())
             return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, st);
+    }
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
 
@@ -1302,7 +1326,8 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st) {
     int logn = 0;
     while ((1 << logn) < N) ++logn;
-    const int qlog = wf_uses_split(logn) ? logn - 14 : 0;
+    // partial rows half- / sub-frame-major: the DIF split's Q = N / 16384, wf_fft_h2's Q = 2
+    const int qlog = wf_uses_split(logn) ? logn - 14 : wf_uses_h2(logn) ? 1 : 0;
     hipLaunchKernelGGL(wf_finalize, dim3((N + 255) / 256, nrows), dim3(256), 0, st, partial,
                        rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out, qlog);
     return hipGetLastError();

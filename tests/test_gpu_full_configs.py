@@ -6,8 +6,9 @@ one C4 GPU's share (61.44 Msps, a 65536-bin waterfall next to 128 mixed chains a
 The int16 waterfall row is FftAdpcm's input (csdr/chain/fft.py:43-45: dB x 100 truncated to
 int16).  The GPU FFT is fp32 and the oracle's is double, so a row value that lands within the
 FFT's rounding of a 0.01 dB truncation boundary can fall on either side: the test requires every
-int16 value within 1 LSB of the oracle's and reports the exact-match fraction
-(gpurun_out/parity_metrics.jsonl).  The ADPCM bytes of the same rows are bit-exact against the
+int16 value within 1 LSB of the oracle's, reports the exact-match fraction
+(gpurun_out/parity_metrics.jsonl), and pins every mismatch to a truncation boundary: the
+oracle's dB x 100 lies within the fp32 error band of an integer (zero mismatches outside it).  The ADPCM bytes of the same rows are bit-exact against the
 oracle's FftAdpcm of the GPU's float rows (the encoder itself is integer work)."""
 import numpy as np
 import pytest
@@ -68,6 +69,19 @@ def _waterfall_full(amd, fs, N, avg_expected, nrows, block, parity_report, name,
     # measured 0.9996-0.9997 at C2 / C4 full averaging (fp32 FFT vs the double oracle at the
     # (short)(dB * 100) truncation boundary); the floor sits just under it so a regression shows
     assert exact > 0.999, exact
+    # Every mismatch must BE such a boundary case: the oracle's value (dB x 100) lies within the
+    # fp32 path's error of an integer (where the truncation flips).  Band = 4 x the largest
+    # float error measured on these rows (in units of 0.01 dB) + 2 ulp of the float32 x 100
+    # product; the count of mismatches outside the band must be 0.
+    v_ref = ref.astype(np.float64) * 100.0
+    dist = np.abs(v_ref - np.round(v_ref))
+    band = 4.0 * err_db * 100.0 + 2.0 * np.spacing(np.abs(v_ref).astype(np.float32)).astype(np.float64)
+    mism = d != 0
+    outside = int(np.count_nonzero(mism & (dist > band)))
+    parity_report(name + "_boundary", mismatches=int(np.count_nonzero(mism)),
+                  band_centi_db=float(4.0 * err_db * 100.0), mismatches_outside_band=outside,
+                  worst_mismatch_distance_centi_db=float(dist[mism].max()) if mism.any() else 0.0)
+    assert outside == 0, outside
     for r in range(nrows):  # the GPU encoder over the GPU rows: bit-exact
         assert ra[r].tobytes() == oracle.fft_adpcm_row(rf[r]), r
     return iq
