@@ -118,8 +118,9 @@ hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, Chain
                              hipStream_t st);
 hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const int* sel, int nsel,
                             hipStream_t st);
+hipError_t launch_signal_block(int64_t* ready, int64_t v, hipStream_t st);
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
-                              int nsel, hipStream_t st);
+                              int nsel, const int64_t* ready, int64_t want, hipStream_t st);
 
 constexpr int kWfMaxFramesPerGroup = 16;  // frames one FFT workgroup sums (N <= kWfLdsMaxN)
 constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
@@ -566,6 +567,7 @@ struct owrx_engine {
     double block_interval_ms = 0;    // running estimate of the interval between block calls
     int64_t stall_ms = 20000;        // the longest any host-side wait blocks before failing
     hipEvent_t evSync = nullptr;     // marker for bounded stream synchronisation
+    int64_t* d_ready = nullptr;      // stream B's last published block + 1 (signal_block)
     bool debug = false;
     int timing = 0;                  // timing events every `timing` blocks (0: off)
     std::vector<GroupWork> work;     // per-block scratch: the groups with outputs
@@ -1796,10 +1798,21 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                                           S.nsel[o][nr], o, dbg, nr, sB));
         if (S.any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, sB));
         HIPCHK(hipEventRecord(S.evF, sB));
-        // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host
-        HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
-        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + S.off[1][0],
-                                  S.nsel[1][0] + S.nsel[1][1], sC));
+        // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host.
+        // With B and C on disjoint CUs the encoder waits for stream B's block in the kernel
+        // (signal_block / wait_block: no cross-stream event between back-to-back encoders);
+        // the unmasked (wide) pair keeps the event (a waiting encoder there could hold CUs its
+        // producer needs).  OWRX_HANDOFF=event keeps the event everywhere (A/B).
+        static const bool handoff = [] {
+            const char* v = getenv("OWRX_HANDOFF");
+            return !(v && strcmp(v, "event") == 0);
+        }();
+        const int nad = S.nsel[1][0] + S.nsel[1][1];
+        const bool in_kernel = handoff && !wide && e->d_ready && nad > 0;
+        if (e->d_ready) HIPCHK(launch_signal_block(e->d_ready, e->block_index + 1, sB));
+        if (!in_kernel) HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
+        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + S.off[1][0], nad,
+                                  in_kernel ? e->d_ready : nullptr, e->block_index + 1, sC));
         if (timed) HIPCHK(hipEventRecord(S.b1, sC));
         // the copies to host go on stream R (behind this block's encoder), so stream C runs
         // encoders back to back: its kernel is the pipeline's longest serial stage
@@ -1969,6 +1982,9 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
     };
     if (create_streams(e) != hipSuccess) return fail("stream");
     if (hipEventCreateWithFlags(&e->evSync, hipEventDisableTiming) != hipSuccess) return fail("event");
+    if (hipMalloc(&e->d_ready, sizeof(int64_t)) != hipSuccess ||
+        hipMemset(e->d_ready, 0, sizeof(int64_t)) != hipSuccess)
+        return fail("hand-off flag");
     for (auto& r : e->rslots) {
         if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
@@ -2054,6 +2070,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamDestroy(st);
     if (e->evSync) hipEventDestroy(e->evSync);
+    if (e->d_ready) hipFree(e->d_ready);
     delete e;
     return OWRX_OK;
 }
