@@ -233,9 +233,11 @@ struct Waterfall {
     float2* d_y4 = nullptr;  // N > 16384: DIF-split sub-frames (fpg frames per group) or the
                              // four-step scratch (one cf32 frame per group)
     float* d_ones = nullptr; // DIF split: the sub-frames' window (the split applied the frame's)
-    int partial_groups = 0;
+    int partial_groups = 0;          // groups d_partial / d_groups hold
     WfGroup* h_groups[kSlots] = {};  // pinned copy sources, per slot of the launching block
     WfRow* h_rows[kSlots] = {};
+    int h_cap[kSlots] = {};          // groups (and rows) each slot's pinned copy sources hold
+    int row_slot_cap[kRowSlots] = {};  // rows each row slot's buffers hold
     float* d_carry[2] = {nullptr, nullptr};
     WfGroup* d_groups = nullptr;
     WfRow* d_rows = nullptr;
@@ -623,6 +625,17 @@ struct owrx_engine {
         void* p;
     };
     std::vector<Retired> pool_retired;
+    // pinned host buffers (waterfall copy sources and row destinations): an exact-size pool,
+    // released by block (stream-A copy sources) or by row slot (stream-R destinations)
+    std::unordered_map<size_t, std::vector<void*>> hpool_free;
+    std::unordered_map<void*, size_t> hpool_size;
+    std::vector<Retired> hpool_retired;
+    struct RowRetired {
+        int64_t row;  // free once row_tail reaches this
+        void* p;
+        bool pinned;
+    };
+    std::vector<RowRetired> row_retired;
     uint8_t* h_up = nullptr;  // pinned staging of those uploads (a ring; wraps after stream A)
     size_t up_cap = 0, up_head = 0;
     // post staging needs of the current chains (kept as chains come and go)
@@ -705,6 +718,46 @@ static void prel(owrx_engine* e, T*& p) {
     p = nullptr;
 }
 
+template <typename T>
+static hipError_t hpalloc(owrx_engine* e, T** p, size_t count) {
+    *p = nullptr;
+    const size_t bytes = (sizeof(T) * std::max<size_t>(count, 1) + 255) & ~(size_t)255;
+    auto it = e->hpool_free.find(bytes);
+    if (it != e->hpool_free.end() && !it->second.empty()) {
+        *p = static_cast<T*>(it->second.back());
+        it->second.pop_back();
+        return hipSuccess;
+    }
+    void* q = nullptr;
+    const hipError_t r = hipHostMalloc(&q, bytes, 0);
+    if (r != hipSuccess) return r;
+    e->hpool_size[q] = bytes;
+    *p = static_cast<T*>(q);
+    return hipSuccess;
+}
+// pinned / device buffers back to their pools: now (nothing can use them), after the blocks
+// enqueued so far drained, or after the row slots enqueued so far drained
+template <typename T>
+static void hprel_now(owrx_engine* e, T*& p) {
+    if (p) e->hpool_free[e->hpool_size[(void*)p]].push_back((void*)p);
+    p = nullptr;
+}
+template <typename T>
+static void prel_now(owrx_engine* e, T*& p) {
+    if (p) e->pool_free[e->pool_size[(void*)p]].push_back((void*)p);
+    p = nullptr;
+}
+template <typename T>
+static void hprel(owrx_engine* e, T*& p) {
+    if (p) e->hpool_retired.push_back({e->block_index, (void*)p});
+    p = nullptr;
+}
+template <typename T>
+static void rowrel(owrx_engine* e, T*& p, bool pinned) {
+    if (p) e->row_retired.push_back({e->row_head, (void*)p, pinned});
+    p = nullptr;
+}
+
 static void pool_collect(owrx_engine* e) {
     size_t k = 0;
     for (const auto& r : e->pool_retired) {
@@ -714,6 +767,27 @@ static void pool_collect(owrx_engine* e) {
             e->pool_retired[k++] = r;
     }
     e->pool_retired.resize(k);
+    k = 0;
+    for (const auto& r : e->hpool_retired) {
+        if (r.block <= e->slot_tail)
+            e->hpool_free[e->hpool_size[r.p]].push_back(r.p);
+        else
+            e->hpool_retired[k++] = r;
+    }
+    e->hpool_retired.resize(k);
+}
+
+static void row_collect(owrx_engine* e) {
+    size_t k = 0;
+    for (const auto& r : e->row_retired) {
+        if (r.row <= e->row_tail) {
+            if (r.pinned) e->hpool_free[e->hpool_size[r.p]].push_back(r.p);
+            else e->pool_free[e->pool_size[r.p]].push_back(r.p);
+        } else {
+            e->row_retired[k++] = r;
+        }
+    }
+    e->row_retired.resize(k);
 }
 
 // n bytes from the host to device memory on stream A, through the pinned upload ring: the
@@ -760,25 +834,28 @@ static void free_chain(owrx_engine* e, Chain* c) {
     prel(e, c->d_sf_tw);
 }
 
-static void free_wf(Waterfall* w) {
-    dfree(w->d_window);
-    dfree(w->d_tw);
-    dfree(w->d_partial);
-    dfree(w->d_y4);
-    dfree(w->d_ones);
-    dfree(w->d_carry[0]);
-    dfree(w->d_carry[1]);
-    dfree(w->d_groups);
-    dfree(w->d_rows);
+// A waterfall's buffers back to the pools without waiting: device buffers read by stream A
+// and the pinned copy sources once the blocks enqueued so far drained, the row-slot buffers
+// (stream R encoders and copies) once the row slots enqueued so far drained.
+static void free_wf(owrx_engine* e, Waterfall* w) {
+    prel(e, w->d_window);
+    prel(e, w->d_tw);
+    prel(e, w->d_partial);
+    prel(e, w->d_y4);
+    prel(e, w->d_ones);
+    prel(e, w->d_carry[0]);
+    prel(e, w->d_carry[1]);
+    prel(e, w->d_groups);
+    prel(e, w->d_rows);
     for (int b = 0; b < kSlots; ++b) {
-        hfree(w->h_groups[b]);
-        hfree(w->h_rows[b]);
+        hprel(e, w->h_groups[b]);
+        hprel(e, w->h_rows[b]);
     }
     for (int s = 0; s < kRowSlots; ++s) {
-        dfree(w->d_s16[s]);
-        dfree(w->d_f32[s]);
-        dfree(w->d_bytes[s]);
-        hfree(w->h_bytes[s]);
+        rowrel(e, w->d_s16[s], false);
+        rowrel(e, w->d_f32[s], false);
+        rowrel(e, w->d_bytes[s], false);
+        rowrel(e, w->h_bytes[s], true);
     }
 }
 
@@ -917,6 +994,7 @@ static int drain_rows(owrx_engine* e, bool block, int keep) {
         r.pending = false;
         e->row_tail++;
     }
+    if (!e->row_retired.empty()) row_collect(e);
     return OWRX_OK;
 }
 
@@ -949,48 +1027,61 @@ static int drain_all(owrx_engine* e) {
     return drain_slots(e, true, 0);
 }
 
-static int wf_alloc_buffers(owrx_engine* e, Waterfall* w) {
-    // capacities derived from the current hop/avg; re-run when they change.  A batched launch
-    // (owrx_waterfall_set_batch) holds at most the frames of the history window plus a block.
-    const int64_t span = w->batch_min > 1 ? e->history + e->max_block : e->max_block;
-    const int64_t frames = span / std::max(1, w->hop) + 2 * kWfMaxFramesPerGroup + 2;
-    const int groups = (int)(frames + 2);  // a group may hold a single frame at row ends
-    const int rows = (int)(frames / std::max(1, w->avg) + 3);
-    if (groups > w->partial_groups || rows > w->rows_cap) RCCHK(drain_all(e));
+// Launch capacity of a waterfall (no drain: reconfiguration and joins run while blocks are in
+// flight).  Buffers only grow, geometrically; a grown stream-A buffer replaces the old one for
+// launches from now on and the old one returns to the pool once the blocks that used it
+// drained.  The pinned copy sources of slot bp and the buffers of row slot ri are idle when a
+// launch stages into them (their previous users drained), so they are swapped at once.
+static int wf_reserve(owrx_engine* e, Waterfall* w, int groups, int rows, int bp, int ri) {
+    groups = std::max(groups, 1);
+    rows = std::max(rows, 1);
     if (groups > w->partial_groups) {
-        dfree(w->d_partial);
-        dfree(w->d_groups);
-        dfree(w->d_y4);
-        HIPCHK(dalloc(&w->d_partial, (size_t)groups * w->N));
+        const int cap = std::max(groups, w->partial_groups + w->partial_groups / 2);
+        prel(e, w->d_partial);
+        prel(e, w->d_groups);
+        prel(e, w->d_y4);
+        HIPCHK(palloc(e, &w->d_partial, (size_t)cap * w->N));
+        HIPCHK(palloc(e, &w->d_groups, (size_t)cap));
         if (w->N > kWfLdsMaxN)
-            HIPCHK(dalloc(&w->d_y4, (size_t)groups * w->N * (wf_uses_split(w->logn) ? kWfSplitMaxFpg : 1)));
-        HIPCHK(dalloc(&w->d_groups, (size_t)groups));
-        for (int b = 0; b < kSlots; ++b) {
-            hfree(w->h_groups[b]);
-            HIPCHK(halloc(&w->h_groups[b], (size_t)groups));
-        }
-        w->partial_groups = groups;
+            HIPCHK(palloc(e, &w->d_y4, (size_t)cap * w->N * (wf_uses_split(w->logn) ? kWfSplitMaxFpg : 1)));
+        w->partial_groups = cap;
     }
-    if (rows > w->rows_cap) {
-        dfree(w->d_rows);
-        HIPCHK(dalloc(&w->d_rows, (size_t)rows + 1));
-        for (int b = 0; b < kSlots; ++b) {
-            hfree(w->h_rows[b]);
-            HIPCHK(halloc(&w->h_rows[b], (size_t)rows + 1));
-        }
-        for (int s = 0; s < kRowSlots; ++s) {
-            dfree(w->d_s16[s]);
-            dfree(w->d_f32[s]);
-            dfree(w->d_bytes[s]);
-            hfree(w->h_bytes[s]);
-            HIPCHK(dalloc(&w->d_s16[s], (size_t)rows * w->N));
-            HIPCHK(dalloc(&w->d_f32[s], (size_t)rows * w->N));
-            HIPCHK(dalloc(&w->d_bytes[s], (size_t)rows * 4 * w->N));
-            HIPCHK(halloc(&w->h_bytes[s], (size_t)rows * 4 * w->N));
-        }
-        w->rows_cap = rows;
+    if (rows + 1 > w->rows_cap) {
+        const int cap = std::max(rows + 1, w->rows_cap + w->rows_cap / 2);
+        prel(e, w->d_rows);
+        HIPCHK(palloc(e, &w->d_rows, (size_t)cap));
+        w->rows_cap = cap;
+    }
+    if (bp >= 0 && std::max(groups, rows + 1) > w->h_cap[bp]) {
+        const int cap = std::max(w->partial_groups, w->rows_cap);
+        hprel_now(e, w->h_groups[bp]);
+        hprel_now(e, w->h_rows[bp]);
+        HIPCHK(hpalloc(e, &w->h_groups[bp], (size_t)cap));
+        HIPCHK(hpalloc(e, &w->h_rows[bp], (size_t)cap));
+        w->h_cap[bp] = cap;
+    }
+    if (ri >= 0 && rows > w->row_slot_cap[ri]) {
+        const int cap = std::max(rows, w->row_slot_cap[ri] + w->row_slot_cap[ri] / 2);
+        prel_now(e, w->d_s16[ri]);
+        prel_now(e, w->d_f32[ri]);
+        prel_now(e, w->d_bytes[ri]);
+        hprel_now(e, w->h_bytes[ri]);
+        HIPCHK(palloc(e, &w->d_s16[ri], (size_t)cap * w->N));
+        HIPCHK(palloc(e, &w->d_f32[ri], (size_t)cap * w->N));
+        HIPCHK(palloc(e, &w->d_bytes[ri], (size_t)cap * 4 * w->N));
+        HIPCHK(hpalloc(e, &w->h_bytes[ri], (size_t)cap * 4 * w->N));
+        w->row_slot_cap[ri] = cap;
     }
     return OWRX_OK;
+}
+
+// the launch sizes a waterfall expects (its first launches then allocate nothing)
+static int wf_initial_reserve(owrx_engine* e, Waterfall* w) {
+    const int64_t span = w->batch_min > 1 ? e->history + e->max_block : e->max_block;
+    const int64_t frames = span / std::max(1, w->hop) + 2;
+    const int groups = (int)(frames / std::max(1, w->fpg) + frames / std::max(1, w->avg) + 4);
+    const int rows = (int)(frames / std::max(1, w->avg) + 3);
+    return wf_reserve(e, w, groups, rows, -1, -1);
 }
 
 static int ensure_post_capacity(owrx_engine* e) {
@@ -1208,6 +1299,15 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         if (ready < w->batch_min && lag < max_lag && !leaving && !late) return OWRX_OK;
     }
     w->pend_t[ri].clear();
+    {
+        // capacity for every frame ready now (groups: at most one per fpg frames plus one short
+        // group per row end; rows: one per avg frames plus a partial one)
+        const int bp = (int)(e->block_index % e->nslots);
+        const int64_t ready = (blk_end - w->N - w->next_start) / std::max(1, w->hop) + 1;
+        const int64_t avg_min = std::max(1, std::min(w->avg, w->pending ? w->new_avg : w->avg));
+        const int64_t rows = ready / avg_min + 2;
+        RCCHK(wf_reserve(e, w, (int)(ready / std::max(1, w->fpg) + rows + 2), (int)rows, bp, ri));
+    }
     int cur_row_first_group = 0;
     bool row_open = false;
     const int adpcm_now = w->adpcm;
@@ -1252,7 +1352,9 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
                 w->pending = false;
                 break;
             }
-            if ((int)w->rowdesc.size() + 1 >= w->rows_cap) break;
+            if ((int)w->rowdesc.size() + 1 >= w->rows_cap ||
+                (int)w->rowdesc.size() >= w->row_slot_cap[ri])
+                break;
         }
     }
     const int ncomplete = (int)w->rowdesc.size();
@@ -2036,7 +2138,7 @@ int owrx_engine_destroy(owrx_engine* e) {
         if (r.stream && e->evSync && sync_stream(e, r.stream) == OWRX_ETIMEDOUT) stuck = true;
     if (stuck) return OWRX_ETIMEDOUT;
     for (auto& kv : e->chains) free_chain(e, kv.second.get());
-    for (auto& kv : e->wfs) free_wf(kv.second.get());
+    for (auto& kv : e->wfs) free_wf(e, kv.second.get());
     for (auto& g : e->groups) {
         dfree(g->d_taps);
         dfree(g->d_h);
@@ -2049,6 +2151,7 @@ int owrx_engine_destroy(owrx_engine* e) {
         for (auto& h : g->h_chains) hfree(h);
     }
     for (auto& kv : e->pool_size) hipFree(kv.first);  // the pool's buffers, in use or not
+    for (auto& kv : e->hpool_size) hipHostFree(kv.first);
     hfree(e->h_up);
     dfree(e->d_ring);
     dfree(e->d_cs16);
@@ -2269,7 +2372,9 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
         set_last_error("owrx_waterfall_create: hop too large for engine history");
         return OWRX_EINVAL;
     }
-    RC_FAIL(e, drain_all(e));
+    // no drain: the new FftChain's buffers come from the pools and its tables are uploaded on
+    // stream A behind the blocks in flight (SpectrumThread restarts on an fft_size change,
+    // owrx/fft.py:89-91, while every client keeps streaming)
     auto w = std::make_unique<Waterfall>();
     w->N = fft_size;
     w->logn = logn;
@@ -2281,20 +2386,24 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
     w->fpg = wf_frames_per_group(e, w.get());
     std::vector<float> win = hamming_window(fft_size);
     std::vector<float> tw = fft_twiddles(fft_size);
-    HIPCHK(dalloc(&w->d_window, (size_t)fft_size));
-    HIPCHK(dalloc(&w->d_tw, (size_t)fft_size));
-    HIPCHK(dalloc(&w->d_carry[0], (size_t)fft_size));
-    HIPCHK(dalloc(&w->d_carry[1], (size_t)fft_size));
-    HIPCHK(hipMemcpy(w->d_window, win.data(), sizeof(float) * fft_size, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(w->d_tw, tw.data(), sizeof(float) * 2 * fft_size, hipMemcpyHostToDevice));
-    if (fft_size > kWfLdsMaxN) {
-        const std::vector<float> ones(kWfLdsMaxN, 1.0f);
-        HIPCHK(dalloc(&w->d_ones, (size_t)kWfLdsMaxN));
-        HIPCHK(hipMemcpy(w->d_ones, ones.data(), sizeof(float) * kWfLdsMaxN, hipMemcpyHostToDevice));
-    }
-    int rc = wf_alloc_buffers(e, w.get());
+    int rc = OWRX_OK;
+    auto setup = [&]() -> int {
+        HIPCHK(palloc(e, &w->d_window, (size_t)fft_size));
+        HIPCHK(palloc(e, &w->d_tw, (size_t)fft_size));
+        HIPCHK(palloc(e, &w->d_carry[0], (size_t)fft_size));
+        HIPCHK(palloc(e, &w->d_carry[1], (size_t)fft_size));
+        RCCHK(upload(e, w->d_window, win.data(), sizeof(float) * fft_size));
+        RCCHK(upload(e, w->d_tw, tw.data(), sizeof(float) * 2 * fft_size));
+        if (fft_size > kWfLdsMaxN) {
+            const std::vector<float> ones(kWfLdsMaxN, 1.0f);
+            HIPCHK(palloc(e, &w->d_ones, (size_t)kWfLdsMaxN));
+            RCCHK(upload(e, w->d_ones, ones.data(), sizeof(float) * kWfLdsMaxN));
+        }
+        return wf_initial_reserve(e, w.get());
+    };
+    rc = setup();
     if (rc) {
-        free_wf(w.get());
+        free_wf(e, w.get());
         return rc;
     }
     const int h = e->next_handle++;
@@ -2310,7 +2419,8 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
     if (it == e->wfs.end() || every_n_samples <= 0 || avg_number < 0) return OWRX_EINVAL;
     Waterfall* w = it->second.get();
     if ((int64_t)every_n_samples + w->N > e->history) return OWRX_EINVAL;
-    RC_FAIL(e, drain_all(e));
+    // no drain: the new settings apply at the next row boundary (process_waterfall), blocks in
+    // flight keep theirs, and launch buffers grow when a launch needs them (wf_reserve)
     w->new_hop = every_n_samples;
     w->new_avg = std::max(1, avg_number);
     w->new_adpcm = adpcm ? 1 : 0;
@@ -2323,7 +2433,6 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
     } else {
         w->pending = true;
     }
-    RC_FAIL(e, wf_alloc_buffers(e, w));  // sized for the larger of old/new settings
     return OWRX_OK;
 }
 
@@ -2332,26 +2441,16 @@ int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t
     auto it = e->wfs.find(handle);
     if (it == e->wfs.end() || max_lag < 0) return OWRX_EINVAL;
     Waterfall* w = it->second.get();
-    // pending frames first (they were grouped under the old rule), at a row boundary only: the
-    // group size may change with the batch, and rows must not mix two group sizes
-    if (e->last_blk) RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr));
-    RC_FAIL(e, drain_all(e));
-    if (w->row_frame != 0 || w->carry_valid) {
-        set_last_error("owrx_waterfall_set_batch: only between rows (set it before the stream starts)");
-        return OWRX_EINVAL;
-    }
-    const int old_min = w->batch_min, old_fpg = w->fpg;
-    w->batch_min = std::max(0, min_frames);
-    w->batch_lag = max_lag;
-    w->fpg = wf_frames_per_group(e, w);
+    // the launch rule only: the groups (frames summed per workgroup) do not depend on it, so it
+    // applies at once, mid-row and mid-stream, without a drain
+    const int bmin = std::max(0, min_frames);
     // a deferred group must still fit the next block's window when its first frame leaves
-    if (w->batch_min > 1 && e->history < 2 * ((int64_t)w->fpg + 1) * w->hop + 2 * (int64_t)w->N) {
-        w->batch_min = old_min;
-        w->fpg = old_fpg;
+    if (bmin > 1 && e->history < 2 * ((int64_t)w->fpg + 1) * w->hop + 2 * (int64_t)w->N) {
         set_last_error("owrx_waterfall_set_batch: engine history too short to batch (owrx_engine_create_ex)");
         return OWRX_EINVAL;
     }
-    RC_FAIL(e, wf_alloc_buffers(e, w));
+    w->batch_min = bmin;
+    w->batch_lag = max_lag;
     return OWRX_OK;
 }
 
@@ -2367,8 +2466,9 @@ int owrx_waterfall_destroy(owrx_engine* e, int handle) {
     ENGINE_GUARD(e);
     auto it = e->wfs.find(handle);
     if (it == e->wfs.end()) return OWRX_EINVAL;
-    RC_FAIL(e, drain_all(e));
-    free_wf(it->second.get());
+    // no drain: rows of it still in flight are dropped when their slot drains (drain_rows only
+    // visits live waterfalls) and its buffers return to the pools once nothing can use them
+    free_wf(e, it->second.get());
     e->wfs.erase(it);
     return OWRX_OK;
 }

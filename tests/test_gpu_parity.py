@@ -268,6 +268,77 @@ def test_waterfall_batched_launches(amd):
     assert st2["waterfall_samples"] == st2["waterfall_frames"] * hop
 
 
+def test_waterfall_reconfigure_without_drain(amd):
+    """SpectrumThread's live settings on a running engine (owrx/fft.py:49-56: fft_fps ->
+    FftChain.setFps, fft_voverlap_factor -> setVOverlapFactor, both re-deriving the averaging
+    and the block size, csdr/chain/fft.py:57-85) with a chain streaming beside the waterfall: an
+    fps change and then an overlap change mid-row, mid-stream.  Rows before each switch row
+    equal the oracle's under the old settings, rows after it the oracle's under the new ones
+    from the switch frame on; a second FftChain is created and destroyed mid-stream; no call
+    drains the pipeline (pipeline_drains unchanged until the final sync)."""
+    from openwebrx_amd import synth
+    fs, N, B = 2400000, 4096, 1 << 16
+    fft = amd.params.fft_parameters
+    settings = [fft(fs, N, 9, 0.3), fft(fs, N, 25, 0.3), fft(fs, N, 25, 0.6)]  # (avg, hop)
+    rows_each = [4, 5, 4]
+    n = sum(a * h * (r + 1) for (a, h), r in zip(settings, rows_each)) + N
+    iq, offs = synth.make_iq(fs, n, ["nfm"])
+    eng = amd.Engine(fs, max_block=B)
+    ch = eng.chain(amd.params.chain_params(fs, offs[0], "nfm"))
+    avg, hop = settings[0]
+    wf = eng.waterfall(N, hop, avg, adpcm=False)
+    d0 = None
+    switches = []  # (frames before the switch row's end, settings index)
+    frames_done, row_frames, cur = 0, 0, 0
+    # push block by block; switch settings once the current setting has produced rows_each rows
+    # plus half a row (mid-row), tracking the engine's frame schedule to know the switch row
+    pos, extra = 0, None
+    while pos < n:
+        m = min(B, n - pos)
+        eng.push(iq[pos:pos + m])
+        pos += m
+        if d0 is None:
+            d0 = eng.stats()["pipeline_drains"]
+        if pos > n // 3 and extra is None:
+            extra = eng.waterfall(2048, 1000, 3, adpcm=True)  # a second FftChain joins ...
+        if pos > n // 2 and extra is not None and extra is not False:
+            extra.close()                                   # ... and leaves mid-stream
+            extra = False
+        if cur + 1 < len(settings):
+            a, h = settings[cur]
+            start = sum(s for s, _ in switches)  # sample where the current setting began
+            launched = (pos - start - N) // h + 1 if pos - start >= N else 0
+            if launched >= a * rows_each[cur] + a // 2:
+                # applies at the end of the row in progress
+                r_cur = launched // a + (1 if launched % a else 0)
+                switches.append((start + r_cur * a * h - start, cur))
+                cur += 1
+                wf.set(settings[cur][1], settings[cur][0], False)
+    assert eng.stats()["pipeline_drains"] == d0, "a waterfall change drained the pipeline"
+    assert cur == len(settings) - 1
+    eng.sync()
+    rows = wf.read_rows()
+    assert ch.read_audio()  # the chain streamed throughout
+    eng.close()
+    # oracle: each setting from its start sample
+    refs, start = [], 0
+    bounds = [s for s, _ in switches] + [None]
+    for k, (a, h) in enumerate(settings):
+        span = bounds[k]
+        seg = iq[start:] if span is None else iq[start:start + span + N - h]
+        r = oracle.waterfall_rows(seg, N, h, a)
+        if span is not None:
+            r = r[:span // (a * h)]
+        refs.extend(oracle.fftswap(x) for x in r)
+        if span is not None:
+            start += span
+    ref = np.stack(refs)
+    assert rows.shape[0] >= ref.shape[0] - 1 and rows.shape[0] <= ref.shape[0], (rows.shape, ref.shape)
+    k = rows.shape[0]
+    err = np.max(np.abs(rows[:k] - ref[:k]))
+    assert err < 2e-3, err
+
+
 def test_input_retention_same_outputs(amd):
     """owrx_set_input_retention: with a resident recording the host runs up to r blocks ahead of
     stream A (no wait for block k - 1 before returning); audio, s-meter and waterfall rows are
