@@ -1014,10 +1014,23 @@ typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 // kHandoffTimeout it gives up (the host's bounded wait then reports the stall).
 constexpr uint64_t kHandoffTimeout = 1000000000ull;  // 10 s of the 100 MHz real-time counter
 
+// the current value of *p through a returning atomic add of 0 (resolved at the memory side,
+// where every XCD's writes meet); inline, so no pass turns the idempotent add into a load
+OWRX_DEV int64_t atomic_peek(const int64_t* p) {
+    int64_t v;
+    const int64_t zero = 0;
+    asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)"
+                 : "=&v"(v) : "v"(p), "v"(zero) : "memory");
+    return v;
+}
+
 OWRX_DEV void wait_block(const int64_t* ready, int64_t want) {
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        // a returning atomic per poll: resolved where every XCD sees the latest value (a plain
+        // or sc1 load can keep hitting a stale copy of the line in this XCD's L2 while the chip
+        // is idle -- measured: one encoder spun to its timeout)
+        while (atomic_peek(ready) < want) {
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > kHandoffTimeout) break;
         }
@@ -1033,7 +1046,7 @@ __global__ void __launch_bounds__(64) signal_block(int64_t* ready, int64_t v) {
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(ready, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(ready, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

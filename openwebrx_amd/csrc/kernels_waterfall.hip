@@ -1213,14 +1213,15 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
-// N = 16384: the half-frame kernel wf_fft_h2 (two workgroups per CU); OWRX_WF_KERNEL=l32 keeps
-// the whole-frame radix-32 kernel and =r16 the radix-16 one (A/B); 1024 <= N <= 8192: radix 16
+// N = 16384: the whole-frame radix-32 kernel wf_fft_l32; OWRX_WF_KERNEL=h2 the half-frame kernel
+// (two workgroups per CU: 68 vs 50 us per 960 C3 frames from HBM, its loads exposed) and =r16
+// the radix-16 one (A/B); 1024 <= N <= 8192: radix 16
 static int wf_n16k_kernel() {  // 0: h2, 1: l32, 2: r16
     static const int v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
         if (s && strcmp(s, "r16") == 0) return 2;
-        if (s && strcmp(s, "l32") == 0) return 1;
-        return 0;
+        if (s && strcmp(s, "h2") == 0) return 0;
+        return 1;
     }();
     return v;
 }
