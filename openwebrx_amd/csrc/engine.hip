@@ -17,6 +17,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <deque>
@@ -178,6 +181,78 @@ static void hfree(T*& p) {
     if (p) hipHostFree((void*)p);
     p = nullptr;
 }
+
+// Host worker pool for the per-chain loops that run every block (moving each chain's outputs
+// into its ring, the batched reads): at tens of thousands of chains one host thread spent tens
+// of milliseconds per block there (the real-time capacity was host-bound).  Chains are
+// independent, so ranges of them go to the workers; below kParMin items the caller's thread
+// does the loop alone.
+class HostPool {
+  public:
+    explicit HostPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { worker(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // fn(begin, end) over [0, n) in chunks of `chunk`, the caller's thread taking part
+    void run(int64_t n, int64_t chunk, const std::function<void(int64_t, int64_t)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            fn_ = &fn;
+            n_ = n;
+            chunk_ = std::max<int64_t>(1, chunk);
+            next_.store(0);
+            busy_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void work() {
+        for (;;) {
+            const int64_t b = next_.fetch_add(chunk_);
+            if (b >= n_) return;
+            (*fn_)(b, std::min(n_, b + chunk_));
+        }
+    }
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (--busy_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int64_t, int64_t)>* fn_ = nullptr;
+    std::atomic<int64_t> next_{0};
+    int64_t n_ = 0, chunk_ = 1;
+    int busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+constexpr int64_t kParMin = 2048;  // per-chain loops shorter than this stay on one thread
 
 struct ByteRing {  // host-side output queue
     std::vector<uint8_t> buf;
@@ -570,6 +645,7 @@ struct owrx_engine {
     int64_t stall_ms = 20000;        // the longest any host-side wait blocks before failing
     hipEvent_t evSync = nullptr;     // marker for bounded stream synchronisation
     int64_t* d_ready = nullptr;      // stream B's last published block + 1 (signal_block)
+    std::unique_ptr<HostPool> pool;  // host workers for per-chain loops (created on first use)
     bool debug = false;
     int timing = 0;                  // timing events every `timing` blocks (0: off)
     std::vector<GroupWork> work;     // per-block scratch: the groups with outputs
@@ -651,6 +727,9 @@ static double now_ms() {
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// fn(begin, end) over [0, n): on the engine's host workers when n is large, else inline
+static void for_range(owrx_engine* e, int64_t n, const std::function<void(int64_t, int64_t)>& fn);
+
 // Bounded waits.  The reference turns a source that stops producing into fail() -> every
 // client's onFail (owrx/source/__init__.py:432-448, owrx/connection.py:292-295); here a GPU
 // that stops completing work must do the same instead of blocking the OpenWebRX process in a
@@ -678,6 +757,21 @@ static int wait_ev(owrx_engine* e, hipEvent_t ev) {
     }
     HIPCHK(q);
     return OWRX_OK;
+}
+
+static void for_range(owrx_engine* e, int64_t n, const std::function<void(int64_t, int64_t)>& fn) {
+    if (n < kParMin) {
+        fn(0, n);
+        return;
+    }
+    if (!e->pool) {
+        const unsigned hw = std::thread::hardware_concurrency();
+        // OWRX_HOST_THREADS: workers besides the caller (default: up to 7, fewer on small hosts)
+        int nt = (int)std::min(7u, hw > 1 ? hw - 1 : 1u);
+        if (const char* v = getenv("OWRX_HOST_THREADS")) nt = std::max(0, atoi(v));
+        e->pool = std::make_unique<HostPool>(nt);
+    }
+    e->pool->run(n, 1024, fn);
 }
 
 // everything enqueued on `st` so far, within the stall bound
@@ -892,18 +986,23 @@ static int drain_slot(owrx_engine* e, int si) {
             s.timed = false;
             s.timed_mac = false;
         }
-        for (size_t k = 0; k < s.post_ids.size(); ++k) {
+        // each chain's outputs into its rings: chains are independent, so ranges of them on
+        // the host workers; the counters are summed per range
+        std::atomic<int64_t> ov{0}, ab{0}, dd{0};
+        for_range(e, (int64_t)s.post_ids.size(), [&](int64_t k0, int64_t k1) {
+        int64_t overruns = 0, audio_bytes = 0, ddc_outputs = 0;
+        for (int64_t k = k0; k < k1; ++k) {
             auto it = e->chains.find(s.post_ids[k]);
             if (it == e->chains.end()) continue;
             Chain* c = it->second.get();
             const ChainCounts& cc = s.h_counts[k];
             const PostLayout& L = s.layout[k];  // as this block was built
             const int64_t nb = std::min<int64_t>(cc.out_bytes, L.out_cap);
-            if (cc.out_bytes > L.out_cap) e->stats.overruns++;
+            if (cc.out_bytes > L.out_cap) overruns++;
             c->audio.push(s.h_out + s.out_off[k], (size_t)nb);
             if (cc.sf_bytes > 0 && L.sf_gen == c->sf_gen) {
                 const int64_t sb = std::min<int64_t>(cc.sf_bytes, L.sf_cap);
-                if (cc.sf_bytes > L.sf_cap) e->stats.overruns++;
+                if (cc.sf_bytes > L.sf_cap) overruns++;
                 c->sfft.push(s.h_out + s.out_off[k] + out_region(L.out_cap), (size_t)sb);
             }
             if (L.tsq_cap + L.tagc_cap > 0 && L.tap_gen == c->tap_gen) {
@@ -911,17 +1010,17 @@ static int drain_slot(owrx_engine* e, int si) {
                                     out_region(L.sf_cap);
                 if (L.tsq_cap > 0) {
                     const int64_t b = std::min<int64_t>(8 * cc.n_gate, L.tsq_cap);
-                    if (8 * cc.n_gate > L.tsq_cap) e->stats.overruns++;
+                    if (8 * cc.n_gate > L.tsq_cap) overruns++;
                     c->tap_sel.push(tb, (size_t)b);
                 }
                 if (L.tagc_cap > 0) {
                     const int64_t b = std::min<int64_t>(4 * cc.n_front, L.tagc_cap);
-                    if (4 * cc.n_front > L.tagc_cap) e->stats.overruns++;
+                    if (4 * cc.n_front > L.tagc_cap) overruns++;
                     c->tap_audio.push(tb + out_region(L.tsq_cap), (size_t)b);
                 }
             }
-            e->stats.audio_bytes += nb;
-            e->stats.ddc_outputs += cc.n_ddc;
+            audio_bytes += nb;
+            ddc_outputs += cc.n_ddc;
             c->smeter.push((const uint8_t*)(s.h_sm + (int64_t)k * e->sm_stride),
                            sizeof(float) * (size_t)std::min<int64_t>(cc.smeter, e->sm_stride));
             if (s.debug && s.h_dbg) {
@@ -935,6 +1034,13 @@ static int drain_slot(owrx_engine* e, int si) {
                 }
             }
         }
+        ov += overruns;
+        ab += audio_bytes;
+        dd += ddc_outputs;
+        });
+        e->stats.overruns += ov.load();
+        e->stats.audio_bytes += ab.load();
+        e->stats.ddc_outputs += dd.load();
     } else if (s.timed) {
         float ms = 0;
         RCCHK(wait_ev(e, s.a3));
@@ -2813,13 +2919,29 @@ int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_
                                int64_t max_bytes, int64_t* lens) {
     ENGINE_GUARD(e);
     if (n < 0 || (n > 0 && (!handles || !dst || !lens)) || max_bytes < 0) return OWRX_EINVAL;
+    // sizes first (each chain's ring, on the host workers), offsets (in order, up to max_bytes),
+    // then the copies (workers again)
+    std::vector<Chain*> cs((size_t)n);
+    std::atomic<bool> bad{false};
+    for_range(e, n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            auto it = e->chains.find(handles[i]);
+            if (it == e->chains.end()) { bad = true; continue; }
+            cs[i] = it->second.get();
+            lens[i] = (int64_t)cs[i]->audio.avail();
+        }
+    });
+    if (bad) return OWRX_EINVAL;
+    std::vector<int64_t> offs((size_t)n);
     int64_t off = 0;
     for (int i = 0; i < n; ++i) {
-        auto it = e->chains.find(handles[i]);
-        if (it == e->chains.end()) return OWRX_EINVAL;
-        lens[i] = (int64_t)it->second->audio.pop(dst + off, (size_t)(max_bytes - off));
+        lens[i] = std::min(lens[i], max_bytes - off);
+        offs[i] = off;
         off += lens[i];
     }
+    for_range(e, n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) cs[i]->audio.pop(dst + offs[i], (size_t)lens[i]);
+    });
     return off;
 }
 
@@ -2827,15 +2949,28 @@ int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float
                                 int64_t max_values, int64_t* counts) {
     ENGINE_GUARD(e);
     if (n < 0 || (n > 0 && (!handles || !dst || !counts)) || max_values < 0) return OWRX_EINVAL;
+    std::vector<Chain*> cs((size_t)n);
+    std::atomic<bool> bad{false};
+    for_range(e, n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            auto it = e->chains.find(handles[i]);
+            if (it == e->chains.end()) { bad = true; continue; }
+            cs[i] = it->second.get();
+            counts[i] = (int64_t)(cs[i]->smeter.avail() / sizeof(float));
+        }
+    });
+    if (bad) return OWRX_EINVAL;
+    std::vector<int64_t> offs((size_t)n);
     int64_t off = 0;
     for (int i = 0; i < n; ++i) {
-        auto it = e->chains.find(handles[i]);
-        if (it == e->chains.end()) return OWRX_EINVAL;
-        counts[i] = (int64_t)(it->second->smeter.pop((uint8_t*)(dst + off),
-                                                     sizeof(float) * (size_t)(max_values - off)) /
-                              sizeof(float));
+        counts[i] = std::min(counts[i], max_values - off);
+        offs[i] = off;
         off += counts[i];
     }
+    for_range(e, n, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i)
+            cs[i]->smeter.pop((uint8_t*)(dst + offs[i]), sizeof(float) * (size_t)counts[i]);
+    });
     return off;
 }
 

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <functional>
 #include <string>
 #include <vector>
@@ -79,7 +80,7 @@ static bool flush_on() {
     static const bool v = !getenv("OWRX_WF_FLUSH") || atoi(getenv("OWRX_WF_FLUSH"));
     return v;
 }
-static double time_us(const std::function<void()>& launch) {
+static double time_us(const std::function<void()>& launch, hipStream_t stream = 0) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -94,10 +95,11 @@ static double time_us(const std::function<void()>& launch) {
         if (flush_on())
             hipLaunchKernelGGL(flush_read, dim3(4096), dim3(256), 0, 0, (const float4*)g_flush, fb / 16,
                                (float*)g_flush);
-        CK(hipEventRecord(e0, 0));
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, stream));
         launch();
-        CK(hipEventRecord(e1, 0));
-        CK(hipEventSynchronize(e1));
+        CK(hipEventRecord(e1, stream));
+        CK(hipDeviceSynchronize());
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         if (i >= 5) t.push_back(ms * 1e3f);
@@ -142,6 +144,24 @@ int main(int argc, char** argv) {
     SETX(0); SETX(1); SETX(2); SETX(3); SETX(4); SETX(5); SETX(6);
     CK(hipFuncSetAttribute((const void*)wf_fft_h2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WfH2::kLds));
     printf("N=%d hop=%d, frames from %s\n", N, hop, flush_on() ? "HBM (512 MiB flushed between launches)" : "cache");
+    // CU-masked streams (the engine's stream A masks 16 CUs off for the serial streams):
+    // bits [0, 240) as create_streams does, and 240 CUs with every 16th bit off instead
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    hipStream_t s_lo = nullptr, s_even = nullptr, s_hi = nullptr;
+    {
+        const int words = (ncu + 31) / 32;
+        std::vector<uint32_t> lo(words, 0), even(words, 0), hi(words, 0);
+        for (int c = 0; c < ncu; ++c) {
+            if (c < ncu - 16) lo[c / 32] |= 1u << (c % 32);
+            if (c % 16 != 15) even[c / 32] |= 1u << (c % 32);
+            if (c >= 16) hi[c / 32] |= 1u << (c % 32);
+        }
+        CK(hipExtStreamCreateWithCUMask(&s_lo, words, lo.data()));
+        CK(hipExtStreamCreateWithCUMask(&s_even, words, even.data()));
+        CK(hipExtStreamCreateWithCUMask(&s_hi, words, hi.data()));
+    }
+    printf("CUs %d\n", ncu);
     for (int FT : fts) {
         const double alg = 8.0 * ((double)(FT - 1) * hop + N);
         for (int F : {2, 4, 8}) {
@@ -159,6 +179,7 @@ int main(int argc, char** argv) {
                 std::function<void()> run;
                 bool check;
                 bool half_major = false;  // partial rows bin 2k + h at h N/2 + k
+                hipStream_t stream = 0;
             };
             std::vector<V> vs = {
                 {"l32", [&] {
@@ -169,6 +190,18 @@ int main(int argc, char** argv) {
                      hipLaunchKernelGGL(wf_fft_r16<14>, dim3(G), dim3(WfR16<14>::NT), WfR16<14>::kLds, 0, dx,
                                         (int64_t)0, dg, dwin, dtw, dpart);
                  }, true},
+                {"l32 mask[0,240)", [&] {
+                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, s_lo, dx, (int64_t)0,
+                                        dg, dwin, dtw, dpart, 0, 0);
+                 }, false, false, s_lo},
+                {"l32 mask[16,256)", [&] {
+                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, s_hi, dx, (int64_t)0,
+                                        dg, dwin, dtw, dpart, 0, 0);
+                 }, false, false, s_hi},
+                {"l32 mask-every16", [&] {
+                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, s_even, dx, (int64_t)0,
+                                        dg, dwin, dtw, dpart, 0, 0);
+                 }, false, false, s_even},
                 {"h2", [&] {
                      hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx,
                                         (int64_t)0, dg, G, dwin, dtw, dpart);
@@ -180,7 +213,7 @@ int main(int argc, char** argv) {
                  }, false},
             };
             for (auto& v : vs) {
-                const double us = time_us(v.run);
+                const double us = time_us(v.run, v.stream);
                 printf("FT=%5d F=%d G=%4d %-8s %8.2f us  %7.1f GB/s  %5.1f %% of 8 TB/s", FT, F, G, v.name, us,
                        alg / us * 1e-3, alg / us * 1e-3 / 80.0);
                 if (v.check) {
