@@ -82,7 +82,8 @@ void set_last_error(const char* fmt, ...) {
 hipError_t launch_debug_sleep(int64_t us, hipStream_t st);  // synth.hip (stall injection)
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, int fpg, const float* window, const float* ones,
-                         const float2* tw, float* partial, float2* scratch, hipStream_t st);
+                         const float2* tw, float* partial, float2* scratch, int* work, int cus,
+                         hipStream_t st);
 bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
 bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_h2 / wf_fft_l32 (not r16)
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
@@ -308,6 +309,7 @@ struct Waterfall {
     float2* d_y4 = nullptr;  // N > 16384: DIF-split sub-frames (fpg frames per group) or the
                              // four-step scratch (one cf32 frame per group)
     float* d_ones = nullptr; // DIF split: the sub-frames' window (the split applied the frame's)
+    int* d_work = nullptr;   // wf_fft_l32's work-item counter (zeroed before each launch)
     int partial_groups = 0;          // groups d_partial / d_groups hold
     WfGroup* h_groups[kSlots] = {};  // pinned copy sources, per slot of the launching block
     WfRow* h_rows[kSlots] = {};
@@ -937,6 +939,7 @@ static void free_wf(owrx_engine* e, Waterfall* w) {
     prel(e, w->d_partial);
     prel(e, w->d_y4);
     prel(e, w->d_ones);
+    prel(e, w->d_work);
     prel(e, w->d_carry[0]);
     prel(e, w->d_carry[1]);
     prel(e, w->d_groups);
@@ -1496,7 +1499,8 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         e->stats.waterfall_timed_samples += nfr * w->hop;
     }
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(), w->fpg,
-                         w->d_window, w->d_ones, w->d_tw, w->d_partial, w->d_y4, e->sA));
+                         w->d_window, w->d_ones, w->d_tw, w->d_partial, w->d_y4, w->d_work,
+                         std::max(1, e->cus_a), e->sA));
     const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
     const int cin = w->carry_idx, cout = 1 - w->carry_idx;
     HIPCHK(launch_wf_finalize(w->d_partial, w->d_rows, (int)w->rowdesc.size(), w->d_carry[cin],
@@ -2006,14 +2010,15 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                                           S.nsel[o][nr], o, dbg, nr, sB));
         if (S.any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, sB));
         HIPCHK(hipEventRecord(S.evF, sB));
-        // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host.
-        // With B and C on disjoint CUs the encoder waits for stream B's block in the kernel
-        // (signal_block / wait_block: no cross-stream event between back-to-back encoders);
-        // the unmasked (wide) pair keeps the event (a waiting encoder there could hold CUs its
-        // producer needs).  OWRX_HANDOFF=event keeps the event everywhere (A/B).
+        // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host,
+        // behind stream B's event.  OWRX_HANDOFF=kernel instead lets the encoder wait for stream
+        // B's block inside the kernel (signal_block / wait_block, no cross-stream event between
+        // back-to-back encoders; B and C on disjoint CUs only).  Off by default: in the C3 bench
+        // one encoder waited out its 10 s bound at the warm-up -> timed transition (twice in two
+        // runs, profiles/r04d_handoff_stall.txt), i.e. stream B's signal was held behind it.
         static const bool handoff = [] {
             const char* v = getenv("OWRX_HANDOFF");
-            return !(v && strcmp(v, "event") == 0);
+            return v && strcmp(v, "kernel") == 0;
         }();
         const int nad = S.nsel[1][0] + S.nsel[1][1];
         const bool in_kernel = handoff && !wide && e->d_ready && nad > 0;
@@ -2150,8 +2155,19 @@ static hipError_t create_streams(owrx_engine* e) {
     const std::vector<uint32_t> mW = nw > 0 ? mask_range(a_end + nb + nc + nr, ncu) : mR;
     const std::pair<hipStream_t*, const std::vector<uint32_t>*> sm[] = {
         {&e->sA, &mA}, {&e->sB, &mB}, {&e->sC, &mC}, {&e->sR, &mR}};
+    // OWRX_MASK_A=0: stream A on every CU (the serial streams keep their own; A's waves may
+    // then share their CUs) -- A/B of the CU mask's cost on A's full-chip kernels
+    static const bool mask_a = [] {
+        const char* v = getenv("OWRX_MASK_A");
+        return !(v && strcmp(v, "0") == 0);
+    }();
     for (auto& x : sm) {
-        err = hipExtStreamCreateWithCUMask(x.first, (uint32_t)words, x.second->data());
+        if (x.first == &e->sA && !mask_a) {
+            err = hipStreamCreateWithFlags(x.first, hipStreamNonBlocking);
+            e->cus_a = ncu;
+        } else {
+            err = hipExtStreamCreateWithCUMask(x.first, (uint32_t)words, x.second->data());
+        }
         if (err != hipSuccess) return err;
     }
     for (auto& r : e->rslots) {
@@ -2496,6 +2512,7 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
     auto setup = [&]() -> int {
         HIPCHK(palloc(e, &w->d_window, (size_t)fft_size));
         HIPCHK(palloc(e, &w->d_tw, (size_t)fft_size));
+        HIPCHK(palloc(e, &w->d_work, 64));
         HIPCHK(palloc(e, &w->d_carry[0], (size_t)fft_size));
         HIPCHK(palloc(e, &w->d_carry[1], (size_t)fft_size));
         RCCHK(upload(e, w->d_window, win.data(), sizeof(float) * fft_size));

@@ -16,6 +16,7 @@
 //   (rows span blocks), 10*log10 + add_db correction, fftshift, quantise (short)(dB*100).
 // wf_adpcm_rows_spec: FftAdpcm (IMA-ADPCM of each padded row), one workgroup per row,
 //   segment-parallel and exact (adpcm_spec.h).
+#include <algorithm>
 #include <stdlib.h>
 #include <string.h>
 
@@ -642,31 +643,46 @@ OWRX_DEV int wf_swz32(int e) { return e ^ ((e >> 5) & 15); }
 __global__ void __launch_bounds__(WfL32::NT)
 wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
            const float* __restrict__ window, const float2* __restrict__ tw,
-           float* __restrict__ partial, int qlog, int fstride) {
+           float* __restrict__ partial, int qlog, int fstride, int items, int* __restrict__ work) {
     using K = WfL32;
     constexpr int N = K::N, NT = K::NT;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    __shared__ int s_next;
     const int t0 = threadIdx.x;
     WF_RSTAMP(14);
     WF_STAMP(0);
-    const int gi = blockIdx.x >> qlog;
-    const WfGroup g = groups[gi];
-    const int64_t g0 = __builtin_amdgcn_readfirstlane(
-        qlog ? (int)((((int64_t)gi * fstride << qlog) + (blockIdx.x & ((1 << qlog) - 1))) * N)
-             : (int)(g.start - blk_start));
-    const int hop = __builtin_amdgcn_readfirstlane(qlog ? N << qlog : g.hop);
-    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
-    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
-        0x00020000);
+    // Work items (a group's frames, or one sub-frame j of a group after the DIF split) are dealt
+    // dynamically: workgroup b starts on item b, then takes the next unclaimed one from `work`
+    // (zeroed before the launch) until none is left.  With one workgroup per CU a launch of one
+    // item per CU doubled its time whenever some CU was busy or its queue's CU mask left a
+    // shader engine short (measured 85 vs 49 us per 960 C3 frames on a CU-masked stream); now a
+    // late CU only takes fewer items.  An item's rows are still summed by one workgroup in frame
+    // order, so the results do not depend on which workgroup took it.
+    struct Item {
+        __amdgpu_buffer_rsrc_t xr;
+        int hop, nfr;
+    };
+    auto item = [&](int w) {
+        const int gi = w >> qlog;
+        const WfGroup g = groups[gi];
+        const int64_t g0 = __builtin_amdgcn_readfirstlane(
+            qlog ? (int)((((int64_t)gi * fstride << qlog) + (w & ((1 << qlog) - 1))) * N)
+                 : (int)(g.start - blk_start));
+        Item it;
+        it.hop = __builtin_amdgcn_readfirstlane(qlog ? N << qlog : g.hop);
+        it.nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+        it.xr = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float2*>(blk + g0), 0,
+            (int)(sizeof(float2) * ((int64_t)(it.nfr - 1) * it.hop + N)), 0x00020000);
+        return it;
+    };
     const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
                                                       (int)(sizeof(float) * N), 0x00020000);
-    // frame f's samples; f == nfr (the prefetch after the last frame) is offset past the
-    // descriptor's range, so those loads return zeros without touching memory.  The prefetch is
-    // unconditional: behind an `if (f + 1 < nfr)` the wait-count pass merged the two paths at
-    // vmcnt(0) before the window products, so every frame waited for its successor's samples.
-    auto load_x = [&](int f, float2* v) {
-        const int fo = f < nfr ? f * hop * 8 : kWfOob;
+    // the samples of the frame at byte offset fo of descriptor xr (fo = kWfOob: zeros, no memory
+    // access).  The prefetch of the next frame is unconditional: behind an `if` the wait-count
+    // pass merged the two paths at vmcnt(0) before the window products, so every frame waited
+    // for its successor's samples.
+    auto load_x = [&](__amdgpu_buffer_rsrc_t xr, int fo, float2* v) {
 #pragma unroll
         for (int r = 0; r < 32; ++r) {
             const int vo = t0 * 8 + fo;
@@ -690,90 +706,107 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         const int e = t0 + NT * i;  // 992 entries: (r - 1) * 32 + k
         t2v[i] = e < 31 * 32 ? tw[(((e >> 5) + 1) * (e & 31)) << (4 + qlog)] : make_float2(0.f, 0.f);
     }
+    int w = blockIdx.x;
+    Item cur = item(w);
     float2 nx[32];
-    load_x(0, nx);
+    load_x(cur.xr, 0, nx);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
         if (t0 + NT * i < 31 * 32) sm[K::TW2 + t0 + NT * i] = t2v[i];
-    float acc[32];
-#pragma unroll
-    for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
     const int sw = wf_swz32(t0);  // swz(t + 512 m) = swz(t) + 512 m
 #pragma unroll 1
-    for (int f = 0; f < nfr; ++f) {
-        int t = threadIdx.x;
-        asm volatile("" : "+v"(t));
-        const int sb = 1 + 6 * f;
-        if (f < 2) WF_STAMP(sb);
-        float2 a[32];
-        {
-            float wv[32];
-            load_w(wv);
-#pragma unroll
-            for (int r = 0; r < 32; ++r) a[r] = make_float2(nx[r].x * wv[r], nx[r].y * wv[r]);
-        }
-        load_x(f + 1, nx);
-        f2dft32(a);
-        if (f < 2) WF_STAMP(sb + 1);
-        __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
-#pragma unroll
-        for (int k = 0; k < 32; ++k) sm[32 * t + (k ^ (t & 15))] = a[l32_at(k)];
-        if (f < 2) WF_STAMP(sb + 2);
+    while (true) {
+        // claim the item after this one now: its first frame is prefetched during this one's last
+        if (t0 == 0) s_next = (int)gridDim.x + atomicAdd(work, 1);
         __syncthreads();
-        // P2
-        {
-            const int ts = wf_swz32(t);
+        const int wn = __builtin_amdgcn_readfirstlane(s_next);
+        const bool has_next = wn < items;
+        const Item nxt = item(has_next ? wn : w);
+        float acc[32];
 #pragma unroll
-            for (int r = 0; r < 32; ++r) a[r] = sm[ts + NT * r];
-            const int k = t & 31;
-            const float2* T = sm + K::TW2 + k;
+        for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
+#pragma unroll 1
+        for (int f = 0; f < cur.nfr; ++f) {
+            int t = threadIdx.x;
+            asm volatile("" : "+v"(t));
+            const int sb = 1 + 6 * f;
+            if (f < 2) WF_STAMP(sb);
+            float2 a[32];
+            {
+                float wv[32];
+                load_w(wv);
 #pragma unroll
-            for (int r = 1; r < 32; ++r) {
-                a[r] = f2mul(a[r], T[(r - 1) * 32]);
-                if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 8 twiddles live
+                for (int r = 0; r < 32; ++r) a[r] = make_float2(nx[r].x * wv[r], nx[r].y * wv[r]);
             }
+            // next frame: this item's, else the next item's first, else nothing (zeros)
+            const bool last = f + 1 == cur.nfr;
+            load_x(last ? nxt.xr : cur.xr,
+                   !last ? (f + 1) * cur.hop * 8 : has_next ? 0 : kWfOob, nx);
             f2dft32(a);
-            __syncthreads();  // every P2 read before any P2 store
-            const int base = (t >> 5) * 1024 + k;
+            if (f < 2) WF_STAMP(sb + 1);
+            __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
 #pragma unroll
-            for (int r = 0; r < 32; ++r) sm[wf_swz32(base + 32 * r)] = a[l32_at(r)];
-        }
-        if (f < 2) WF_STAMP(sb + 3);
-        __syncthreads();
-        // P3
+            for (int k = 0; k < 32; ++k) sm[32 * t + (k ^ (t & 15))] = a[l32_at(k)];
+            if (f < 2) WF_STAMP(sb + 2);
+            __syncthreads();
+            // P2
+            {
+                const int ts = wf_swz32(t);
 #pragma unroll
-        for (int m = 0; m < 32; ++m) a[m] = sm[sw + NT * m];
-        if (f < 2) WF_STAMP(sb + 4);
-        float2 tb[16];  // W_N^(r t) from the exact powers of two, at most three products each
-        tb[1] = tp[0];
-        tb[2] = tp[1];
-        tb[4] = tp[2];
-        tb[8] = tp[3];
-        tb[3] = f2mul(tp[0], tp[1]);
-        tb[5] = f2mul(tp[0], tp[2]);
-        tb[6] = f2mul(tp[1], tp[2]);
-        tb[7] = f2mul(tb[3], tp[2]);
+                for (int r = 0; r < 32; ++r) a[r] = sm[ts + NT * r];
+                const int k = t & 31;
+                const float2* T = sm + K::TW2 + k;
 #pragma unroll
-        for (int r = 9; r < 16; ++r) tb[r] = f2mul(tb[r - 8], tp[3]);
+                for (int r = 1; r < 32; ++r) {
+                    a[r] = f2mul(a[r], T[(r - 1) * 32]);
+                    if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // <= 8 twiddles live
+                }
+                f2dft32(a);
+                __syncthreads();  // every P2 read before any P2 store
+                const int base = (t >> 5) * 1024 + k;
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            float2 c[16];
-            c[0] = a[b];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) {
-                const float2 w = b ? f2mul32(tb[r], r) : tb[r];
-                c[r] = f2mul(a[b + 2 * r], w);
+                for (int r = 0; r < 32; ++r) sm[wf_swz32(base + 32 * r)] = a[l32_at(r)];
             }
-            f2dft<16>(c);
+            if (f < 2) WF_STAMP(sb + 3);
+            __syncthreads();
+            // P3
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-                acc[b + 2 * r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b + 2 * r]));
+            for (int m = 0; m < 32; ++m) a[m] = sm[sw + NT * m];
+            if (f < 2) WF_STAMP(sb + 4);
+            float2 tb[16];  // W_N^(r t) from the exact powers of two, at most three products each
+            tb[1] = tp[0];
+            tb[2] = tp[1];
+            tb[4] = tp[2];
+            tb[8] = tp[3];
+            tb[3] = f2mul(tp[0], tp[1]);
+            tb[5] = f2mul(tp[0], tp[2]);
+            tb[6] = f2mul(tp[1], tp[2]);
+            tb[7] = f2mul(tb[3], tp[2]);
+#pragma unroll
+            for (int r = 9; r < 16; ++r) tb[r] = f2mul(tb[r - 8], tp[3]);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                float2 c[16];
+                c[0] = a[b];
+#pragma unroll
+                for (int r = 1; r < 16; ++r) {
+                    const float2 wt = b ? f2mul32(tb[r], r) : tb[r];
+                    c[r] = f2mul(a[b + 2 * r], wt);
+                }
+                f2dft<16>(c);
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    acc[b + 2 * r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b + 2 * r]));
+            }
+            if (f < 2) WF_STAMP(sb + 5);
         }
-        if (f < 2) WF_STAMP(sb + 5);
-    }
-    float* out = partial + (int64_t)blockIdx.x * N;  // = group * (N << qlog) + j * N
+        float* out = partial + (int64_t)w * N;  // = group * (N << qlog) + j * N
 #pragma unroll
-    for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
+        for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
+        if (!has_next) break;
+        w = wn;
+        cur = nxt;
+    }
     WF_STAMP(13);
     WF_RSTAMP(15);
 }
@@ -1241,7 +1274,8 @@ bool wf_uses_split(int logn) {
 
 static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw,
-                                 float* partial, hipStream_t st, int qlog = 0, int fstride = 0) {
+                                 float* partial, int* work, int cus, hipStream_t st, int qlog = 0,
+                                 int fstride = 0) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)wf_fft_l32,
@@ -1250,8 +1284,14 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(wf_fft_l32, dim3(ngroups << qlog), dim3(WfL32::NT), WfL32::kLds, st, blk,
-                       blk_start, groups, window, tw, partial, qlog, fstride);
+    if (!work) return hipErrorInvalidValue;
+    const int items = ngroups << qlog;
+    hipError_t e = hipMemsetAsync(work, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    // one workgroup per CU (the 136 KiB image), at most one per item
+    const int grid = std::max(1, std::min(items, cus));
+    hipLaunchKernelGGL(wf_fft_l32, dim3(grid), dim3(WfL32::NT), WfL32::kLds, st, blk, blk_start,
+                       groups, window, tw, partial, qlog, fstride, items, work);
     return hipGetLastError();
 }
 
@@ -1260,11 +1300,12 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
 template <int QLOG>
 static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                    int ngroups, int fpg, const float* window, const float* ones,
-                                   const float2* tw, float* partial, float2* scratch, hipStream_t st) {
+                                   const float2* tw, float* partial, float2* scratch, int* work,
+                                   int cus, hipStream_t st) {
     if (!scratch || !ones || fpg < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wf_dif_split<QLOG>, dim3(16384 / 256, fpg, ngroups), dim3(256), 0, st, blk,
                        blk_start, groups, window, tw, fpg, scratch);
-    return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, st, QLOG, fpg);
+    return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, work, cus, st, QLOG, fpg);
 }
 
 static hipError_t launch_fft_h2(const float2* blk, int64_t blk_start, const WfGroup* groups,
@@ -1287,12 +1328,12 @@ static hipError_t launch_fft_h2(const float2* blk, int64_t blk_start, const WfGr
 template <int LOGN>
 static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw, float* partial,
-                                 hipStream_t st) {
+                                 int* work, int cus, hipStream_t st) {
     if constexpr (LOGN == 14) {
         if (wf_uses_h2(LOGN))
             return launch_fft_h2(blk, blk_start, groups, ngroups, window, tw, partial, st);
         if (!wf_force_r16())
-            return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, st);
+            return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
     }
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
@@ -1300,20 +1341,21 @@ static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfG
 
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, int fpg, const float* window, const float* ones,
-                         const float2* tw, float* partial, float2* scratch, hipStream_t st) {
+                         const float2* tw, float* partial, float2* scratch, int* work, int cus,
+                         hipStream_t st) {
     if (wf_uses_split(logn))
         return logn == 15 ? launch_fft_split<1>(blk, blk_start, groups, ngroups, fpg, window, ones, tw,
-                                                partial, scratch, st)
+                                                partial, scratch, work, cus, st)
                           : launch_fft_split<2>(blk, blk_start, groups, ngroups, fpg, window, ones, tw,
-                                                partial, scratch, st);
+                                                partial, scratch, work, cus, st);
     switch (logn) {
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 10: return launch_fft_sel<10>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 11: return launch_fft_sel<11>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 12: return launch_fft_sel<12>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 13: return launch_fft_sel<13>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 14: return launch_fft_sel<14>(blk, blk_start, groups, ngroups, window, tw, partial, st);
+        case 10: return launch_fft_sel<10>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
+        case 11: return launch_fft_sel<11>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
+        case 12: return launch_fft_sel<12>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
+        case 13: return launch_fft_sel<13>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
+        case 14: return launch_fft_sel<14>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
         case 15: return launch_fft4_t<7, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
                                             scratch, st);
         case 16: return launch_fft4_t<8, 8>(blk, blk_start, groups, ngroups, window, tw, partial,

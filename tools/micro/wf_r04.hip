@@ -133,6 +133,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dref, sizeof(float) * (size_t)FTmax * N));
     CK(hipMalloc(&dpart, sizeof(float) * (size_t)FTmax * N));
     CK(hipMalloc(&dg, sizeof(WfGroup) * FTmax));
+    int* dwork;
+    CK(hipMalloc(&dwork, 64));
     CK(hipMemcpy(dx, x.data(), sizeof(float2) * S, hipMemcpyHostToDevice));
     CK(hipMemcpy(dtw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice));
     CK(hipMemcpy(dwin, win.data(), sizeof(float) * N, hipMemcpyHostToDevice));
@@ -148,7 +150,8 @@ int main(int argc, char** argv) {
     // bits [0, 240) as create_streams does, and 240 CUs with every 16th bit off instead
     int ncu = 0;
     CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
-    hipStream_t s_lo = nullptr, s_even = nullptr, s_hi = nullptr;
+    hipStream_t s_lo = nullptr, s_even = nullptr, s_hi = nullptr, s_all = nullptr, s_plain = nullptr;
+    CK(hipStreamCreateWithFlags(&s_plain, hipStreamNonBlocking));
     {
         const int words = (ncu + 31) / 32;
         std::vector<uint32_t> lo(words, 0), even(words, 0), hi(words, 0);
@@ -160,7 +163,14 @@ int main(int argc, char** argv) {
         CK(hipExtStreamCreateWithCUMask(&s_lo, words, lo.data()));
         CK(hipExtStreamCreateWithCUMask(&s_even, words, even.data()));
         CK(hipExtStreamCreateWithCUMask(&s_hi, words, hi.data()));
+        std::vector<uint32_t> all(words, 0xffffffffu);
+        CK(hipExtStreamCreateWithCUMask(&s_all, words, all.data()));
     }
+    auto l32 = [&](int G, hipStream_t st) {
+        CK(hipMemsetAsync(dwork, 0, sizeof(int), st));
+        hipLaunchKernelGGL(wf_fft_l32, dim3(std::min(G, st == 0 || st == s_plain || st == s_all ? 256 : 240)), dim3(WfL32::NT), WfL32::kLds, st, dx, (int64_t)0,
+                           dg, dwin, dtw, dpart, 0, 0, G, dwork);
+    };
     printf("CUs %d\n", ncu);
     for (int FT : fts) {
         const double alg = 8.0 * ((double)(FT - 1) * hop + N);
@@ -183,24 +193,29 @@ int main(int argc, char** argv) {
             };
             std::vector<V> vs = {
                 {"l32", [&] {
-                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, (int64_t)0,
-                                        dg, dwin, dtw, dpart, 0, 0);
+                     l32(G, 0);
                  }, true},
                 {"r16", [&] {
                      hipLaunchKernelGGL(wf_fft_r16<14>, dim3(G), dim3(WfR16<14>::NT), WfR16<14>::kLds, 0, dx,
                                         (int64_t)0, dg, dwin, dtw, dpart);
                  }, true},
                 {"l32 mask[0,240)", [&] {
-                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, s_lo, dx, (int64_t)0,
-                                        dg, dwin, dtw, dpart, 0, 0);
+                     l32(G, s_lo);
                  }, false, false, s_lo},
                 {"l32 mask[16,256)", [&] {
-                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, s_hi, dx, (int64_t)0,
-                                        dg, dwin, dtw, dpart, 0, 0);
+                     l32(G, s_hi);
                  }, false, false, s_hi},
+                {"l32 mask-all", [&] {
+                     l32(G, s_all);
+                 }, false, false, s_all},
+                {"l32 stream", [&] {
+                     l32(G, s_plain);
+                 }, false, false, s_plain},
+                {"mem mask[0,240)", [&] {
+                     hipLaunchKernelGGL(wf_mem_pf, dim3(G), dim3(512), 0, s_lo, dx, dg, dpart);
+                 }, false, false, s_lo},
                 {"l32 mask-every16", [&] {
-                     hipLaunchKernelGGL(wf_fft_l32, dim3(G), dim3(WfL32::NT), WfL32::kLds, s_even, dx, (int64_t)0,
-                                        dg, dwin, dtw, dpart, 0, 0);
+                     l32(G, s_even);
                  }, false, false, s_even},
                 {"h2", [&] {
                      hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx,
