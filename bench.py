@@ -177,7 +177,7 @@ def cpu_baseline(fs, n_fft, hop, avg, plist):
 
 
 def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds, block,
-                   ddc_mode="fast", churn=False, pipelined=None):
+                   ddc_mode="fast", churn=False, pipelined=None, wf_batch=0, wf_cap_ms=0.0):
     """SURVEY.md 8d measurement 1: feed the stream at its nominal rate through the host push path
     (SDR -> host cf32 -> PCIe -> HBM, owrx_push_iq) to a fresh engine with the same waterfall and
     chains; every block is pushed on its wall-clock deadline.  Without `churn` each block is then
@@ -190,13 +190,23 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     bandpass (owrx_chain_set_bandpass) while that block and its predecessors are in flight.  It
     keeps up when every push returned before the next deadline (a GPU slower than the stream
     back-pressures push) and nothing overran; `pipeline_drains` counts full pipeline drains inside
-    the loop (none: those calls do not drain); the host latency of each call is reported."""
+    the loop (none: those calls do not drain); the host latency of each call is reported.
+
+    `wf_batch` > 1: the waterfall batches its FFT launches as the headline engine does
+    (owrx_waterfall_set_batch), bounded by `wf_cap_ms` of wall clock (owrx_waterfall_set_latency);
+    the rows' measured latency (the call of the block that completed a row to the row in the
+    host ring) is reported."""
     if pipelined is None:
         pipelined = churn
     t_setup = time.perf_counter()
-    eng = Engine(fs, max_block=block)
+    hist = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
+    eng = Engine(fs, max_block=block, history=hist)
     eng.set_ddc_mode(ddc_mode)
     wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
+    if wf_batch > 1:
+        wf.set_batch(wf_batch)
+        if wf_cap_ms > 0:
+            wf.set_latency(wf_cap_ms)
     chains = []
     try:
         for i, p in enumerate(plist):
@@ -258,6 +268,13 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             "read_ms": round(1e3 * tr / nblocks, 3)}
     for k in ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots", "host_ms_wait_rows"):
         host[k] = round((st[k] - st0[k]) / nblocks, 3)
+    nrow = st["wf_rows_latency_n"] - st0["wf_rows_latency_n"]
+    rows = {"rows": int(st["waterfall_rows"] - st0["waterfall_rows"]),
+            "batch_frames": wf_batch, "cap_ms": wf_cap_ms,
+            "latency_ms_max": round(st["wf_row_latency_ms_max"], 3),
+            "latency_ms_mean": round((st["wf_row_latency_ms_sum"] - st0["wf_row_latency_ms_sum"])
+                                     / max(1, nrow), 3),
+            "launches": int(st["waterfall_launches"] - st0["waterfall_launches"])}
     eng.close()
     extra = {}
 
@@ -277,6 +294,7 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
                                    "deadline to the end of the block's push + churn + reads "
                                    "(pipelined, no per-block sync)"),
             "overruns": int(st["overruns"]),
+            "waterfall_rows": rows,
             "host_per_block": host,
             "finish_lag_ms": round(1e3 * finish_lag, 3) if pipelined else None,
             "keeps_up": bool(st["overruns"] == 0 and max(lat) < period and
@@ -285,7 +303,8 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
 
 
 def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, stream_host,
-                        seconds, block, ladder, ddc_mode, budget_s, agree=None, world=1):
+                        seconds, block, ladder, ddc_mode, budget_s, agree=None, world=1,
+                        hold_s=0.0, wf_batch=0, wf_cap_ms=0.0):
     """BASELINE.md 3 / SURVEY.md 8d: the largest chain count C (from `ladder`) for which the paced
     real-time check at the config's stream rate keeps up (no overrun, every block within its
     period), with the waterfall running too.  Stops at the first failure (a level that does not
@@ -306,35 +325,237 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
         _log("capacity level: %d chains" % C)
         try:
             r = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seconds,
-                               block, ddc_mode, pipelined=True)
+                               block, ddc_mode, pipelined=True, wf_batch=wf_batch,
+                               wf_cap_ms=wf_cap_ms)
             ok = r["keeps_up"]
         except Exception as exc:  # e.g. out of device memory: this level does not run
             r, ok = {"chains": C, "error": str(exc)[:200], "setup_s": 0.0}, False
             _log("  failed: %s" % exc)
         ok = bool(agree(1.0 if ok else 0.0, "min") > 0)
         lvl = {k: r[k] for k in ("chains", "max_block_latency_ms", "mean_block_latency_ms",
-                                 "finish_lag_ms", "overruns", "setup_s", "host_per_block", "error")
+                                 "finish_lag_ms", "overruns", "setup_s", "host_per_block",
+                                 "waterfall_rows", "error")
                if k in r}
         lvl["keeps_up"] = ok
         if world > 1:
             lvl["max_block_latency_ms_all_ranks"] = round(agree(r.get("max_block_latency_ms", 1e9), "max"), 3)
         levels.append(lvl)
         if "error" not in r:
-            _log("  setup %.2f s, keeps_up %s, max block latency %.2f ms"
-                 % (r["setup_s"], ok, r["max_block_latency_ms"]))
+            _log("  setup %.2f s, keeps_up %s, max block latency %.2f ms, finish lag %.2f ms, "
+                 "overruns %d, host/block %s" % (r["setup_s"], ok, r["max_block_latency_ms"],
+                                                 r["finish_lag_ms"], r["overruns"],
+                                                 json.dumps(r["host_per_block"])))
         if not ok:
             break
         best = C
     failing = next((l["chains"] for l in levels if l.get("keeps_up") is False), None)
+    hold = None
+    if best and hold_s > 0:
+        # the top passing level once more, held for hold_s of stream (60 s)
+        _log("capacity hold: %d chains for %.0f s" % (best, hold_s))
+        ms = [modes[c % len(modes)] for c in range(best)]
+        plist = [params.chain_params(fs, o, m) for o, m in zip(offsets_of(best), ms)]
+        try:
+            r = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, hold_s,
+                               block, ddc_mode, pipelined=True, wf_batch=wf_batch,
+                               wf_cap_ms=wf_cap_ms)
+            ok = bool(agree(1.0 if r["keeps_up"] else 0.0, "min") > 0)
+            hold = {k: r[k] for k in ("chains", "seconds", "blocks", "max_block_latency_ms",
+                                      "mean_block_latency_ms", "finish_lag_ms", "overruns",
+                                      "waterfall_rows", "host_per_block") if k in r}
+            hold["keeps_up"] = ok
+        except Exception as exc:
+            hold = {"chains": best, "error": str(exc)[:200], "keeps_up": False}
+        _log("  hold: " + json.dumps(hold))
     return {"max_realtime_chains": best * world, "per_gpu": best, "first_failing_level": failing,
+            "hold": hold,
             "stream_msps": fs / 1e6, "block_samples": block,
             "seconds_per_level": seconds, "levels": levels,
+            "waterfall": "batched launches of up to %d frames, bounded by %.0f ms of wall clock "
+                         "(owrx_waterfall_set_batch + owrx_waterfall_set_latency)"
+                         % (wf_batch, wf_cap_ms) if wf_batch > 1 else "per-block launches",
             "note": "paced pushes of host cf32 through owrx_push_iq at the stream's wall-clock rate, "
                     "waterfall + C chains per GPU (modes cycled), pipelined like a server (outputs "
                     "read as they arrive, no per-block sync: a push that cannot keep its deadline "
                     "fails the level); largest C "
                     "that kept up on every GPU, times N; the ladder stops at the first level that did "
                     "not (first_failing_level) or the time budget"}
+
+
+def _dropin_run(fs, C, blocks, paced, pump_limit):
+    """One drop-in run: C ClientDemodulatorChain graphs as the reference builds them
+    (tests/golden/dsp_graph.json "nfm": Shift -> FirDecimate -> ... -> AdpcmEncoder, one Shift
+    rate per client) plus the SpectrumThread's FftChain (tests/golden/spectrum_graph.json
+    "start_adpcm") on one wideband pycsdr Buffer, each output read by its own pump thread
+    (owrx/dsp.py:846-863, owrx/fft.py:73), the stream written in 2^18-sample writes (the shim
+    driver's block).  The driver plans and creates its segments on the first writes; the
+    measured writes start once every segment runs and the driver has caught up."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dsp_replay  # graph rebuilder (data from tests/golden; no reference code)
+    from openwebrx_amd import params, synth
+    from openwebrx_amd.pycsdr import _graph
+    from openwebrx_amd.pycsdr import modules as M
+    from openwebrx_amd.pycsdr.types import Format
+    if 2 * C + 1 > pump_limit:
+        raise ValueError("%d pump threads over the limit %d" % (2 * C + 1, pump_limit))
+    s = dsp_replay.steps()["nfm"]
+    offs = synth.carrier_offsets(fs, C)
+    wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 23)
+    pumps, got = [], {}
+
+    def pump(name, buf):
+        r = buf.getReader()
+        got[name] = [0, None]
+
+        def run():
+            for data in iter(r.read, None):  # csdr.chain.Chain.pump(reader.read, write)
+                got[name][0] += len(data)
+                got[name][1] = time.perf_counter()
+        t = threading.Thread(target=run, name="dsp_pump_" + name, daemon=True)
+        t.start()
+        pumps.append((r, t))
+
+    cls = [d["class"] for _, d, _ in s["graph"]]
+    for c in range(C):
+        _, mods, outs, power = dsp_replay.build(s, wide=wide)
+        mods[0].setRate(params.shift_rate(offs[c], fs))
+        for m in mods:  # the recorded Python consumer of the wideband buffer: not served here
+            if isinstance(m, M.Reader):
+                m.stop()
+        pump("audio%d" % c, outs[cls.index("AdpcmEncoder")])
+        pump("smeter%d" % c, power)
+    with open(os.path.join(ROOT, "tests", "golden", "spectrum_graph.json")) as f:
+        sg = {x["step"]: x for x in json.load(f)}["start_adpcm"]
+    fmods = [dsp_replay._make(d) for d in sg["graph"]]
+    for a, b in zip(fmods, fmods[1:]):
+        buf = M.Buffer(a.getOutputFormat())
+        a.setWriter(buf)
+        b.setReader(buf.getReader())
+    rows = M.Buffer(Format.CHAR)
+    fmods[-1].setWriter(rows)
+    fmods[0].setReader(wide.getReader())
+    pump("waterfall", rows)
+
+    blk = _graph.BLOCK
+    iq, _ = synth.make_iq(fs, 8 * blk, ["nfm"] * 16)
+    chunks = [iq[k * blk:(k + 1) * blk].tobytes() for k in range(8)]
+    # set-up: a few writes make the driver plan and create every segment; wait until it runs
+    # them all and has consumed what it was given
+    t_setup = time.perf_counter()
+    drv = None
+    for k in range(4):
+        wide.write(chunks[k % 8])
+        drv = drv or _graph._drivers.get(id(wide))
+    t_log = t_setup
+    while time.perf_counter() - t_setup < 60:
+        drv = drv or _graph._drivers.get(id(wide))
+        if drv and drv.state != "RUNNING":
+            break
+        if drv and drv.engine is not None and len(drv.segments) == C + 1 \
+                and drv.reader.available() == 0:
+            break
+        if time.perf_counter() - t_log > 5:
+            t_log = time.perf_counter()
+            _log("  setup: driver %s, segments %d" % (drv and drv.state,
+                                                      len(drv.segments) if drv else 0))
+        time.sleep(0.01)
+    fused = bool(drv and drv.engine is not None and len(drv.segments) == C + 1)
+    t_setup = time.perf_counter() - t_setup
+    if not fused:
+        state = (drv.state, str(drv.error)[:160]) if drv else ("no driver", "")
+        _graph.finish(wide)
+        for r, t in pumps:
+            r.stop()
+            t.join(5)
+        raise RuntimeError("drop-in did not fuse %d clients in %.0f s: %s" % (C, t_setup, state))
+    a0 = sum(v[0] for v in got.values())
+    lag, t0 = [], time.perf_counter()
+    period = blk / fs
+    for k in range(blocks):
+        if paced:
+            wait = t0 + k * period - time.perf_counter()
+            if wait > 0:
+                time.sleep(wait)
+        else:  # as fast as the driver takes it: at most four writes ahead of it
+            while drv.reader.available() > 4 * 8 * blk:
+                time.sleep(0.0002)
+        wide.write(chunks[k % 8])
+        lag.append(drv.reader.available() / 8 / blk)
+    t_last = time.perf_counter()
+    while drv.reader.available() > 0 and time.perf_counter() - t_last < 30:
+        time.sleep(0.002)
+    t_fed = time.perf_counter()
+    time.sleep(period)  # the last block's outputs: a period for the pumps to receive them
+    last = max(v[1] or 0 for v in got.values())
+    audio = [got["audio%d" % c][0] for c in range(C)]
+    out_bytes = sum(v[0] for v in got.values()) - a0
+    wf_bytes = got["waterfall"][0]
+    _graph.finish(wide)
+    for r, t in pumps:
+        r.stop()
+        t.join(5)
+    t_end = max(t_fed, last)
+    res = {"clients": C, "pump_threads": len(pumps), "fused": fused,
+           "setup_s": round(t_setup, 2), "writes": blocks, "write_samples": blk,
+           "max_driver_lag_blocks": round(max(lag), 2),
+           "mean_driver_lag_blocks": round(sum(lag) / len(lag), 3),
+           "audio_bytes_min": min(audio), "waterfall_bytes": wf_bytes,
+           "output_bytes": out_bytes}
+    if paced:
+        finish_lag = t_end - t_last
+        res["finish_lag_ms"] = round(1e3 * finish_lag, 1)
+        res["period_ms"] = round(1e3 * period, 1)
+        res["keeps_up"] = bool(fused and max(lag) <= 2.0 and finish_lag < period + 0.05
+                               and min(audio) > 0)
+    else:
+        res["msps"] = round(blocks * blk / (t_end - t0) / 1e6, 2)
+        res["seconds"] = round(t_end - t0, 3)
+    return res
+
+
+def dropin_check(fs, clients, ladder, seconds, budget_s, pump_limit):
+    """what the drop-in (pycsdr shim -> _graph.EngineDriver -> engine) runs.
+    `msps`: the shim path's ingest rate with `clients` clients, the stream written as fast as the
+    driver takes it; `max_clients`: the largest client count of `ladder` whose paced 10 Msps run
+    keeps up (driver never more than two blocks behind the writer, every output delivered within
+    a period of the last write), each output on its own pump thread."""
+    import threading
+    from openwebrx_amd.pycsdr import _graph
+    blk = _graph.BLOCK
+    t0 = time.perf_counter()
+    _log("drop-in: %d clients unpaced (threads alive: %d)" % (clients, threading.active_count()))
+    try:
+        thr = _dropin_run(fs, clients, max(8, int(seconds * fs / blk)), False, pump_limit)
+    except Exception as exc:
+        thr = {"clients": clients, "error": str(exc)[:200]}
+    levels, best = [], 0
+    for C in ladder:
+        if levels and time.perf_counter() - t0 + 2.5 * levels[-1].get("setup_s", 0) + seconds \
+                > budget_s:
+            levels.append({"clients": C, "skipped": "time budget"})
+            break
+        _log("drop-in: %d clients paced (threads alive: %d)" % (C, threading.active_count()))
+        try:
+            r = _dropin_run(fs, C, max(8, int(seconds * fs / blk)), True, pump_limit)
+        except Exception as exc:
+            r = {"clients": C, "error": str(exc)[:200], "keeps_up": False}
+        levels.append(r)
+        _log("  " + json.dumps(r))
+        if not r["keeps_up"]:
+            break
+        best = C
+    return {"msps": thr.get("msps"), "msps_clients": clients, "unpaced": thr,
+            "max_clients_paced": best, "levels": levels,
+            "stream_msps": fs / 1e6,
+            "wf_latency_cap_ms": _graph.wf_latency_ms(),
+            "note": "the pycsdr shim as the reference drives it: ClientDemodulatorChain graphs "
+                    "(tests/golden/dsp_graph.json nfm) + the FftChain on one wideband Buffer, "
+                    "fused by openwebrx_amd.pycsdr._graph onto one engine (2^18-sample blocks, "
+                    "waterfall batched under the wall-clock row-latency cap), every output on "
+                    "its own Python pump thread; msps = samples written / (first measured write "
+                    "to the last output delivered); the ladder is bounded by %d pump threads "
+                    "(the GPU box's task limit)" % pump_limit}
 
 
 def pmc_traffic(prefix, config):
@@ -432,6 +653,17 @@ def main():
                     help="chain counts tried by the max_realtime_chains sweep ('' = skip)")
     ap.add_argument("--capacity-seconds", type=float, default=2.0,
                     help="seconds of paced stream per sweep level")
+    ap.add_argument("--capacity-hold-seconds", type=float, default=60.0,
+                    help="the top passing level once more for this long (0: skip)")
+    ap.add_argument("--wf-latency-ms", type=float, default=100.0,
+                    help="wall-clock bound on a ready waterfall frame's wait for its batch "
+                         "(owrx_waterfall_set_latency; one 9 fps row period less a margin for "
+                         "the launch itself)")
+    ap.add_argument("--dropin-clients", type=int, default=256,
+                    help="clients of the drop-in's unpaced throughput run (0: skip the drop-in)")
+    ap.add_argument("--dropin-ladder", default="256,384",
+                    help="client counts of the drop-in's paced ladder (2 pump threads each)")
+    ap.add_argument("--dropin-seconds", type=float, default=3.0)
     args = ap.parse_args()
 
     import torch
@@ -494,6 +726,7 @@ def main():
         wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
         if wf_batch > 1:
             wf.set_batch(wf_batch)
+            wf.set_latency(args.wf_latency_ms)
     chains = [eng.chain(p) for p in plist]
 
     # engine priming before the W warmup steps: the first ~10 blocks of a fresh engine include
@@ -640,20 +873,21 @@ def main():
     wf_traffic_src = "; ".join(sorted(set(wf_traffic_src)))
 
     # fc_mac_lds (LDS-DMA ring) where the GEMM grid takes more than one workgroup per CU, fc_mac
-    # (register operands) otherwise or with OWRX_FC_MAC=reg: the newest PMC summary names which ran
-    mac_name = "fc_mac"
-    traffic, traffic_src = None, "direct-form DDC"
-    for pref in (("fc_mac_lds<", "fc_mac<") if fast else ("ddc_lds<",)):
-        traffic, traffic_src = pmc_traffic(pref, args.config)
-        if traffic is not None:
-            mac_name = pref.rstrip("<")
-            break
+    # (register operands) otherwise or with OWRX_FC_MAC=reg: the engine reports which form its
+    # timed launches took (and the K slices of the ring form); the PMC traffic is that kernel's
+    mac_lds = d["ddc_mac_lds_launches"] > 0
+    mac_name = ("fc_mac_lds" if mac_lds else "fc_mac") if fast else "ddc_lds"
+    mac_kslices = int(s1["ddc_mac_kslices_max"]) if mac_lds else None
+    traffic, traffic_src = pmc_traffic(mac_name + "<", args.config)
+    if not fast:
+        traffic_src = "direct-form DDC: " + traffic_src
     rt = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
         _log("real-time check")
         rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
-                            args.realtime_seconds, 1 << 20, args.ddc)
+                            args.realtime_seconds, 1 << 20, args.ddc, wf_batch=wf_batch,
+                            wf_cap_ms=args.wf_latency_ms)
     churn = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0 and args.churn_chains > 0:
         host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
@@ -662,7 +896,8 @@ def main():
         pc = [params.chain_params(fs, o, cfg["modes"][c % len(cfg["modes"])])
               for c, o in enumerate(carrier_offsets(fs, Cc))]
         churn = realtime_check(Engine, params, fs, n_fft, hop, avg, pc, host,
-                               args.realtime_seconds, 1 << 20, args.ddc, churn=True)
+                               args.realtime_seconds, 1 << 20, args.ddc, churn=True,
+                               wf_batch=wf_batch, wf_cap_ms=args.wf_latency_ms)
     cap = None
     if args.capacity_ladder:
         # every rank: 2 s of the same stream on the host (rank 0 slices its own; the others
@@ -684,7 +919,14 @@ def main():
         cap = max_realtime_chains(Engine, params, fs, n_fft, hop, avg, cfg["modes"],
                                   lambda c: carrier_offsets(fs, c), host,
                                   args.capacity_seconds, 1 << 20, ladder, args.ddc, 150.0,
-                                  agree=agree, world=world)
+                                  agree=agree, world=world, hold_s=args.capacity_hold_seconds,
+                                  wf_batch=wf_batch if world == 1 else 0,
+                                  wf_cap_ms=args.wf_latency_ms)
+    dropin = None
+    if rank == 0 and world == 1 and args.dropin_clients > 0:
+        dropin = dropin_check(fs, args.dropin_clients,
+                              [int(v) for v in args.dropin_ladder.split(",") if v],
+                              args.dropin_seconds, 60.0, 900)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -735,6 +977,8 @@ def main():
                 "frac": round(mac_gbs / HBM_PEAK_GBS if mac_bound == "hbm"
                               else achieved_tf / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
+                "mac_form": mac_name,
+                "k_slices": mac_kslices,
                 "algorithmic_bytes_per_launch": round(mac_bytes_launch) if mac_bytes_launch else None,
                 "algorithmic_flop_per_launch": round(mac_flop_launch) if mac_flop_launch else None,
                 "arithmetic_intensity_flop_per_byte": round(mac_ai, 2) if mac_ai else None,
@@ -776,10 +1020,22 @@ def main():
             "waterfall_batch": {
                 "min_frames": wf_batch,
                 "engine_history_samples": hist,
-                "row_latency_s": round(wf_batch * hop / fs, 3) if wf_batch > 1 else 0.0,
-                "note": "owrx_waterfall_set_batch: the FFT launches once the batch's frames are "
-                        "ready (rows reach the reader up to row_latency_s of stream later than "
-                        "with per-block launches; rows bit-identical for any block cut)",
+                "latency_cap_s": round(args.wf_latency_ms / 1e3, 3) if wf_batch > 1 else None,
+                "row_latency_s": round(s1["wf_row_latency_ms_max"] / 1e3, 4),
+                "row_latency_mean_s": round((s1["wf_row_latency_ms_sum"] - s0["wf_row_latency_ms_sum"])
+                                            / max(1, d["wf_rows_latency_n"]) / 1e3, 4),
+                "batch_stream_span_s": round(wf_batch * hop / fs, 3) if wf_batch > 1 else 0.0,
+                "realtime_row_latency_s": round(rt["waterfall_rows"]["latency_ms_max"] / 1e3, 4)
+                if rt else None,
+                "note": "owrx_waterfall_set_batch: the FFT launches once min_frames frames are "
+                        "ready, or when waiting for the next block would hold a ready frame "
+                        "longer than latency_cap_s of wall clock (owrx_waterfall_set_latency); "
+                        "row_latency_s = the most wall-clock time any row took from the call of "
+                        "the block that completed it to the row in the host ring (engine stats, "
+                        "the whole run).  Fed faster than real time the batch fills in far less "
+                        "than the cap (batch_stream_span_s of stream per launch); at the stream's "
+                        "rate (the paced check, realtime_row_latency_s) the cap launches every "
+                        "block.  Rows are bit-identical for any batching",
             },
             "ddc": {
                 "form": "fast convolution" if fast else "direct",
@@ -811,6 +1067,7 @@ def main():
             "realtime_churn": churn,
             "max_realtime_chains": cap["max_realtime_chains"] if cap else None,
             "capacity": cap,
+            "dropin": dropin,
             "cpu_baseline": cpu,
             "output_bytes": out_bytes,
         }

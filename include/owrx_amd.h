@@ -299,6 +299,10 @@ typedef struct {
     double  wf_row_latency_ms_max;
     double  wf_row_latency_ms_sum;
     int64_t wf_rows_latency_n;
+    /* the fast-convolution GEMM form launched: fc_mac_lds (LDS-DMA ring) launches of all the
+     * fast DDC launches, and the most K slices across workgroups one of them used */
+    int64_t ddc_mac_lds_launches;
+    int64_t ddc_mac_kslices_max;
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

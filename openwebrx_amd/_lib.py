@@ -110,6 +110,8 @@ class Stats(ctypes.Structure):
         ("wf_row_latency_ms_max", ctypes.c_double),
         ("wf_row_latency_ms_sum", ctypes.c_double),
         ("wf_rows_latency_n", ctypes.c_int64),
+        ("ddc_mac_lds_launches", ctypes.c_int64),
+        ("ddc_mac_kslices_max", ctypes.c_int64),
     ]
 
 

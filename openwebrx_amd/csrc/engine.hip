@@ -83,12 +83,14 @@ hipError_t launch_debug_sleep(int64_t us, hipStream_t st);  // synth.hip (stall 
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, int fpg, const float* window, const float* ones,
                          const float2* tw, float* partial, float2* scratch, int* work, int cus,
-                         hipStream_t st);
+                         hipStream_t st, int skip, int tail);
+int wf_tail_split(int logn, int ngroups, int cus);
 bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
 bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_h2 / wf_fft_l32 (not r16)
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
-                              int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st);
+                              int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st,
+                              const WfGroup* groups, int ngroups, int skip);
 hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, int row_bytes,
                            hipStream_t st);
 hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_end,
@@ -108,7 +110,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
-                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1);
+                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form);
 int fc_kslices_max(int M, int nchains, int Dp, int ncu);  // Y slices a group may need
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
                                 const StepTable& steps, hipStream_t st);
@@ -309,7 +311,7 @@ struct Waterfall {
     float2* d_y4 = nullptr;  // N > 16384: DIF-split sub-frames (fpg frames per group) or the
                              // four-step scratch (one cf32 frame per group)
     float* d_ones = nullptr; // DIF split: the sub-frames' window (the split applied the frame's)
-    int* d_work = nullptr;   // wf_fft_l32's work-item counter (zeroed before each launch)
+    int* d_work = nullptr;   // wf_fft_l32's claim + exit counters (left zeroed by each launch)
     int partial_groups = 0;          // groups d_partial / d_groups hold
     WfGroup* h_groups[kSlots] = {};  // pinned copy sources, per slot of the launching block
     WfRow* h_rows[kSlots] = {};
@@ -1489,6 +1491,28 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     // the launching block's slot (its previous user, block k - kSlots, has drained; at
     // owrx_sync every slot has)
     const int bp = (int)(e->block_index % e->nslots);
+    // tail split (wf_fft_l32): the last `skip` groups are also listed frame by frame after the
+    // groups, and the kernel deals those frames instead (the rows do not change)
+    const int ngroups = (int)w->groups.size();
+    const int skip = wf_tail_split(w->logn, ngroups, std::max(1, e->cus_a));
+    int tail = 0;
+    for (int gi = ngroups - skip; gi < ngroups; ++gi) {
+        const WfGroup g = w->groups[gi];
+        for (int j = 0; j < g.nframes; ++j) {
+            w->groups.push_back(WfGroup{g.start + (int64_t)j * g.hop, 1, g.hop});
+            ++tail;
+        }
+    }
+    if (tail) {
+        RCCHK(wf_reserve(e, w, (int)w->groups.size(), (int)w->rowdesc.size(), bp, ri));
+        // each row reaching into the split groups: its first split frame's descriptor (pad)
+        const int g_split = ngroups - skip;
+        for (WfRow& r : w->rowdesc) {
+            r.pad = ngroups;
+            for (int gi = g_split; gi < std::max(g_split, r.first_group); ++gi)
+                r.pad += w->groups[gi].nframes;
+        }
+    }
     memcpy(w->h_groups[bp], w->groups.data(), sizeof(WfGroup) * w->groups.size());
     memcpy(w->h_rows[bp], w->rowdesc.data(), sizeof(WfRow) * w->rowdesc.size());
     HIPCHK(kcopy(w->d_groups, w->h_groups[bp], sizeof(WfGroup) * w->groups.size(), e->sA));
@@ -1498,14 +1522,14 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
         HIPCHK(hipEventRecord(S->w0, e->sA));
         e->stats.waterfall_timed_samples += nfr * w->hop;
     }
-    HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, (int)w->groups.size(), w->fpg,
+    HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, ngroups, w->fpg,
                          w->d_window, w->d_ones, w->d_tw, w->d_partial, w->d_y4, w->d_work,
-                         std::max(1, e->cus_a), e->sA));
+                         std::max(1, e->cus_a), e->sA, skip, tail));
     const float corr = (float)((double)w->add_db - 10.0 * std::log10((double)std::max(1, avg_now)));
     const int cin = w->carry_idx, cout = 1 - w->carry_idx;
     HIPCHK(launch_wf_finalize(w->d_partial, w->d_rows, (int)w->rowdesc.size(), w->d_carry[cin],
                               w->d_carry[cout], w->N, corr, adpcm_now, w->d_s16[ri],
-                              w->d_f32[ri], e->sA));
+                              w->d_f32[ri], e->sA, w->d_groups, ngroups, skip));
     if (tm) {
         HIPCHK(hipEventRecord(S->w1, e->sA));
         S->timed_wff = true;
@@ -1939,12 +1963,15 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         if (gw.fast) {
             // the first fast group's GEMM is timed (one group in the benchmark configurations)
             const bool tm = timed && !S.timed_mac;
+            int form = 0;
             HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, blk_end, g->d_chains, g->d_fc_w,
                                  g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
                                  g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
                                  g->d_fc_y, (int64_t)g->fc_y_elems, g->d_partial[si], e->sA,
                                  tm ? S.m0 : nullptr,
-                                 tm ? S.m1 : nullptr));
+                                 tm ? S.m1 : nullptr, &form));
+            if (form > 0) e->stats.ddc_mac_lds_launches++;
+            e->stats.ddc_mac_kslices_max = std::max<int64_t>(e->stats.ddc_mac_kslices_max, form);
             if (tm) {
                 // algorithmic work of that GEMM: 8 flop per complex MAC over the frames that
                 // carry outputs; bytes = W (every member's spectra) + U + Y, each moved once
@@ -2515,6 +2542,12 @@ int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int
         HIPCHK(palloc(e, &w->d_work, 64));
         HIPCHK(palloc(e, &w->d_carry[0], (size_t)fft_size));
         HIPCHK(palloc(e, &w->d_carry[1], (size_t)fft_size));
+        {
+            // wf_fft_l32's claim and exit counters start at zero (the kernel's last workgroup
+            // zeroes them again for the next launch)
+            const int zero[2] = {0, 0};
+            RCCHK(upload(e, w->d_work, zero, sizeof(zero)));
+        }
         RCCHK(upload(e, w->d_window, win.data(), sizeof(float) * fft_size));
         RCCHK(upload(e, w->d_tw, tw.data(), sizeof(float) * 2 * fft_size));
         if (fft_size > kWfLdsMaxN) {

@@ -657,7 +657,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
                          const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
-                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1) {
+                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form) {
     const int F = (nk + V - 1) / V;
     if (F > Fs || nk <= 0 || nchains <= 0) return hipErrorInvalidValue;
     const dim3 gf(Dp / kFcRT, F);
@@ -701,6 +701,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
     while (ks > 1 && ((Dp >> 3) / kFcKSplit) % ks) --ks;
     const dim3 gk(gm.x * ks);
     const bool ring = lds_ring && (int)gk.x > ncu;
+    if (form) *form = ring ? ks : 0;  // 0: register form; k >= 1: the ring with k K slices
     if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
     if (ring && wide)
         hipLaunchKernelGGL((fc_mac_lds<2, 4, 2>), gk, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y, ks, y_slice);

@@ -640,10 +640,18 @@ OWRX_DEV int wf_swz32(int e) { return e ^ ((e >> 5) & 15); }
 // transforms sub-frame j of its group's frames from the split scratch (blk; sub-frames of one
 // group `fstride` frames apart), its partial row landing at partial + group * (N << qlog) +
 // j * N; tw then is the (N << qlog)-point table, read at stride 1 << qlog.
+//
+// Tail split (qlog = 0): the launch's last `skip` groups also come as single-frame descriptors
+// after the `whole` + `skip` groups (host-built), and item i is descriptor i < whole ? i :
+// i + skip.  Every frame's |X|^2 is added to its accumulator as one rounded value (acc + p, p =
+// fma(y, y, x x)), so a group summed in a workgroup's registers and the same group's frames
+// folded in order by wf_finalize from their own partial rows give the same bits: the split
+// changes no result, only how finely the last round of work is dealt.
 __global__ void __launch_bounds__(WfL32::NT)
 wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
            const float* __restrict__ window, const float2* __restrict__ tw,
-           float* __restrict__ partial, int qlog, int fstride, int items, int* __restrict__ work) {
+           float* __restrict__ partial, int qlog, int fstride, int items, int* __restrict__ work,
+           int whole, int skip) {
     using K = WfL32;
     constexpr int N = K::N, NT = K::NT;
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
@@ -652,16 +660,19 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     WF_RSTAMP(14);
     WF_STAMP(0);
     // Work items (a group's frames, or one sub-frame j of a group after the DIF split) are dealt
-    // dynamically: workgroup b starts on item b, then takes the next unclaimed one from `work`
-    // (zeroed before the launch) until none is left.  With one workgroup per CU a launch of one
-    // item per CU doubled its time whenever some CU was busy or its queue's CU mask left a
-    // shader engine short (measured 85 vs 49 us per 960 C3 frames on a CU-masked stream); now a
-    // late CU only takes fewer items.  An item's rows are still summed by one workgroup in frame
-    // order, so the results do not depend on which workgroup took it.
+    // dynamically: every workgroup, its first item included, takes the next unclaimed one from
+    // `work` (zeroed before the launch) until none is left.  With one workgroup per CU a static
+    // first item (workgroup b on item b) doubled a launch's time whenever some workgroups were
+    // placed late: on a CU-masked queue part of the grid only starts when the first wave of
+    // workgroups retires, and each of those then still ran its own item at the end (measured 88
+    // vs 52 us per 960 C3 frames, and the same with the first items alone static).  A late
+    // workgroup now finds the items taken and exits.  An item's rows are still summed by one
+    // workgroup in frame order, so the results do not depend on which workgroup took it.
     struct Item {
         __amdgpu_buffer_rsrc_t xr;
         int hop, nfr;
     };
+    auto desc = [&](int i) { return i < whole ? i : i + skip; };  // item -> descriptor
     auto item = [&](int w) {
         const int gi = w >> qlog;
         const WfGroup g = groups[gi];
@@ -706,7 +717,23 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         const int e = t0 + NT * i;  // 992 entries: (r - 1) * 32 + k
         t2v[i] = e < 31 * 32 ? tw[(((e >> 5) + 1) * (e & 31)) << (4 + qlog)] : make_float2(0.f, 0.f);
     }
-    int w = blockIdx.x;
+    // work[0] counts claims, work[1] exits: the last workgroup out zeroes both, so the next
+    // launch on the stream finds them zero without a memset in between
+    auto finish = [&]() {
+        __syncthreads();
+        if (t0 == 0 && atomicAdd(work + 1, 1) == (int)gridDim.x - 1) {
+            atomicExch(work, 0);
+            atomicExch(work + 1, 0);
+        }
+    };
+    if (t0 == 0) s_next = atomicAdd(work, 1);
+    __syncthreads();
+    int w = __builtin_amdgcn_readfirstlane(s_next);
+    if (w >= items) {  // uniform: every item is taken
+        finish();
+        return;
+    }
+    w = desc(w);
     Item cur = item(w);
     float2 nx[32];
     load_x(cur.xr, 0, nx);
@@ -717,11 +744,13 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 #pragma unroll 1
     while (true) {
         // claim the item after this one now: its first frame is prefetched during this one's last
-        if (t0 == 0) s_next = (int)gridDim.x + atomicAdd(work, 1);
+        __syncthreads();  // every wave has read s_next (the item it holds) before it changes
+        if (t0 == 0) s_next = atomicAdd(work, 1);
         __syncthreads();
-        const int wn = __builtin_amdgcn_readfirstlane(s_next);
-        const bool has_next = wn < items;
-        const Item nxt = item(has_next ? wn : w);
+        const int wi = __builtin_amdgcn_readfirstlane(s_next);
+        const bool has_next = wi < items;
+        const int wn = has_next ? desc(wi) : w;
+        const Item nxt = item(wn);
         float acc[32];
 #pragma unroll
         for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
@@ -796,11 +825,11 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
                 f2dft<16>(c);
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    acc[b + 2 * r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b + 2 * r]));
+                    acc[b + 2 * r] = acc[b + 2 * r] + fmaf(c[r].y, c[r].y, c[r].x * c[r].x);
             }
             if (f < 2) WF_STAMP(sb + 5);
         }
-        float* out = partial + (int64_t)w * N;  // = group * (N << qlog) + j * N
+        float* out = partial + (int64_t)w * N;  // = group * (N << qlog) + j * N, or descriptor w
 #pragma unroll
         for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
         if (!has_next) break;
@@ -809,6 +838,7 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     }
     WF_STAMP(13);
     WF_RSTAMP(15);
+    finish();
 }
 
 // ---- wf_fft_h2: N = 16384 as two 8192-point halves, two workgroups per CU ------------------
@@ -1108,7 +1138,8 @@ __global__ void __launch_bounds__(256)
 wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
             const float* __restrict__ carry_in, float* __restrict__ carry_out, int N,
             float add_corr, int adpcm, int16_t* __restrict__ s16_out,
-            float* __restrict__ f32_out, int qlog) {
+            float* __restrict__ f32_out, int qlog, const WfGroup* __restrict__ groups,
+            int ngroups, int skip) {
 #pragma clang fp contract(off)
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
@@ -1117,17 +1148,57 @@ wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
     // bin i's place in a partial row: natural, or j-major after the DIF split (bin Q k + j at
     // j (N / Q) + k)
     const int pi = qlog ? ((i & ((1 << qlog) - 1)) * (N >> qlog)) + (i >> qlog) : i;
-    // the groups' partials in order (the row's summation order); loads batched 8 deep
+    // the groups' partials in order (the row's summation order); loads batched 16 deep
     const float* pp = partial + (int64_t)r.first_group * N + pi;
+    // groups [ngroups - skip, ngroups) were transformed frame by frame (wf_fft_l32's tail
+    // split): their frames' partial rows follow the groups', folded here in frame order into the
+    // group's sum first, as the workgroup would have
+    const int g_split = ngroups - skip;
+    const int n_whole = max(0, min(r.ngroups, g_split - r.first_group));
     int gi = 0;
-    for (; gi + 8 <= r.ngroups; gi += 8) {
+    for (; gi + 16 <= n_whole; gi += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = pp[(int64_t)(gi + u) * N];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    if (gi + 8 <= n_whole) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = pp[(int64_t)(gi + u) * N];
 #pragma unroll
         for (int u = 0; u < 8; ++u) s += v[u];
+        gi += 8;
     }
-    for (; gi < r.ngroups; ++gi) s += pp[(int64_t)gi * N];
+    for (; gi < n_whole; ++gi) s += pp[(int64_t)gi * N];
+    if (gi < r.ngroups) {
+        // (loads issued eight groups' frame counts and up to four frames at a time: a serial
+        // chain of dependent L2 reads per group cost tens of us per launch)
+        int f0 = r.pad;  // the row's first split frame's descriptor (host-computed)
+        for (; gi < r.ngroups; gi += 8) {
+            int nfv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                nfv[u] = gi + u < r.ngroups ? groups[r.first_group + gi + u].nframes : 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int nf = nfv[u];
+                if (nf == 0) break;
+                const float* fp = partial + (int64_t)f0 * N + pi;
+                float v[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = j < nf ? fp[(int64_t)j * N] : 0.0f;
+                float g = v[0];
+#pragma unroll
+                for (int j = 1; j < 4; ++j)
+                    if (j < nf) g = g + v[j];
+                for (int j = 4; j < nf; ++j) g = g + fp[(int64_t)j * N];
+                s += g;
+                f0 += nf;
+            }
+        }
+    }
     if (!r.complete) {
         carry_out[i] = s;
         return;
@@ -1275,7 +1346,7 @@ bool wf_uses_split(int logn) {
 static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw,
                                  float* partial, int* work, int cus, hipStream_t st, int qlog = 0,
-                                 int fstride = 0) {
+                                 int fstride = 0, int skip = 0, int tail = 0) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)wf_fft_l32,
@@ -1284,15 +1355,34 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
         if (e != hipSuccess) return e;
         attr = true;
     }
-    if (!work) return hipErrorInvalidValue;
-    const int items = ngroups << qlog;
-    hipError_t e = hipMemsetAsync(work, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
+    if (!work || skip < 0 || skip > ngroups || (qlog && (skip || tail))) return hipErrorInvalidValue;
+    // items: the whole groups, then the split groups' frames (descriptors ngroups ..)
+    const int whole = (ngroups - skip) << qlog;
+    const int items = whole + tail;
     // one workgroup per CU (the 136 KiB image), at most one per item
     const int grid = std::max(1, std::min(items, cus));
     hipLaunchKernelGGL(wf_fft_l32, dim3(grid), dim3(WfL32::NT), WfL32::kLds, st, blk, blk_start,
-                       groups, window, tw, partial, qlog, fstride, items, work);
+                       groups, window, tw, partial, qlog, fstride, items, work, whole, skip);
     return hipGetLastError();
+}
+
+// the tail split of a wf_fft_l32 launch of `ngroups` groups on `cus` CUs: how many of the last
+// groups go frame by frame.  The workgroups placed at once on a CU-masked queue are fewer than
+// its CUs (measured 227-230 of 240 for the engine's stream-A mask: the dispatcher's per-engine
+// share), so a launch of one item per CU ran its last items in a second round, doubling its time
+// (89 vs 52 us per 960 C3 frames); the groups that would start that round, plus an eighth of a
+// round, are dealt as single frames instead.  0 for the other kernels.
+int wf_tail_split(int logn, int ngroups, int cus) {
+    if (logn != 14 || wf_n16k_kernel() != 1 || cus < 8 || ngroups < 2) return 0;
+    static const int mode = [] {
+        const char* s = getenv("OWRX_WF_TAIL");
+        return s ? atoi(s) : -1;
+    }();
+    if (mode == 0) return 0;
+    const int lo = cus - cus / 8;
+    if (ngroups <= lo) return 0;
+    const int s = ngroups <= cus ? ngroups - lo : ngroups % cus + cus / 8;
+    return std::min(s, ngroups);
 }
 
 // N = 16384 << QLOG: the split into sub-frames, then wf_fft_l32 on them (window of ones: the
@@ -1328,12 +1418,13 @@ static hipError_t launch_fft_h2(const float2* blk, int64_t blk_start, const WfGr
 template <int LOGN>
 static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw, float* partial,
-                                 int* work, int cus, hipStream_t st) {
+                                 int* work, int cus, hipStream_t st, int skip, int tail) {
     if constexpr (LOGN == 14) {
         if (wf_uses_h2(LOGN))
             return launch_fft_h2(blk, blk_start, groups, ngroups, window, tw, partial, st);
         if (!wf_force_r16())
-            return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
+            return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
+                                  0, 0, skip, tail);
     }
     return launch_fft_r16<LOGN>(blk, blk_start, groups, ngroups, window, tw, partial, st);
 }
@@ -1342,7 +1433,10 @@ static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfG
 hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const WfGroup* groups,
                          int ngroups, int fpg, const float* window, const float* ones,
                          const float2* tw, float* partial, float2* scratch, int* work, int cus,
-                         hipStream_t st) {
+                         hipStream_t st, int skip, int tail) {
+    if ((skip || tail) && logn != 14) return hipErrorInvalidValue;
+    if (logn == 14) return launch_fft_sel<14>(blk, blk_start, groups, ngroups, window, tw, partial,
+                                              work, cus, st, skip, tail);
     if (wf_uses_split(logn))
         return logn == 15 ? launch_fft_split<1>(blk, blk_start, groups, ngroups, fpg, window, ones, tw,
                                                 partial, scratch, work, cus, st)
@@ -1351,11 +1445,11 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
     switch (logn) {
         case 8: return launch_fft_t<8>(blk, blk_start, groups, ngroups, window, tw, partial, st);
         case 9: return launch_fft_t<9>(blk, blk_start, groups, ngroups, window, tw, partial, st);
-        case 10: return launch_fft_sel<10>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
-        case 11: return launch_fft_sel<11>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
-        case 12: return launch_fft_sel<12>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
-        case 13: return launch_fft_sel<13>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
-        case 14: return launch_fft_sel<14>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st);
+        case 10: return launch_fft_sel<10>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st, 0, 0);
+        case 11: return launch_fft_sel<11>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st, 0, 0);
+        case 12: return launch_fft_sel<12>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st, 0, 0);
+        case 13: return launch_fft_sel<13>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st, 0, 0);
+        case 14: return launch_fft_sel<14>(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st, 0, 0);
         case 15: return launch_fft4_t<7, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
                                             scratch, st);
         case 16: return launch_fft4_t<8, 8>(blk, blk_start, groups, ngroups, window, tw, partial,
@@ -1366,13 +1460,15 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
 
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
-                              int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st) {
+                              int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st,
+                              const WfGroup* groups, int ngroups, int skip) {
     int logn = 0;
     while ((1 << logn) < N) ++logn;
     // partial rows half- / sub-frame-major: the DIF split's Q = N / 16384, wf_fft_h2's Q = 2
     const int qlog = wf_uses_split(logn) ? logn - 14 : wf_uses_h2(logn) ? 1 : 0;
     hipLaunchKernelGGL(wf_finalize, dim3((N + 255) / 256, nrows), dim3(256), 0, st, partial,
-                       rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out, qlog);
+                       rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out, qlog,
+                       groups, ngroups, skip);
     return hipGetLastError();
 }
 

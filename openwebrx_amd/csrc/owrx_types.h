@@ -20,7 +20,7 @@ struct WfRow {
     int32_t use_carry;   // add the carried accumulator first
     int32_t complete;    // emit the row (else store the sum into the carry)
     int32_t out_index;   // row slot in the output staging buffer
-    int32_t pad;
+    int32_t pad;         // wf_fft_l32 tail split: the descriptor of the row's first split frame
 };
 
 // ---- DDC (Shift + FirDecimate, fused, all chains of one (D, taps) group) ----------------

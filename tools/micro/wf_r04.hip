@@ -80,6 +80,12 @@ static bool flush_on() {
     static const bool v = !getenv("OWRX_WF_FLUSH") || atoi(getenv("OWRX_WF_FLUSH"));
     return v;
 }
+#ifdef OWRX_WF_STAMPS
+__global__ void mark_rt(unsigned long long* out, int i) {
+    if (threadIdx.x == 0) out[i] = __builtin_amdgcn_s_memrealtime();
+}
+#endif
+
 static double time_us(const std::function<void()>& launch, hipStream_t stream = 0) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -131,10 +137,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dtw, sizeof(float2) * N));
     CK(hipMalloc(&dwin, sizeof(float) * N));
     CK(hipMalloc(&dref, sizeof(float) * (size_t)FTmax * N));
-    CK(hipMalloc(&dpart, sizeof(float) * (size_t)FTmax * N));
-    CK(hipMalloc(&dg, sizeof(WfGroup) * FTmax));
+    CK(hipMalloc(&dpart, sizeof(float) * (size_t)2 * FTmax * N));
+    CK(hipMalloc(&dg, sizeof(WfGroup) * 2 * FTmax));
     int* dwork;
     CK(hipMalloc(&dwork, 64));
+    CK(hipMemset(dwork, 0, 64));
     CK(hipMemcpy(dx, x.data(), sizeof(float2) * S, hipMemcpyHostToDevice));
     CK(hipMemcpy(dtw, tw.data(), sizeof(float2) * N, hipMemcpyHostToDevice));
     CK(hipMemcpy(dwin, win.data(), sizeof(float) * N, hipMemcpyHostToDevice));
@@ -166,10 +173,10 @@ int main(int argc, char** argv) {
         std::vector<uint32_t> all(words, 0xffffffffu);
         CK(hipExtStreamCreateWithCUMask(&s_all, words, all.data()));
     }
-    auto l32 = [&](int G, hipStream_t st) {
-        CK(hipMemsetAsync(dwork, 0, sizeof(int), st));
-        hipLaunchKernelGGL(wf_fft_l32, dim3(std::min(G, st == 0 || st == s_plain || st == s_all ? 256 : 240)), dim3(WfL32::NT), WfL32::kLds, st, dx, (int64_t)0,
-                           dg, dwin, dtw, dpart, 0, 0, G, dwork);
+    auto l32 = [&](int G, hipStream_t st, int skip = 0, int tail = 0) {
+        const int items = G - skip + tail;  // (the counters are left zeroed by each launch)
+        hipLaunchKernelGGL(wf_fft_l32, dim3(std::min(items, st == 0 || st == s_plain || st == s_all ? 256 : 240)), dim3(WfL32::NT), WfL32::kLds, st, dx, (int64_t)0,
+                           dg, dwin, dtw, dpart, 0, 0, items, dwork, G - skip, skip);
     };
     printf("CUs %d\n", ncu);
     for (int FT : fts) {
@@ -178,7 +185,40 @@ int main(int argc, char** argv) {
             const int G = (FT + F - 1) / F;
             std::vector<WfGroup> grp(G);
             for (int g = 0; g < G; ++g) grp[g] = WfGroup{(int64_t)g * F * hop, std::min(F, FT - g * F), hop};
-            CK(hipMemcpy(dg, grp.data(), sizeof(WfGroup) * G, hipMemcpyHostToDevice));
+            // the engine's tail split for a 240-CU stream: the last S groups also frame by frame
+            const int S = wf_tail_split(14, G, 240);
+            int T = 0;
+            for (int g = G - S; g < G; ++g)
+                for (int j = 0; j < grp[g].nframes; ++j, ++T)
+                    grp.push_back(WfGroup{grp[g].start + (int64_t)j * hop, 1, hop});
+            CK(hipMemcpy(dg, grp.data(), sizeof(WfGroup) * grp.size(), hipMemcpyHostToDevice));
+            {
+                // bit identity: a split group's frames folded in order == the group's own sum
+                l32(G, 0);
+                CK(hipDeviceSynchronize());
+                std::vector<float> A((size_t)G * N), B((size_t)(G + T) * N);
+                CK(hipMemcpy(A.data(), dpart, sizeof(float) * A.size(), hipMemcpyDeviceToHost));
+                l32(G, 0, S, T);
+                CK(hipDeviceSynchronize());
+                CK(hipMemcpy(B.data(), dpart, sizeof(float) * B.size(), hipMemcpyDeviceToHost));
+                size_t bad = 0;
+                int f0 = G;
+                for (int g = 0; g < G; ++g) {
+                    for (int k = 0; k < N; ++k) {
+                        float v;
+                        if (g < G - S) {
+                            v = B[(size_t)g * N + k];
+                        } else {
+                            v = B[(size_t)f0 * N + k];
+                            for (int j = 1; j < grp[g].nframes; ++j) v = v + B[(size_t)(f0 + j) * N + k];
+                        }
+                        bad += memcmp(&v, &A[(size_t)g * N + k], 4) != 0;
+                    }
+                    if (g >= G - S) f0 += grp[g].nframes;
+                }
+                printf("FT=%5d F=%d G=%4d tail split S=%d groups (%d frames): %zu of %zu partial bins differ from the unsplit launch\n",
+                       FT, F, G, S, T, bad, (size_t)G * N);
+            }
             hipLaunchKernelGGL(wf_fft_r16<14>, dim3(G), dim3(WfR16<14>::NT), WfR16<14>::kLds, 0, dx, (int64_t)0,
                                dg, dwin, dtw, dref);
             CK(hipDeviceSynchronize());
@@ -202,6 +242,12 @@ int main(int argc, char** argv) {
                 {"l32 mask[0,240)", [&] {
                      l32(G, s_lo);
                  }, false, false, s_lo},
+                {"l32 tail mask[0,240)", [&] {
+                     l32(G, s_lo, S, T);
+                 }, false, false, s_lo},
+                {"l32 tail plain", [&] {
+                     l32(G, s_plain, S, T);
+                 }, false, false, s_plain},
                 {"l32 mask[16,256)", [&] {
                      l32(G, s_hi);
                  }, false, false, s_hi},
@@ -277,6 +323,42 @@ int main(int argc, char** argv) {
                     }
                     printf("   frame 2.. to end: %lld\n", med(12, 13));
                 };
+                // l32 on a plain and on a CU-masked stream: per-workgroup start and end (realtime)
+                unsigned long long* dmark = nullptr;
+                CK(hipMalloc(&dmark, 64));
+                for (hipStream_t sq : {s_plain, s_lo}) {
+                    time_us([&] {
+                        hipLaunchKernelGGL(mark_rt, dim3(1), dim3(64), 0, sq, dmark, 0);
+                        l32(G, sq);
+                        hipLaunchKernelGGL(mark_rt, dim3(1), dim3(64), 0, sq, dmark, 1);
+                    }, sq);
+                    unsigned long long mk[2];
+                    CK(hipMemcpy(mk, dmark, 16, hipMemcpyDeviceToHost));
+                    std::vector<unsigned long long> st((size_t)1024 * 16);
+                    CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wf_stamp), sizeof(unsigned long long) * st.size()));
+                    const int nwg = std::min(G, sq == s_plain ? 256 : 240);
+                    unsigned long long t0m = ~0ull;
+                    for (int q = 0; q < nwg; ++q) t0m = std::min(t0m, st[q * 16 + 14]);
+                    std::vector<double> a0, a1, du;
+                    for (int q = 0; q < nwg; ++q) {
+                        a0.push_back((st[q * 16 + 14] - t0m) / 100.0);
+                        a1.push_back((st[q * 16 + 15] - t0m) / 100.0);
+                        du.push_back((st[q * 16 + 15] - st[q * 16 + 14]) / 100.0);
+                    }
+                    auto pr = [&](const char* nm, std::vector<double> v) {
+                        std::sort(v.begin(), v.end());
+                        printf("  %s p0 %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f", nm, v[0], v[v.size() / 10],
+                               v[v.size() / 2], v[v.size() * 9 / 10], v.back());
+                    };
+                    printf("   l32 %s: first workgroup %.1f us after the marker before, marker after at %.1f us\n",
+                           sq == s_plain ? "plain" : "mask[0,240)", ((long long)t0m - (long long)mk[0]) / 100.0,
+                           ((long long)mk[1] - (long long)mk[0]) / 100.0);
+                    printf("   l32 %s wg us:", sq == s_plain ? "plain" : "mask[0,240)");
+                    pr("start", a0);
+                    pr("end", a1);
+                    pr("dur", du);
+                    printf("\n");
+                }
                 stamps("x0", G, [&] { hipLaunchKernelGGL(wf_fft_l32x<0>, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, dg, dwin, dtw, dpart); });
                 stamps("h2", 2 * G, [&] { hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx, (int64_t)0, dg, G, dwin, dtw, dpart); });
             }
