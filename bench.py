@@ -664,6 +664,9 @@ def main():
     ap.add_argument("--dropin-ladder", default="256,384",
                     help="client counts of the drop-in's paced ladder (2 pump threads each)")
     ap.add_argument("--dropin-seconds", type=float, default=3.0)
+    ap.add_argument("--loop-blocks", type=int, default=0,
+                    help="A/B: the recording holds this many blocks and the stream loops over "
+                         "them (0: one recording as long as the run)")
     args = ap.parse_args()
 
     import torch
@@ -737,9 +740,11 @@ def main():
     prime = max(0, -(-(12 - args.warmup * bps) // bps))  # priming steps: >= 12 untimed blocks
     nsteps = prime + args.warmup + args.steps
     total = nsteps * bps * block
+    loop = args.loop_blocks if 0 < args.loop_blocks < nsteps * bps else 0
+    span = loop * block if loop else total  # samples of the recording after the history
     stream = None
     if rank == 0:
-        stream = gen_stream_torch(torch, dev, fs, hist + total, modes, offs)
+        stream = gen_stream_torch(torch, dev, fs, hist + span, modes, offs)
         base = stream.data_ptr() + 8 * hist
     bcast = IqBroadcast(torch, dist, dev, hist, block, stream=stream) if dist else None
     torch.cuda.synchronize(dev)
@@ -767,7 +772,7 @@ def main():
         for j in range(i * bps, (i + 1) * bps):
             if world == 1:
                 t0 = time.perf_counter()
-                eng.process_device(base + 8 * j * block, block)
+                eng.process_device(base + 8 * (j % loop if loop else j) * block, block)
                 dt_ = time.perf_counter() - t0
                 host_s["process"] += dt_
                 if i >= prime + args.warmup:
@@ -814,7 +819,7 @@ def main():
     s1 = eng.stats()
     xblock = None
     if world == 1 and args.extra_block and args.extra_block != block:
-        xblock = extra_block_run(Engine, fs, n_fft, hop, avg, wf_batch, plist, stream, total,
+        xblock = extra_block_run(Engine, fs, n_fft, hop, avg, wf_batch, plist, stream, span,
                                  args.extra_block, args.no_waterfall)
     gc.enable()
     if dist:
@@ -883,14 +888,14 @@ def main():
         traffic_src = "direct-form DDC: " + traffic_src
     rt = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0:
-        host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        host = stream[hist:hist + min(span, int(fs * 2))].cpu().numpy()
         _log("real-time check")
         rt = realtime_check(Engine, params, fs, n_fft, hop, avg, plist, host,
                             args.realtime_seconds, 1 << 20, args.ddc, wf_batch=wf_batch,
                             wf_cap_ms=args.wf_latency_ms)
     churn = None
     if rank == 0 and world == 1 and args.realtime_seconds > 0 and args.churn_chains > 0:
-        host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+        host = stream[hist:hist + min(span, int(fs * 2))].cpu().numpy()
         Cc = args.churn_chains
         _log("paced churn check: %d chains" % Cc)
         pc = [params.chain_params(fs, o, cfg["modes"][c % len(cfg["modes"])])
@@ -903,7 +908,7 @@ def main():
         # every rank: 2 s of the same stream on the host (rank 0 slices its own; the others
         # generate it, the synthetic source being deterministic)
         if stream is not None:
-            host = stream[hist:hist + min(total, int(fs * 2))].cpu().numpy()
+            host = stream[hist:hist + min(span, int(fs * 2))].cpu().numpy()
         else:
             host = gen_stream_torch(torch, dev, fs, hist + int(fs * 2), modes, offs)[hist:].cpu().numpy()
         ladder = [int(v) for v in args.capacity_ladder.split(",") if v]
@@ -1054,6 +1059,7 @@ def main():
                 "post_to_encoder_end": round(d["gpu_ms_serial"] / tsteps, 3),
                 "timed_blocks": d["timed_blocks"],
             },
+            "pool_allocs_timed": int(d["pool_allocs"]),
             "host_ms_per_block": {k[8:]: round(d[k] / (args.steps * bps), 3) for k in
                                  ("host_ms_process", "host_ms_wait_input", "host_ms_wait_slots",
                                   "host_ms_wait_rows", "host_ms_build", "host_ms_launch",

@@ -303,6 +303,10 @@ typedef struct {
      * fast DDC launches, and the most K slices across workgroups one of them used */
     int64_t ddc_mac_lds_launches;
     int64_t ddc_mac_kslices_max;
+    /* device (hipMalloc) and pinned (hipHostMalloc) allocations made by the engine's pools so
+     * far: none should happen while blocks stream, since each stalls the GPU's running kernels */
+    int64_t pool_allocs;
+    double  gpu_ms_waterfall_fft_max;  /* the longest timed waterfall FFT + finalize launch */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

@@ -112,6 +112,8 @@ class Stats(ctypes.Structure):
         ("wf_rows_latency_n", ctypes.c_int64),
         ("ddc_mac_lds_launches", ctypes.c_int64),
         ("ddc_mac_kslices_max", ctypes.c_int64),
+        ("pool_allocs", ctypes.c_int64),
+        ("gpu_ms_waterfall_fft_max", ctypes.c_double),
     ]
 
 

@@ -501,10 +501,11 @@ struct Slot {  // one block's outputs in flight on streams B / C
 };
 
 struct RowSlot {  // one block's waterfall rows being encoded / copied on stream R
-    hipStream_t stream = nullptr;  // own stream on the R CUs (row slots encode concurrently)
+    hipStream_t stream = nullptr;  // the row queue (W CUs), shared by the row slots
     hipEvent_t evWf = nullptr;  // stream A finished the block's finalize
     hipEvent_t evC = nullptr;   // rows copied to host
     bool pending = false;
+    bool shared_stream = false;  // another row slot's stream (one row queue by default)
 };
 
 
@@ -625,9 +626,10 @@ struct GroupWork {
 
 struct owrx_engine {
     int device = 0;
-    // A: waterfall FFT + DDC + post_parallel; B: post_serial_front; C: ADPCM + output copies;
-    // R: waterfall row encoding + copies.  Four streams = the four hardware queues HIP gives a
-    // process (GPU_MAX_HW_QUEUES), so no two of them serialise on a shared queue.
+    // A: waterfall FFT + DDC + post_parallel; B: post_serial_front; C: ADPCM; R: output
+    // gathers + copies; the row slots' queue: waterfall row encoding + copies.  Each is a
+    // CU-masked HSA queue of its own (none serialise on a shared queue); create_streams orders
+    // them so A, B and C each have a CP pipe to themselves.
     hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sR = nullptr;
     // unmasked twins of B and C: past kWideSerialChains chains the serial kernels are
     // throughput-bound on their few CUs and spread over the chip instead (serial_wide)
@@ -637,6 +639,7 @@ struct owrx_engine {
     double samp_rate = 0;
     int64_t max_block = 0;
     int cus_a = 0;  // CUs of stream A (DDC launch shape)
+    std::vector<float> wf_ms_log;  // timed waterfall launches (OWRX_WF_LOG=1: printed at destroy)
     int64_t history = kDefaultHistory;
     int64_t pos = 0;  // absolute samples processed
     int64_t block_index = 0;
@@ -804,6 +807,7 @@ static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
         const hipError_t r = hipMalloc(&q, bytes);
         if (r != hipSuccess) return r;
         e->pool_size[q] = bytes;
+        e->stats.pool_allocs++;
     }
     *p = static_cast<T*>(q);
     return hipMemsetAsync(q, 0, bytes, e->sA);
@@ -830,6 +834,7 @@ static hipError_t hpalloc(owrx_engine* e, T** p, size_t count) {
     const hipError_t r = hipHostMalloc(&q, bytes, 0);
     if (r != hipSuccess) return r;
     e->hpool_size[q] = bytes;
+    e->stats.pool_allocs++;
     *p = static_cast<T*>(q);
     return hipSuccess;
 }
@@ -1064,7 +1069,11 @@ static int drain_slot(owrx_engine* e, int si) {
     if (s.timed_wff) {
         float ms = 0;
         RCCHK(wait_ev(e, s.w1));
-        if (hipEventElapsedTime(&ms, s.w0, s.w1) == hipSuccess) e->stats.gpu_ms_waterfall_fft += ms;
+        if (hipEventElapsedTime(&ms, s.w0, s.w1) == hipSuccess) {
+            e->stats.gpu_ms_waterfall_fft += ms;
+            e->stats.gpu_ms_waterfall_fft_max = std::max<double>(e->stats.gpu_ms_waterfall_fft_max, ms);
+            if (e->wf_ms_log.size() < 4096) e->wf_ms_log.push_back((float)ms);
+        }
         s.timed_wff = false;
     }
     return OWRX_OK;
@@ -1141,8 +1150,8 @@ static int drain_all(owrx_engine* e) {
 // Launch capacity of a waterfall (no drain: reconfiguration and joins run while blocks are in
 // flight).  Buffers only grow, geometrically; a grown stream-A buffer replaces the old one for
 // launches from now on and the old one returns to the pool once the blocks that used it
-// drained.  The pinned copy sources of slot bp and the buffers of row slot ri are idle when a
-// launch stages into them (their previous users drained), so they are swapped at once.
+// drained; so are the pinned copy sources of slot bp (by block) and the buffers of row slot ri
+// (by row slot), so a reservation may run while blocks are in flight.
 static int wf_reserve(owrx_engine* e, Waterfall* w, int groups, int rows, int bp, int ri) {
     groups = std::max(groups, 1);
     rows = std::max(rows, 1);
@@ -1165,18 +1174,18 @@ static int wf_reserve(owrx_engine* e, Waterfall* w, int groups, int rows, int bp
     }
     if (bp >= 0 && std::max(groups, rows + 1) > w->h_cap[bp]) {
         const int cap = std::max(w->partial_groups, w->rows_cap);
-        hprel_now(e, w->h_groups[bp]);
-        hprel_now(e, w->h_rows[bp]);
+        hprel(e, w->h_groups[bp]);
+        hprel(e, w->h_rows[bp]);
         HIPCHK(hpalloc(e, &w->h_groups[bp], (size_t)cap));
         HIPCHK(hpalloc(e, &w->h_rows[bp], (size_t)cap));
         w->h_cap[bp] = cap;
     }
     if (ri >= 0 && rows > w->row_slot_cap[ri]) {
         const int cap = std::max(rows, w->row_slot_cap[ri] + w->row_slot_cap[ri] / 2);
-        prel_now(e, w->d_s16[ri]);
-        prel_now(e, w->d_f32[ri]);
-        prel_now(e, w->d_bytes[ri]);
-        hprel_now(e, w->h_bytes[ri]);
+        rowrel(e, w->d_s16[ri], false);
+        rowrel(e, w->d_f32[ri], false);
+        rowrel(e, w->d_bytes[ri], false);
+        rowrel(e, w->h_bytes[ri], true);
         HIPCHK(palloc(e, &w->d_s16[ri], (size_t)cap * w->N));
         HIPCHK(palloc(e, &w->d_f32[ri], (size_t)cap * w->N));
         HIPCHK(palloc(e, &w->d_bytes[ri], (size_t)cap * 4 * w->N));
@@ -1186,13 +1195,22 @@ static int wf_reserve(owrx_engine* e, Waterfall* w, int groups, int rows, int bp
     return OWRX_OK;
 }
 
-// the launch sizes a waterfall expects (its first launches then allocate nothing)
+// the launch sizes a waterfall expects, for every block slot and row slot (its launches then
+// allocate nothing: a hipMalloc / hipHostMalloc mid-stream maps pages into the GPU's address
+// space, and the launches around one ran several times slower, measured 0.5-1 ms of stalled
+// kernels per allocation).  Descriptors: the groups plus the tail split's single frames.
 static int wf_initial_reserve(owrx_engine* e, Waterfall* w) {
     const int64_t span = w->batch_min > 1 ? e->history + e->max_block : e->max_block;
-    const int64_t frames = span / std::max(1, w->hop) + 2;
-    const int groups = (int)(frames / std::max(1, w->fpg) + frames / std::max(1, w->avg) + 4);
-    const int rows = (int)(frames / std::max(1, w->avg) + 3);
-    return wf_reserve(e, w, groups, rows, -1, -1);
+    const int hop = std::max(1, w->pending ? std::min(w->hop, w->new_hop) : w->hop);
+    const int avg = std::max(1, w->pending ? std::min(w->avg, w->new_avg) : w->avg);
+    const int64_t frames = span / hop + 2;
+    const int groups = (int)(frames / std::max(1, w->fpg) + frames / avg + 4);
+    const int rows = (int)(frames / avg + 3);
+    const int descs = groups + (int)frames;
+    RCCHK(wf_reserve(e, w, descs, rows, -1, -1));
+    for (int bp = 0; bp < kSlots; ++bp) RCCHK(wf_reserve(e, w, descs, rows, bp, -1));
+    for (int ri = 0; ri < kRowSlots; ++ri) RCCHK(wf_reserve(e, w, descs, rows, -1, ri));
+    return OWRX_OK;
 }
 
 static int ensure_post_capacity(owrx_engine* e) {
@@ -2146,9 +2164,7 @@ static hipError_t create_streams(owrx_engine* e) {
         err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
         if (err != hipSuccess) return err;
     }
-    // R (8 CUs) holds the output gathers and the waterfall row encoders: one stream per row
-    // slot, so the rows of consecutive blocks (independent: FftAdpcm restarts every row)
-    // encode concurrently instead of queueing behind each other
+    // B, C: the serial demodulator stages; R: the output gathers; W: the waterfall row encoders
     int nb = 4, nc = 4, nr = 4, nw = 4;
     if (const char* v = getenv("OWRX_SERIAL_CUS")) {
         const int k = sscanf(v, "%d,%d,%d,%d", &nb, &nc, &nr, &nw);
@@ -2180,6 +2196,26 @@ static hipError_t create_streams(owrx_engine* e) {
     const std::vector<uint32_t> mC = mask_range(a_end + nb, a_end + nb + nc);
     const std::vector<uint32_t> mR = mask_range(a_end + nb + nc, a_end + nb + nc + nr);
     const std::vector<uint32_t> mW = nw > 0 ? mask_range(a_end + nb + nc + nr, ncu) : mR;
+    // Hardware queues and the command processor's pipes.  Every CU-masked stream is an HSA
+    // queue of its own, and a process's queues are spread over the CP's four compute pipes in
+    // creation order (measured: the 1st, 5th and 9th masked queue share one).  A queue holding a
+    // cross-queue wait (hipStreamWaitEvent's barrier packet) slows the dispatch of a busy queue
+    // on the same pipe: with the four row-slot queues created after A, B, C and R, every launch
+    // whose rows went to the first of them (A's pipe) ran its waterfall FFT + finalize in
+    // 0.15-0.20 ms instead of 0.072 and the following DDC launch up to 8x slower, and the
+    // others (B's and C's pipes) slowed the serial stages (profiles/r04_pipe_layout_ab.txt).
+    // So the row encoders get one queue, created first: it shares a pipe with R only (both
+    // mostly waiting), and A, B and C each have a pipe to themselves.  All row slots encode on
+    // it in order (~1 ms per 960-frame batch, one batch per ~2 ms at C3).  OWRX_ROW_STREAMS=4
+    // restores the four row queues after R (A/B).
+    static const int row_streams = [] {
+        const char* v = getenv("OWRX_ROW_STREAMS");
+        return v ? std::max(1, std::min(kRowSlots, atoi(v))) : 1;
+    }();
+    if (row_streams == 1) {
+        err = hipExtStreamCreateWithCUMask(&e->rslots[0].stream, (uint32_t)words, mW.data());
+        if (err != hipSuccess) return err;
+    }
     const std::pair<hipStream_t*, const std::vector<uint32_t>*> sm[] = {
         {&e->sA, &mA}, {&e->sB, &mB}, {&e->sC, &mC}, {&e->sR, &mR}};
     // OWRX_MASK_A=0: stream A on every CU (the serial streams keep their own; A's waves may
@@ -2197,9 +2233,15 @@ static hipError_t create_streams(owrx_engine* e) {
         }
         if (err != hipSuccess) return err;
     }
-    for (auto& r : e->rslots) {
-        err = hipExtStreamCreateWithCUMask(&r.stream, (uint32_t)words, mW.data());
-        if (err != hipSuccess) return err;
+    for (int i = 0; i < kRowSlots; ++i) {
+        auto& r = e->rslots[i];
+        if (i >= row_streams) {
+            r.stream = e->rslots[i % row_streams].stream;
+            r.shared_stream = true;
+        } else if (row_streams > 1) {
+            err = hipExtStreamCreateWithCUMask(&r.stream, (uint32_t)words, mW.data());
+            if (err != hipSuccess) return err;
+        }
     }
     return hipSuccess;
 }
@@ -2276,6 +2318,11 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
 int owrx_engine_destroy(owrx_engine* e) {
     if (!e) return OWRX_EINVAL;
     hipSetDevice(e->device);
+    if (getenv("OWRX_WF_LOG") && !e->wf_ms_log.empty()) {
+        fprintf(stderr, "owrx waterfall launches (ms):");
+        for (float v : e->wf_ms_log) fprintf(stderr, " %.3f", v);
+        fprintf(stderr, "\n");
+    }
     // every stream drained, within the stall bound (a stalled engine gets one more bound to
     // finish; if its work still has not completed, its buffers are leaked rather than freed
     // under a running kernel, and the process keeps going)
@@ -2317,7 +2364,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     for (auto& r : e->rslots) {
         if (r.evWf) hipEventDestroy(r.evWf);
         if (r.evC) hipEventDestroy(r.evC);
-        if (r.stream) hipStreamDestroy(r.stream);
+        if (r.stream && !r.shared_stream) hipStreamDestroy(r.stream);
     }
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamDestroy(st);
@@ -2589,7 +2636,7 @@ int owrx_waterfall_set(owrx_engine* e, int handle, int every_n_samples, int avg_
     } else {
         w->pending = true;
     }
-    return OWRX_OK;
+    return wf_initial_reserve(e, w);
 }
 
 int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t max_lag) {
@@ -2607,7 +2654,7 @@ int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t
     }
     w->batch_min = bmin;
     w->batch_lag = max_lag;
-    return OWRX_OK;
+    return wf_initial_reserve(e, w);
 }
 
 int owrx_waterfall_set_latency(owrx_engine* e, int handle, double max_wall_ms) {

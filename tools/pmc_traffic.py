@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of the engine kernels from two rocprofv3 --pmc passes
-(tools/gpu_round.sh ... pmc): FETCH_SIZE and WRITE_SIZE (KB per dispatch), averaged over
+(tools/gpu_steps.sh pmc): FETCH_SIZE and WRITE_SIZE (KB per dispatch), averaged over
 dispatches.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half of
 the bytes of wide coalesced streaming reads, so fetched bytes = 2 x FETCH_SIZE; WRITE_SIZE is
 taken as is.  Writes profiles/<tag>_pmc_traffic_<config>.json, which bench.py reports as
