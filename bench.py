@@ -224,6 +224,12 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     tp = ts = tr = 0.0  # host seconds in push (block build + launches), sync, output reads
     st0 = eng.stats()
     rng = np.random.default_rng(7)
+    # the harness's own Python objects (C chain handles and parameter records) make the
+    # collector's full passes take tens of ms at 10^5 chains: none during the paced loop
+    import gc
+    gc_was = gc.isenabled()
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     for i in range(nblocks):
         deadline = t0 + i * period
@@ -259,6 +265,8 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
         # pipelined: how late the block's push (and this iteration) ran against its deadline
         lat.append(e - a if not pipelined else e - deadline)
     st_loop = eng.stats()
+    if gc_was:
+        gc.enable()
     eng.sync()
     # pipelined: the level's last outputs are in the host rings within one period of its last
     # deadline (a GPU slower than the stream accumulates lag block by block)
