@@ -221,6 +221,9 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     period = block / fs
     nblocks = max(1, int(seconds / period))
     lat, joins, leaves, bps = [], [], [], []
+    wf_settings = [(avg, hop), params.fft_parameters(fs, n_fft, 25, 0.3)]
+    wf_every = max(1, int(round(1.0 / period)))  # blocks per second of stream
+    wf_alt, wf_set_ms = 0, []
     tp = ts = tr = 0.0  # host seconds in push (block build + launches), sync, output reads
     st0 = eng.stats()
     rng = np.random.default_rng(7)
@@ -240,6 +243,14 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
         eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
         b = time.perf_counter()
         tp += b - a
+        if churn and i % wf_every == wf_every - 1:
+            # the client's waterfall settings change once a second (fps 9 <-> 25, the
+            # SpectrumThread's setProperty path, owrx/fft.py:49-56): no drain
+            wf_alt = 1 - wf_alt
+            a_, h_ = wf_settings[wf_alt]
+            w0 = time.perf_counter()
+            wf.set(h_, a_, True)
+            wf_set_ms.append(time.perf_counter() - w0)
         if churn and chains:
             c0 = time.perf_counter()
             chains.pop(int(rng.integers(len(chains)))).close()
@@ -291,6 +302,8 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     if joins:
         extra = {"client_join_ms": summ(joins), "client_leave_ms": summ(leaves),
                  "set_bandpass_ms": summ(bps),
+                 "waterfall_fps_changes": len(wf_set_ms),
+                 "waterfall_set_ms": summ(wf_set_ms) if wf_set_ms else None,
                  "pipeline_drains": int(st_loop["pipeline_drains"] - st0["pipeline_drains"])}
     return {**extra, "seconds": round(nblocks * period, 2), "stream_msps": fs / 1e6, "chains": len(plist),
             "setup_s": round(t_setup, 2),
