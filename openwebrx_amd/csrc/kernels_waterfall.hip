@@ -1134,6 +1134,14 @@ wf_fft4_rows(const float2* __restrict__ Y, const float2* __restrict__ tw,
     }
 }
 
+// Each thread sums four consecutive positions of the partial rows (16-B loads; a position is
+// bin i's place in a partial row: natural, or j-major after the DIF split / in wf_fft_h2's
+// half-major rows, bin Q k + j at j (N / Q) + k).  The carried accumulator is kept in position
+// order too.
+OWRX_DEV float4 f4add(float4 a, float4 b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
 __global__ void __launch_bounds__(256)
 wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
             const float* __restrict__ carry_in, float* __restrict__ carry_out, int N,
@@ -1141,15 +1149,16 @@ wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
             float* __restrict__ f32_out, int qlog, const WfGroup* __restrict__ groups,
             int ngroups, int skip) {
 #pragma clang fp contract(off)
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
+    const int p0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (p0 >= N) return;
     const WfRow r = rows[blockIdx.y];
-    float s = r.use_carry ? carry_in[i] : 0.0f;
-    // bin i's place in a partial row: natural, or j-major after the DIF split (bin Q k + j at
-    // j (N / Q) + k)
-    const int pi = qlog ? ((i & ((1 << qlog) - 1)) * (N >> qlog)) + (i >> qlog) : i;
+    float4 s = r.use_carry ? *reinterpret_cast<const float4*>(carry_in + p0)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto at = [&](const float* base, int64_t row) {
+        return *reinterpret_cast<const float4*>(base + row * N);
+    };
     // the groups' partials in order (the row's summation order); loads batched 16 deep
-    const float* pp = partial + (int64_t)r.first_group * N + pi;
+    const float* pp = partial + (int64_t)r.first_group * N + p0;
     // groups [ngroups - skip, ngroups) were transformed frame by frame (wf_fft_l32's tail
     // split): their frames' partial rows follow the groups', folded here in frame order into the
     // group's sum first, as the workgroup would have
@@ -1157,21 +1166,21 @@ wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
     const int n_whole = max(0, min(r.ngroups, g_split - r.first_group));
     int gi = 0;
     for (; gi + 16 <= n_whole; gi += 16) {
-        float v[16];
+        float4 v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = pp[(int64_t)(gi + u) * N];
+        for (int u = 0; u < 16; ++u) v[u] = at(pp, gi + u);
 #pragma unroll
-        for (int u = 0; u < 16; ++u) s += v[u];
+        for (int u = 0; u < 16; ++u) s = f4add(s, v[u]);
     }
     if (gi + 8 <= n_whole) {
-        float v[8];
+        float4 v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = pp[(int64_t)(gi + u) * N];
+        for (int u = 0; u < 8; ++u) v[u] = at(pp, gi + u);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
+        for (int u = 0; u < 8; ++u) s = f4add(s, v[u]);
         gi += 8;
     }
-    for (; gi < n_whole; ++gi) s += pp[(int64_t)gi * N];
+    for (; gi < n_whole; ++gi) s = f4add(s, at(pp, gi));
     if (gi < r.ngroups) {
         // (loads issued eight groups' frame counts and up to four frames at a time: a serial
         // chain of dependent L2 reads per group cost tens of us per launch)
@@ -1185,32 +1194,39 @@ wf_finalize(const float* __restrict__ partial, const WfRow* __restrict__ rows,
             for (int u = 0; u < 8; ++u) {
                 const int nf = nfv[u];
                 if (nf == 0) break;
-                const float* fp = partial + (int64_t)f0 * N + pi;
-                float v[4];
+                const float* fp = partial + (int64_t)f0 * N + p0;
+                float4 v[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = j < nf ? fp[(int64_t)j * N] : 0.0f;
-                float g = v[0];
+                for (int q = 0; q < 4; ++q) v[q] = q < nf ? at(fp, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 g = v[0];
 #pragma unroll
-                for (int j = 1; j < 4; ++j)
-                    if (j < nf) g = g + v[j];
-                for (int j = 4; j < nf; ++j) g = g + fp[(int64_t)j * N];
-                s += g;
+                for (int q = 1; q < 4; ++q)
+                    if (q < nf) g = f4add(g, v[q]);
+                for (int q = 4; q < nf; ++q) g = f4add(g, at(fp, q));
+                s = f4add(s, g);
                 f0 += nf;
             }
         }
     }
     if (!r.complete) {
-        carry_out[i] = s;
+        *reinterpret_cast<float4*>(carry_out + p0) = s;
         return;
     }
-    const float lg = log10f(s);
-    const float t = 10.0f * lg;
-    const float db = t + add_corr;
-    const int o = (i + N / 2) & (N - 1);   // FftSwap
-    if (adpcm)
-        s16_out[(int64_t)r.out_index * N + o] = db_to_s16(db);
-    else
-        f32_out[(int64_t)r.out_index * N + o] = db;
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+    const int nq = N >> qlog;  // positions per sub-row
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int p = p0 + c;
+        const int i = qlog ? ((p % nq) << qlog) + p / nq : p;  // the position's bin
+        const float lg = log10f(sv[c]);
+        const float t = 10.0f * lg;
+        const float db = t + add_corr;
+        const int o = (i + N / 2) & (N - 1);  // FftSwap
+        if (adpcm)
+            s16_out[(int64_t)r.out_index * N + o] = db_to_s16(db);
+        else
+            f32_out[(int64_t)r.out_index * N + o] = db;
+    }
 }
 
 // FftAdpcm: 10 copies of the first value (COMPRESS_FFT_PAD_N, htdocs/openwebrx.js:845), then
@@ -1466,7 +1482,8 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
     while ((1 << logn) < N) ++logn;
     // partial rows half- / sub-frame-major: the DIF split's Q = N / 16384, wf_fft_h2's Q = 2
     const int qlog = wf_uses_split(logn) ? logn - 14 : wf_uses_h2(logn) ? 1 : 0;
-    hipLaunchKernelGGL(wf_finalize, dim3((N + 255) / 256, nrows), dim3(256), 0, st, partial,
+    if (N % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wf_finalize, dim3((N / 4 + 255) / 256, nrows), dim3(256), 0, st, partial,
                        rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out, qlog,
                        groups, ngroups, skip);
     return hipGetLastError();
