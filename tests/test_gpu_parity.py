@@ -268,6 +268,34 @@ def test_waterfall_batched_launches(amd):
     assert st2["waterfall_samples"] == st2["waterfall_frames"] * hop
 
 
+def test_waterfall_tail_split_rows_bit_identical(amd):
+    """wf_fft_l32's tail split (a launch's last groups dealt frame by frame, their frames folded
+    in order by wf_finalize): C3's waterfall (16384 bins, avg 97, hop 11454) over 1 100 frames,
+    once batched into launches of ~1 000 frames (over 7/8 of a launch's groups per CU, so the
+    split is on) and once per 2^20-sample block (~91 frames per launch: no split).  The rows
+    are bit-identical, and equal the oracle's to 2e-3 dB on the first rows."""
+    fs, N = 10000000, 16384
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+    from openwebrx_amd import synth
+    n = hop * 1100 + N
+    iq, _ = synth.make_iq(fs, n, ["nfm", "am", "usb"])
+    hist = 1000 * hop + 2 * N + (1 << 20)
+    a, st, st2 = _wf_batched(amd, iq, fs, N, hop, avg, 1 << 20, 1000, hist)
+    eng = amd.Engine(fs, max_block=1 << 20)
+    wf = eng.waterfall(N, hop, avg, adpcm=False)
+    for i in range(0, iq.size, 1 << 20):
+        eng.push(iq[i:i + (1 << 20)])
+    eng.sync()
+    b = wf.read_rows()
+    eng.close()
+    assert a.shape == b.shape and a.shape[0] >= 10, (a.shape, b.shape)
+    assert st2["waterfall_launches"] <= 3, st2
+    assert np.array_equal(a, b)
+    ref = np.stack([oracle.fftswap(r) for r in oracle.waterfall_rows(iq[:hop * avg * 2 + N], N,
+                                                                      hop, avg)])
+    assert np.max(np.abs(a[:ref.shape[0]] - ref)) < 2e-3
+
+
 def test_waterfall_reconfigure_without_drain(amd):
     """SpectrumThread's live settings on a running engine (owrx/fft.py:49-56: fft_fps ->
     FftChain.setFps, fft_voverlap_factor -> setVOverlapFactor, both re-deriving the averaging
