@@ -215,6 +215,22 @@ def test_waterfall_float_rows(amd, N, fs):
     assert np.max(err) < 2e-3, np.max(err)   # dB; fp32 FFT vs double
 
 
+@pytest.mark.parametrize("N,hop", [(16384, 200000), (65536, 150000)])
+def test_waterfall_hop_near_the_history(amd, N, hop):
+    """A waterfall whose every_n_samples is a large share of the engine's history (2^18 by
+    default): a group still open at a block's end must keep its first frame inside the next
+    block's window, so the frames per group are clamped to the history
+    (wf_frames_per_group).  Rows equal the oracle's, with avg 3."""
+    fs, avg = 10000000, 3
+    from openwebrx_amd import synth
+    n = hop * avg * 4 + N
+    iq, _ = synth.make_iq(fs, n, ["nfm", "am"])
+    g = _wf(amd, iq, fs, N, hop, avg, False, 1 << 17)
+    ref = np.stack([oracle.fftswap(r) for r in oracle.waterfall_rows(iq, N, hop, avg)])
+    assert g.shape == ref.shape
+    assert np.max(np.abs(g - ref)) < 2e-3
+
+
 def _wf_batched(amd, iq, fs, N, hop, avg, block, min_frames, history, ingest=False):
     eng = amd.Engine(fs, max_block=block, history=history)
     wf = eng.waterfall(N, hop, avg, adpcm=False)
