@@ -599,7 +599,13 @@ def pmc_traffic(prefix, config):
     (profiles/*_pmc_traffic_<config>.json, written by tools/pmc_traffic.py from rocprofv3 --pmc
     passes of this same bench command); (None, reason) when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_%s.json" % config)))
+    import re
+
+    def order(f):  # tags rNN<suffix>: round, then suffix a..z, then aa..zz (later in a round)
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_%s.json" % config)),
+                   key=order)
     if not files:
         return None, "no PMC summary committed for config %s" % config
     d = json.load(open(files[-1]))
