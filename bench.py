@@ -12,7 +12,7 @@ A step is `--blocks-per-step` (4) blocks of `--block` IQ samples (2^20, SURVEY.m
 20 steps stream 2^26.3 samples in 2^20-sample blocks) pushed through all of it, inputs resident
 in HBM, outputs (waterfall rows, ADPCM audio, s-meter) copied back to host rings and drained
 once per step.  The waterfall FFT launches once per `--wf-batch` frames (owrx_waterfall_
-set_batch; four per stream-A CU by default), not once per block.
+set_batch; eight per stream-A CU by default), not once per block.
 
 N>1 (torchrun, one rank per GPU): rank 0 owns the stream and broadcasts each block over RCCL
 (the path's one exchange step); every rank runs its own chains (weak scaling:
@@ -672,8 +672,9 @@ def main():
     ap.add_argument("--block", type=int, default=1 << 20,
                     help="IQ samples per step (SURVEY.md 8d: 2^20-sample blocks)")
     ap.add_argument("--wf-batch", type=int, default=-1,
-                    help="waterfall frames per FFT launch (owrx_waterfall_set_batch; -1: four per "
-                         "stream-A CU, 0: every block's frames in that block)")
+                    help="waterfall frames per FFT launch (owrx_waterfall_set_batch; -1: eight per "
+                         "stream-A CU at N <= 16384, two above, 0: every block's frames in that "
+                         "block)")
     ap.add_argument("--chains", type=int, default=None,
                     help="chains per GPU (default: the config's)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
@@ -751,9 +752,11 @@ def main():
     wf_batch = 0
     if world == 1 and not args.no_waterfall:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        # four frames per stream-A CU for the 16384-point kernel (4 frames per workgroup); one
-        # per CU above it (each frame is 4 or 2 sub-frames of that kernel after the DIF split)
-        per_cu = 4 if n_fft <= 16384 else 1
+        # eight frames per stream-A CU for the 16384-point kernel (two groups of 4 per
+        # workgroup: its start-up and first frame amortise over twice the frames, 0.187 vs
+        # 0.156 of HBM at C3); two per CU above it (each frame is 4 or 2 sub-frames of that
+        # kernel after the DIF split).  The row-latency cap bounds the wait at real-time rates.
+        per_cu = 8 if n_fft <= 16384 else 2
         wf_batch = per_cu * max(1, cus - 16) if args.wf_batch < 0 else args.wf_batch
     history = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
     eng = Engine(fs, max_block=block, device=local, history=history)
