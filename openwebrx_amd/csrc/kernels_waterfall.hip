@@ -841,248 +841,6 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     finish();
 }
 
-// ---- wf_fft_l32p: wf_fft_l32 with the next frame's first pass pipelined into this one's ------
-// Same transform, same items, same partial rows (bit-identical).  wf_fft_l32 runs each frame's
-// phases in order between its four barriers, so while a phase's LDS stores drain nothing else
-// issues: P1's and P2's stores each sit alone in a barrier interval.  Here a frame's P2 and P3
-// overlap the next frame's P1:
-//   barrier | P2 reads, twiddles, DFT32 | barrier | P2 stores + next frame's window and DFT32 |
-//   barrier | P3 reads | barrier | next frame's P1 stores + the frame after's loads + P3 math
-// so both store phases run beside VALU work.  The next frame's P1 result (64 VGPRs) and this
-// frame's P3 inputs (64) are live together instead of the prefetched samples, which are now
-// loaded one frame ahead after the P1 stores.  Frames come from a small generator over the
-// dealt items: an item's claim is issued by thread 0 inside the iteration before it is needed
-// and read by every wave after the next barrier.
-__global__ void __launch_bounds__(WfL32::NT)
-wf_fft_l32p(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
-            const float* __restrict__ window, const float2* __restrict__ tw,
-            float* __restrict__ partial, int qlog, int fstride, int items, int* __restrict__ work,
-            int whole, int skip) {
-    using K = WfL32;
-    constexpr int N = K::N, NT = K::NT;
-    extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    __shared__ int s_claim;
-    const int t0 = threadIdx.x;
-    struct Item {
-        __amdgpu_buffer_rsrc_t xr;
-        int hop, nfr, w;
-    };
-    struct Frame {
-        __amdgpu_buffer_rsrc_t xr;
-        int fo, w;
-        bool last, valid;
-    };
-    auto desc = [&](int i) { return i < whole ? i : i + skip; };
-    auto item = [&](int w) {
-        const int gi = w >> qlog;
-        const WfGroup g = groups[gi];
-        const int64_t g0 = __builtin_amdgcn_readfirstlane(
-            qlog ? (int)((((int64_t)gi * fstride << qlog) + (w & ((1 << qlog) - 1))) * N)
-                 : (int)(g.start - blk_start));
-        Item it;
-        it.hop = __builtin_amdgcn_readfirstlane(qlog ? N << qlog : g.hop);
-        it.nfr = __builtin_amdgcn_readfirstlane(g.nframes);
-        it.w = w;
-        it.xr = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float2*>(blk + g0), 0,
-            (int)(sizeof(float2) * ((int64_t)(it.nfr - 1) * it.hop + N)), 0x00020000);
-        return it;
-    };
-    const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
-                                                      (int)(sizeof(float) * N), 0x00020000);
-    auto load_x = [&](const Frame& F, float2* v) {
-        const int fo = F.valid ? F.fo : kWfOob;
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            const int vo = t0 * 8 + fo;
-            v[r] = make_float2(
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(F.xr, vo, r * NT * 8, 0)),
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(F.xr, vo + 4, r * NT * 8, 0)));
-        }
-    };
-    float2 tp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) tp[i] = tw[((t0 << i) & (N - 1)) << qlog];
-    float2 t2v[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int e = t0 + NT * i;
-        t2v[i] = e < 31 * 32 ? tw[(((e >> 5) + 1) * (e & 31)) << (4 + qlog)] : make_float2(0.f, 0.f);
-    }
-    auto finish = [&]() {
-        __syncthreads();
-        if (t0 == 0 && atomicAdd(work + 1, 1) == (int)gridDim.x - 1) {
-            atomicExch(work, 0);
-            atomicExch(work + 1, 0);
-        }
-    };
-    // the frame generator: `g_it` is the item being handed out, `g_f` its next frame
-    Item g_it;
-    int g_f = 0;
-    bool g_more = true;  // an item may still be claimed
-    auto claim_now = [&]() -> int {  // synchronous claim (prologue only)
-        if (t0 == 0) s_claim = atomicAdd(work, 1);
-        __syncthreads();
-        const int c = __builtin_amdgcn_readfirstlane(s_claim);
-        __syncthreads();
-        return c;
-    };
-    auto gen = [&](int claimed) -> Frame {  // claimed: the claim read for an exhausted item
-        Frame F;
-        F.valid = false;
-        F.fo = kWfOob;
-        F.last = true;
-        F.w = 0;
-        F.xr = g_it.xr;
-        if (g_f >= g_it.nfr) {
-            if (!g_more || claimed >= items) {
-                g_more = false;
-                return F;
-            }
-            g_it = item(desc(claimed));
-            g_f = 0;
-        }
-        F.xr = g_it.xr;
-        F.fo = g_f * g_it.hop * 8;
-        F.w = g_it.w;
-        F.valid = true;
-        ++g_f;
-        F.last = g_f == g_it.nfr;
-        return F;
-    };
-    {
-        const int c0 = claim_now();
-        if (c0 >= items) {
-            finish();
-            return;
-        }
-        g_it = item(desc(c0));
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-        if (t0 + NT * i < 31 * 32) sm[K::TW2 + t0 + NT * i] = t2v[i];
-    const int sw = wf_swz32(t0);
-    // P1 of a frame: window, DFT32 (into b), and its store into the image
-    auto p1_math = [&](const float2* x, float2* b) {
-        float wv[32];
-#pragma unroll
-        for (int r = 0; r < 32; ++r)
-            wv[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, t0 * 4, r * NT * 4, 0));
-#pragma unroll
-        for (int r = 0; r < 32; ++r) b[r] = make_float2(x[r].x * wv[r], x[r].y * wv[r]);
-        f2dft32(b);
-    };
-    auto p1_store = [&](const float2* b) {
-        int t = threadIdx.x;
-        asm volatile("" : "+v"(t));
-#pragma unroll
-        for (int k = 0; k < 32; ++k) sm[32 * t + (k ^ (t & 15))] = b[l32_at(k)];
-    };
-    float2 nx[32];
-    Frame F0 = gen(0);
-    {
-        load_x(F0, nx);
-        float2 b[32];
-        p1_math(nx, b);
-        __syncthreads();  // the twiddle table stores before the image's (distinct regions; cheap)
-        p1_store(b);
-    }
-    Frame F1;
-    {
-        int c = 0;
-        if (g_f >= g_it.nfr && g_more) c = claim_now();
-        F1 = gen(c);
-    }
-    load_x(F1, nx);
-    float acc[32];
-#pragma unroll
-    for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
-#pragma unroll 1
-    while (F0.valid) {
-        int t = threadIdx.x;
-        asm volatile("" : "+v"(t));
-        // does the frame after F1 need a new item?  (uniform)
-        const bool need = g_more && g_f >= g_it.nfr;
-        __syncthreads();  // (1) F0's P1 stores are visible
-        float2 a[32];
-        {
-            const int ts = wf_swz32(t);
-#pragma unroll
-            for (int r = 0; r < 32; ++r) a[r] = sm[ts + NT * r];
-            const int k = t & 31;
-            const float2* T = sm + K::TW2 + k;
-#pragma unroll
-            for (int r = 1; r < 32; ++r) {
-                a[r] = f2mul(a[r], T[(r - 1) * 32]);
-                if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-            }
-            f2dft32(a);
-        }
-        __syncthreads();  // (3) every P2 read before any P2 store
-        {
-            const int base = (t >> 5) * 1024 + (t & 31);
-#pragma unroll
-            for (int r = 0; r < 32; ++r) sm[wf_swz32(base + 32 * r)] = a[l32_at(r)];
-        }
-        __builtin_amdgcn_sched_barrier(0);  // the P2 stores issue (a dies) before F1's P1 math
-        if (need && t0 == 0) s_claim = atomicAdd(work, 1);
-        float2 b[32];
-        if (F1.valid) p1_math(nx, b);  // F1's window and DFT32 beside the P2 stores
-        __syncthreads();  // (6) P2 stores visible; the claim too
-        const int claimed = need ? __builtin_amdgcn_readfirstlane(s_claim) : 0;
-        float2 c[32];
-#pragma unroll
-        for (int m = 0; m < 32; ++m) c[m] = sm[sw + NT * m];
-        __syncthreads();  // (8) every P3 read done: the image is free
-        if (F1.valid) p1_store(b);  // F1's P1 stores beside F0's P3 math
-        __builtin_amdgcn_sched_barrier(0);  // b dies before the loads into nx
-        const Frame F2 = gen(claimed);
-        load_x(F2, nx);
-        {
-            // (the bases made opaque each frame: hoisted out of the loop, the 30 twiddles built
-            // from them were kept in scratch)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(tp[i].x), "+v"(tp[i].y));
-            float2 tb[16];
-            tb[1] = tp[0];
-            tb[2] = tp[1];
-            tb[4] = tp[2];
-            tb[8] = tp[3];
-            tb[3] = f2mul(tp[0], tp[1]);
-            tb[5] = f2mul(tp[0], tp[2]);
-            tb[6] = f2mul(tp[1], tp[2]);
-            tb[7] = f2mul(tb[3], tp[2]);
-#pragma unroll
-            for (int r = 9; r < 16; ++r) tb[r] = f2mul(tb[r - 8], tp[3]);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                float2 d[16];
-                d[0] = c[h];
-#pragma unroll
-                for (int r = 1; r < 16; ++r) {
-                    const float2 wt = h ? f2mul32(tb[r], r) : tb[r];
-                    d[r] = f2mul(c[h + 2 * r], wt);
-                }
-                f2dft<16>(d);
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    acc[h + 2 * r] = acc[h + 2 * r] + fmaf(d[r].y, d[r].y, d[r].x * d[r].x);
-            }
-        }
-        if (F0.last) {
-            float* out = partial + (int64_t)F0.w * N;
-#pragma unroll
-            for (int m = 0; m < 32; ++m) {
-                out[t0 + NT * m] = acc[m];
-                acc[m] = 0.0f;
-            }
-        }
-        F0 = F1;
-        F1 = F2;
-    }
-    finish();
-}
-
 // ---- wf_fft_h2: N = 16384 as two 8192-point halves, two workgroups per CU ------------------
 // wf_fft_l32 holds a whole frame's image (128 KiB) in one CU's LDS, so one 512-thread workgroup
 // per CU runs its passes in lockstep: while its waves wait at a barrier, for the LDS or for the
@@ -1578,12 +1336,11 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
 // N = 16384: the whole-frame radix-32 kernel wf_fft_l32; OWRX_WF_KERNEL=h2 the half-frame kernel
 // (two workgroups per CU: 68 vs 50 us per 960 C3 frames from HBM, its loads exposed) and =r16
 // the radix-16 one (A/B); 1024 <= N <= 8192: radix 16
-static int wf_n16k_kernel() {  // 0: h2, 1: l32, 2: r16, 3: l32p
+static int wf_n16k_kernel() {  // 0: h2, 1: l32, 2: r16
     static const int v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
         if (s && strcmp(s, "r16") == 0) return 2;
         if (s && strcmp(s, "h2") == 0) return 0;
-        if (s && strcmp(s, "l32p") == 0) return 3;
         return 1;
     }();
     return v;
@@ -1608,11 +1365,10 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
                                  int fstride = 0, int skip = 0, int tail = 0) {
     static bool attr = false;
     if (!attr) {
-        for (const void* f : {(const void*)wf_fft_l32, (const void*)wf_fft_l32p}) {
-            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)WfL32::kLds);
-            if (e != hipSuccess) return e;
-        }
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_l32,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)WfL32::kLds);
+        if (e != hipSuccess) return e;
         attr = true;
     }
     if (!work || skip < 0 || skip > ngroups || (qlog && (skip || tail))) return hipErrorInvalidValue;
@@ -1621,9 +1377,8 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
     const int items = whole + tail;
     // one workgroup per CU (the 136 KiB image), at most one per item
     const int grid = std::max(1, std::min(items, cus));
-    hipLaunchKernelGGL(wf_n16k_kernel() == 3 ? wf_fft_l32p : wf_fft_l32, dim3(grid), dim3(WfL32::NT),
-                       WfL32::kLds, st, blk, blk_start, groups, window, tw, partial, qlog, fstride,
-                       items, work, whole, skip);
+    hipLaunchKernelGGL(wf_fft_l32, dim3(grid), dim3(WfL32::NT), WfL32::kLds, st, blk, blk_start,
+                       groups, window, tw, partial, qlog, fstride, items, work, whole, skip);
     return hipGetLastError();
 }
 
@@ -1634,8 +1389,7 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
 // (89 vs 52 us per 960 C3 frames); the groups that would start that round, plus an eighth of a
 // round, are dealt as single frames instead.  0 for the other kernels.
 int wf_tail_split(int logn, int ngroups, int cus) {
-    if (logn != 14 || (wf_n16k_kernel() != 1 && wf_n16k_kernel() != 3) || cus < 8 || ngroups < 2)
-        return 0;
+    if (logn != 14 || wf_n16k_kernel() != 1 || cus < 8 || ngroups < 2) return 0;
     static const int mode = [] {
         const char* s = getenv("OWRX_WF_TAIL");
         return s ? atoi(s) : -1;

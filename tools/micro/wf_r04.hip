@@ -173,11 +173,9 @@ int main(int argc, char** argv) {
         std::vector<uint32_t> all(words, 0xffffffffu);
         CK(hipExtStreamCreateWithCUMask(&s_all, words, all.data()));
     }
-    CK(hipFuncSetAttribute((const void*)wf_fft_l32p, hipFuncAttributeMaxDynamicSharedMemorySize,
-                           (int)WfL32::kLds));
-    auto l32 = [&](int G, hipStream_t st, int skip = 0, int tail = 0, bool piped = false) {
+    auto l32 = [&](int G, hipStream_t st, int skip = 0, int tail = 0) {
         const int items = G - skip + tail;  // (the counters are left zeroed by each launch)
-        hipLaunchKernelGGL(piped ? wf_fft_l32p : wf_fft_l32, dim3(std::min(items, st == 0 || st == s_plain || st == s_all ? 256 : 240)), dim3(WfL32::NT), WfL32::kLds, st, dx, (int64_t)0,
+        hipLaunchKernelGGL(wf_fft_l32, dim3(std::min(items, st == 0 || st == s_plain || st == s_all ? 256 : 240)), dim3(WfL32::NT), WfL32::kLds, st, dx, (int64_t)0,
                            dg, dwin, dtw, dpart, 0, 0, items, dwork, G - skip, skip);
     };
     printf("CUs %d\n", ncu);
@@ -220,12 +218,6 @@ int main(int argc, char** argv) {
                 }
                 printf("FT=%5d F=%d G=%4d tail split S=%d groups (%d frames): %zu of %zu partial bins differ from the unsplit launch\n",
                        FT, F, G, S, T, bad, (size_t)G * N);
-                l32(G, 0, 0, 0, true);
-                CK(hipDeviceSynchronize());
-                CK(hipMemcpy(B.data(), dpart, sizeof(float) * (size_t)G * N, hipMemcpyDeviceToHost));
-                size_t badp = 0;
-                for (size_t q = 0; q < (size_t)G * N; ++q) badp += memcmp(&A[q], &B[q], 4) != 0;
-                printf("FT=%5d F=%d G=%4d l32p: %zu of %zu partial bins differ from l32\n", FT, F, G, badp, (size_t)G * N);
             }
             hipLaunchKernelGGL(wf_fft_r16<14>, dim3(G), dim3(WfR16<14>::NT), WfR16<14>::kLds, 0, dx, (int64_t)0,
                                dg, dwin, dtw, dref);
@@ -253,12 +245,7 @@ int main(int argc, char** argv) {
                 {"l32 tail mask[0,240)", [&] {
                      l32(G, s_lo, S, T);
                  }, false, false, s_lo},
-                {"l32p", [&] {
-                     l32(G, 0, 0, 0, true);
-                 }, true},
-                {"l32p tail mask[0,240)", [&] {
-                     l32(G, s_lo, S, T, true);
-                 }, false, false, s_lo},
+
                 {"l32 tail plain", [&] {
                      l32(G, s_plain, S, T);
                  }, false, false, s_plain},
