@@ -375,7 +375,9 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
     if best and hold_s > 0:
         # the top passing level once more, held for hold_s of stream (60 s); if
         # it does not keep up that long, the level below it once
+        import gc
         for C in passed[::-1][:2]:
+            gc.collect()  # the failed level's Python objects (its engine is closed already)
             _log("capacity hold: %d chains for %.0f s" % (C, hold_s))
             ms = [modes[c % len(modes)] for c in range(C)]
             plist = [params.chain_params(fs, o, m) for o, m in zip(offsets_of(C), ms)]

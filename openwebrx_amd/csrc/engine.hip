@@ -2165,7 +2165,11 @@ static hipError_t create_streams(owrx_engine* e) {
         if (err != hipSuccess) return err;
     }
     // B, C: the serial demodulator stages; R: the output gathers; W: the waterfall row encoders
-    int nb = 4, nc = 4, nr = 4, nw = 4;
+    // B 8 and C 12 CUs: the serial one-lane-per-chain kernels are memory-latency bound, and
+    // spread over more CUs they finish sooner (C3 6.0-6.3 -> 7.0 Gsps against 4 + 4; C4 and C5
+    // +1.5-2 % with 8 + 8; A's 228 CUs cost the DDC GEMM nothing measurable:
+    // profiles/r04_serial_cus_ab.txt)
+    int nb = 8, nc = 12, nr = 4, nw = 4;
     if (const char* v = getenv("OWRX_SERIAL_CUS")) {
         const int k = sscanf(v, "%d,%d,%d,%d", &nb, &nc, &nr, &nw);
         if (k == 3) nw = 0;  // the row encoders share R's CUs (the round-2 layout)
