@@ -166,6 +166,9 @@ static hipError_t dalloc(T** p, size_t count) {
     if (count == 0) count = 1;
     hipError_t e = hipMalloc((void**)p, sizeof(T) * count);
     if (e == hipSuccess) e = hipMemset(*p, 0, sizeof(T) * count);
+    // a failed allocation is reported here; clear the runtime's sticky last error, or the next
+    // launch's hipGetLastError (any engine's, on this thread) would report it again
+    if (e != hipSuccess) (void)hipGetLastError();
     return e;
 }
 template <typename T>
@@ -805,7 +808,10 @@ static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
         it->second.pop_back();
     } else {
         const hipError_t r = hipMalloc(&q, bytes);
-        if (r != hipSuccess) return r;
+        if (r != hipSuccess) {
+            (void)hipGetLastError();  // not sticky for the next launch (see dalloc)
+            return r;
+        }
         e->pool_size[q] = bytes;
         e->stats.pool_allocs++;
     }
@@ -832,7 +838,10 @@ static hipError_t hpalloc(owrx_engine* e, T** p, size_t count) {
     }
     void* q = nullptr;
     const hipError_t r = hipHostMalloc(&q, bytes, 0);
-    if (r != hipSuccess) return r;
+    if (r != hipSuccess) {
+        (void)hipGetLastError();
+        return r;
+    }
     e->hpool_size[q] = bytes;
     e->stats.pool_allocs++;
     *p = static_cast<T*>(q);
@@ -2266,6 +2275,7 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
         return OWRX_ENODEV;
     }
     HIPCHK(hipSetDevice(device));
+    (void)hipGetLastError();  // no stale error of an earlier engine on this thread
     owrx_engine* e = new owrx_engine();
     e->device = device;
     e->samp_rate = samp_rate;
