@@ -615,7 +615,10 @@ int fc_kslices(int tiles, int Dp, int ncu) {
     const int per_wave = (Dp >> 3) / kFcKSplit;  // K-blocks per wave, unsliced
     auto ok = [&](int k) { return k >= 1 && k <= kFcMaxKSlices && per_wave % k == 0; };
     if (forced > 0) return ok(forced) ? forced : 1;
-    if (tiles >= 3 * ncu) return 1;
+    // a grid that already covers the CUs once keeps whole K: C3's 384 tiles on 228 CUs ran 0.53
+    // of HBM unsliced vs 0.51 with 3 slices (profiles/r04_fc_kslices_c3.txt); C4's 128 and C5's
+    // 64 tiles gain 0.32 -> 0.48 and 0.25 -> 0.36 from slicing
+    if (tiles >= ncu) return 1;
     int best = 1;
     for (int k = 2; k <= kFcMaxKSlices; ++k) {
         if (!ok(k)) continue;
