@@ -844,9 +844,9 @@ def main():
     gc.collect()
     gc.disable()
     eng.sync()
-    # HIP events in every 4th block (each block's events cost host time; the waterfall's
-    # batched launches are all timed)
-    eng.set_timing(not args.no_timing, every=4)
+    # HIP events in every 8th block (each block's events cost host time: ~8 more API calls; the
+    # waterfall's batched launches are all timed)
+    eng.set_timing(not args.no_timing, every=8)
     s0 = eng.stats()
     if dist:
         dist.barrier()

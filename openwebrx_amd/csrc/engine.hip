@@ -2076,7 +2076,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         }();
         const int nad = S.nsel[1][0] + S.nsel[1][1];
         const bool in_kernel = handoff && !wide && e->d_ready && nad > 0;
-        if (e->d_ready) HIPCHK(launch_signal_block(e->d_ready, e->block_index + 1, sB));
+        // (the block counter is only read by an in-kernel wait: no launch per block without one)
+        if (e->d_ready && handoff) HIPCHK(launch_signal_block(e->d_ready, e->block_index + 1, sB));
         if (!in_kernel) HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
         HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + S.off[1][0], nad,
                                   in_kernel ? e->d_ready : nullptr, e->block_index + 1, sC));
