@@ -1386,8 +1386,8 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
 // groups go frame by frame.  The workgroups placed at once on a CU-masked queue are fewer than
 // its CUs (measured 227-230 of 240 for the engine's stream-A mask: the dispatcher's per-engine
 // share), so a launch of one item per CU ran its last items in a second round, doubling its time
-// (89 vs 52 us per 960 C3 frames); the groups that would start that round, plus an eighth of a
-// round, are dealt as single frames instead.  0 for the other kernels.
+// (89 vs 52 us per 960 C3 frames); the groups that would start a partial last round, plus a
+// 16th of a round, are dealt as single frames instead.  0 for the other kernels.
 int wf_tail_split(int logn, int ngroups, int cus) {
     if (logn != 14 || wf_n16k_kernel() != 1 || cus < 8 || ngroups < 2) return 0;
     static const int mode = [] {
@@ -1395,9 +1395,12 @@ int wf_tail_split(int logn, int ngroups, int cus) {
         return s ? atoi(s) : -1;
     }();
     if (mode == 0) return 0;
-    const int lo = cus - cus / 8;
+    // the workgroups a masked queue holds at once: ~15/16 of its CUs (measured 227-230 of 240);
+    // the groups past the last full round of those, plus a 16th of a round, go frame by frame
+    const int held = cus - cus / 16;
+    const int lo = held - cus / 16;
     if (ngroups <= lo) return 0;
-    const int s = ngroups <= cus ? ngroups - lo : ngroups % cus + cus / 8;
+    const int s = ngroups <= held ? ngroups - lo : ngroups % held + cus / 16;
     return std::min(s, ngroups);
 }
 
