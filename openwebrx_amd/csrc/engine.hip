@@ -1406,7 +1406,11 @@ static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
         if (!wf_uses_split(w->logn)) return 1;
         fpg = kWfSplitMaxFpg;
     } else if (wf_uses_l32(w->logn)) {
-        fpg = 4;
+        static const int l32_fpg = [] {  // OWRX_WF_FPG: frames per group of wf_fft_l32 (A/B)
+            const char* v = getenv("OWRX_WF_FPG");
+            return v ? std::max(1, std::min(16, atoi(v))) : 4;
+        }();
+        fpg = l32_fpg;
     } else {
         fpg = std::min<int64_t>((frames + cus - 1) / cus, kWfMaxFramesPerGroup);
     }
