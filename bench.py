@@ -825,11 +825,13 @@ def main():
                 if i >= prime + args.warmup:
                     host_s["process_t"] += dt_
             else:  # the one exchange step: rank 0's block to every rank over RCCL
-                t, off = bcast.step(j)
+                # block j + 1's broadcast is enqueued before block j is processed, so it runs
+                # beside this block's host and GPU work (three windows, multi.IqBroadcast)
+                if j + 1 < nsteps * bps:
+                    bcast.issue(j + 1)
+                t, off = bcast.wait(j)
                 # wait for this broadcast only (an event behind it on torch's stream), not for
-                # the device: the engine's own streams keep blocks j-1 .. j-3 in flight
-                # meanwhile, and the next broadcast overlaps block j (its window was released by
-                # this call)
+                # the device: the engine's own streams keep earlier blocks in flight meanwhile
                 arrived = torch.cuda.Event()
                 arrived.record()
                 arrived.synchronize()

@@ -7,8 +7,8 @@ wideband IQ broadcast from rank 0 as the only exchange step.
 * IqBroadcast -- rank 0 owns the stream (host ingest or an HBM-resident recording); each
   block goes to every rank with one torch.distributed broadcast (RCCL over xGMI with the
   "nccl" backend, gloo in the CPU tests).  Ranks > 0 assemble [history | block] windows,
-  alternating two, because the engine still reads block k (asynchronously) while k+1 arrives
-  (owrx_process_device contract, include/owrx_amd.h).
+  rotating three, because the engine still reads block k (asynchronously) while k+1 arrives
+  and k+2's broadcast is already enqueued (owrx_process_device contract, include/owrx_amd.h).
 * Placement -- the same balance for the in-process drop-in (pycsdr shim, one engine per GPU
   in one OpenWebRX process), where chains come and go one at a time.
 No reduction: every rank returns its own chains' outputs to the host.
@@ -56,26 +56,68 @@ class Placement:
 class IqBroadcast:
     """Per-block IQ distribution.  step(i) returns (tensor, offset) such that the engine can
     process tensor[offset : offset + block] with tensor[offset - history : offset] holding
-    the preceding samples."""
+    the preceding samples.
+
+    Pipelined use (issue / wait): issue(i + 1) is enqueued before block i is processed, so the
+    broadcast of the next block overlaps this block's host and GPU work.  Ranks > 0 therefore
+    rotate three windows: issue(i + 1) rewrites block i - 2's window, which the engine has
+    finished once owrx_process_device(i - 1) returned (its contract: the caller may reuse the
+    block before the one just passed)."""
+
+    NWIN = 3
 
     def __init__(self, torch, dist, device, history, block, src=0, stream=None):
         self.torch, self.dist = torch, dist
         self.history, self.block, self.src = history, block, src
         self.rank = dist.get_rank()
         self.stream = stream  # rank src: complex64 tensor [history | blocks...]
+        self.pending = {}     # block -> async broadcast handle
+        self.next_issue = 0   # broadcasts are enqueued in block order on every rank
         if self.rank != src:
             self.windows = [torch.zeros(history + block, dtype=torch.complex64, device=device)
-                            for _ in range(2)]
+                            for _ in range(self.NWIN)]
 
-    def step(self, i):
+    def _view(self, i):
         h, b = self.history, self.block
         lo = 0 if i == 0 else h  # the first broadcast also carries the initial history
         if self.rank == self.src:
-            blk = self.stream[lo + i * b if i else 0: h + (i + 1) * b]
-            self.dist.broadcast(self.torch.view_as_real(blk), src=self.src)
-            return self.stream, h + i * b
-        w, prev = self.windows[i % 2], self.windows[(i + 1) % 2]
-        if i > 0:
-            w[:h].copy_(prev[b:b + h])
-        self.dist.broadcast(self.torch.view_as_real(w[lo:h + b]), src=self.src)
-        return w, h
+            return self.stream[lo + i * b if i else 0: h + (i + 1) * b], self.stream, h + i * b
+        w = self.windows[i % self.NWIN]
+        return w[lo:h + b], w, h
+
+    def issue(self, i):
+        """Enqueue the broadcasts up to block i's (not waiting for them), in block order: the
+        ranks' collectives must match one for one."""
+        while self.next_issue <= i:
+            self._issue(self.next_issue)
+            self.next_issue += 1
+
+    def _issue(self, i):
+        h, b = self.history, self.block
+        if self.rank != self.src and i > 0:
+            # the window starts with the previous block's last `history` samples: that block's
+            # broadcast must land first (a stream-level wait with RCCL)
+            prev = self.pending.get(i - 1)
+            if prev is not None:
+                prev.wait()
+            w, pw = self.windows[i % self.NWIN], self.windows[(i - 1) % self.NWIN]
+            w[:h].copy_(pw[b:b + h])
+        part, _, _ = self._view(i)
+        self.pending[i] = self.dist.broadcast(self.torch.view_as_real(part), src=self.src,
+                                              async_op=True)
+
+    def wait(self, i):
+        """Block i's (tensor, offset) once its broadcast has landed (issued if it was not)."""
+        self.issue(i)
+        w = self.pending.pop(i, None)
+        if w is not None:
+            w.wait()
+        # older handles whose windows issue(i) already waited for
+        for k in [k for k in self.pending if k < i]:
+            self.pending.pop(k)
+        _, t, off = self._view(i)
+        return t, off
+
+    def step(self, i):
+        """Unpipelined: broadcast block i and return it."""
+        return self.wait(i)

@@ -37,7 +37,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, hist, block, nblocks, q):
+def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -47,7 +47,9 @@ def _worker(rank, world, port, hist, block, nblocks, q):
     bc = IqBroadcast(torch, dist, "cpu", hist, block, stream=full if rank == 0 else None)
     ok = True
     for i in range(nblocks):
-        t, off = bc.step(i)
+        if pipelined and i + 1 < nblocks:
+            bc.issue(i + 1)  # the next block's broadcast is in flight while block i is used
+        t, off = bc.wait(i) if pipelined else bc.step(i)
         got = t[off - hist: off + block]
         want = full[i * block: i * block + hist + block]
         ok &= bool(torch.equal(got, want))
@@ -57,11 +59,15 @@ def _worker(rank, world, port, hist, block, nblocks, q):
     dist.destroy_process_group()
 
 
-def test_iq_broadcast_world2_gloo():
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_iq_broadcast_world2_gloo(pipelined):
+    """Every rank reconstructs [history | block] windows equal to rank 0's stream, with the
+    broadcasts one at a time or pipelined one block ahead (bench.py's N > 1 loop)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 5, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 7, q, pipelined))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
