@@ -86,7 +86,7 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
                          hipStream_t st, int skip, int tail);
 int wf_tail_split(int logn, int ngroups, int cus);
 bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
-bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_h2 / wf_fft_l32 (not r16)
+bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_l32 (not r16)
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st,

@@ -600,21 +600,6 @@ OWRX_DEV void f2dft32(float2* a) {
     for (int k1 = 0; k1 < 8; ++k1) f2dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
 }
 
-// W_64^m = exp(-2 pi i m / 64), m a compile-time constant after unrolling
-OWRX_DEV float2 w64c(int m) {
-    constexpr float q[17] = {1.00000000000000000f, 0.99518472667219693f, 0.98078528040323043f,
-                             0.95694033573220882f, 0.92387953251128674f, 0.88192126434835505f,
-                             0.83146961230254524f, 0.77301045336273699f, 0.70710678118654757f,
-                             0.63439328416364549f, 0.55557023301960229f, 0.47139673682599781f,
-                             0.38268343236508984f, 0.29028467725446233f, 0.19509032201612833f,
-                             0.09801714032956077f, 0.0f};
-    // cos(2 pi m / 64) over the whole turn from the first quadrant's table
-    auto cs = [&](int v) {
-        v &= 63;
-        return v <= 16 ? q[v] : v <= 32 ? -q[32 - v] : v <= 48 ? -q[v - 32] : q[64 - v];
-    };
-    return make_float2(cs(m), -cs(m - 16));  // sin(2 pi m / 64) = cos(2 pi (m - 16) / 64)
-}
 
 // ---- wf_fft_l32: N = 16384 as 32 x 32 x 16, two LDS exchanges ------------------------------
 // 512 threads of 32 points (two waves per SIMD, up to 256 VGPRs each), one workgroup per CU.
@@ -841,192 +826,6 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     finish();
 }
 
-// ---- wf_fft_h2: N = 16384 as two 8192-point halves, two workgroups per CU ------------------
-// wf_fft_l32 holds a whole frame's image (128 KiB) in one CU's LDS, so one 512-thread workgroup
-// per CU runs its passes in lockstep: while its waves wait at a barrier, for the LDS or for the
-// window loads, nothing else issues (measured: ~20 k cycles per frame against ~6.6 k of VALU).
-// Here one decimation-in-frequency step splits the frame, X[2k + h] = DFT_8192(y_h)[k] with
-//   y_h[n] = (w[n] x[n] + (-1)^h w[n + 8192] x[n + 8192]) W_16384^(h n),   n < 8192,
-// and a 256-thread workgroup transforms one half h of its group's frames through a 64 KiB image,
-// so two independent workgroups share each CU and one's exchanges and barriers run under the
-// other's arithmetic.  Each reads the whole frame (the pair's second read of a frame is an L2
-// hit: the halves of group g are blocks b and b + 8, one XCD under round-robin placement).
-// The 8192-point transform is Stockham radix 32 x 16 x 16, 32 points per thread:
-//  P1 (Ns = 1):   a[r] = y[t + 256 r] (h = 1: times W_64^r) -> DFT32 (h = 1: times W_N^t)
-//                 -> image[32 t + k]
-//  P2 (Ns = 32):  j = t + 256 b (b < 2): image[j + 512 r] * W_512^(r (t & 31)) (LDS table
-//                 [15][32]) -> DFT16 -> image[(j >> 5) 512 + (j & 31) + 32 r]
-//  P3 (Ns = 512): j = t + 256 b: image[j + 512 r] * W_8192^(r j) (bases W_8192^(r t) from four
-//                 exact powers, W_32^(r b)) -> DFT16 -> |Y|^2 of half-bins j + 512 r, summed in
-//                 registers over the group's frames
-// The image uses wf_fft_l32's XOR swizzle (every store and read bank-conflict-free).  The
-// window taps of the thread's 64 samples stay in registers for the whole group.  The partial
-// row is written half-major (bin 2k + h at h 8192 + k), as the DIF-split path's rows are, and
-// wf_finalize reads it back in bin order.
-struct WfH2 {
-    static constexpr int N = 16384, M = 8192, NT = 256;
-    static constexpr int TW2 = M;  // [15][32]: W_512^(r k), r = 1..15
-    static constexpr size_t kLds = sizeof(float2) * (M + 15 * 32);
-};
-
-__global__ void __launch_bounds__(WfH2::NT, 2)
-wf_fft_h2(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
-          int ngroups, const float* __restrict__ window, const float2* __restrict__ tw,
-          float* __restrict__ partial) {
-    using K = WfH2;
-    constexpr int N = K::N, M = K::M, NT = K::NT;
-    extern __shared__ __attribute__((aligned(16))) float2 sm[];
-    const int b0 = blockIdx.x;
-    const int gi = (b0 >> 4) * 8 + (b0 & 7);  // groups in runs of 8 workgroups, halves 8 apart
-    const int h = (b0 >> 3) & 1;
-    if (gi >= ngroups) return;
-    const int t0 = threadIdx.x;
-    WF_RSTAMP(14);
-    WF_STAMP(0);
-    const WfGroup g = groups[gi];
-    const int64_t g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
-    const int hop = __builtin_amdgcn_readfirstlane(g.hop);
-    const int nfr = __builtin_amdgcn_readfirstlane(g.nframes);
-    const auto xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float2*>(blk + g0), 0, (int)(sizeof(float2) * ((int64_t)(nfr - 1) * hop + N)),
-        0x00020000);
-    // samples t + 256 r and their partners + 8192 of frame f, in batches of kB values of r
-    constexpr int kB = 8;
-    auto load_x = [&](int f, int rb, float2* va, float2* vb) {
-        const int vo = t0 * 8 + f * hop * 8;
-#pragma unroll
-        for (int r = 0; r < kB; ++r) {
-            const int so = (rb * kB + r) * NT * 8;
-            va[r] = make_float2(
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, so, 0)),
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, so, 0)));
-            vb[r] = make_float2(
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + M * 8, so, 0)),
-                __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + M * 8 + 4, so, 0)));
-        }
-    };
-    // tables (L2-resident) first: vmcnt retires in order
-    float wa[32], wb[32];
-#pragma unroll
-    for (int r = 0; r < 32; ++r) {
-        wa[r] = window[t0 + NT * r];
-        wb[r] = window[t0 + NT * r + M];
-    }
-    float2 tp[4];  // W_8192^(2^i t) = W_N^(2^(i+1) t): P3's bases W_8192^(r t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) tp[i] = tw[(t0 << (i + 1)) & (N - 1)];
-    const float2 wt = tw[t0];  // W_N^t (h = 1)
-    float2 t2v[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int e = t0 + NT * i;  // 480 entries: (r - 1) * 32 + k, W_512^(r k) = W_N^(32 r k)
-        t2v[i] = e < 15 * 32 ? tw[((((e >> 5) + 1) * (e & 31)) << 5) & (N - 1)] : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-        if (t0 + NT * i < 15 * 32) sm[K::TW2 + t0 + NT * i] = t2v[i];
-    if (h) {
-#pragma unroll
-        for (int r = 0; r < 32; ++r) wb[r] = -wb[r];  // y_1: the partner sample subtracted
-    }
-    float acc[32];
-#pragma unroll
-    for (int m = 0; m < 32; ++m) acc[m] = 0.0f;
-#pragma unroll 1
-    for (int f = 0; f < nfr; ++f) {
-        int t = threadIdx.x;
-        asm volatile("" : "+v"(t));
-        const int sb = 1 + 6 * f;
-        if (f < 2) WF_STAMP(sb);
-        float2 a[32];
-#pragma unroll
-        for (int rb = 0; rb < 32 / kB; ++rb) {
-            float2 va[kB], vb[kB];
-            load_x(f, rb, va, vb);
-#pragma unroll
-            for (int i = 0; i < kB; ++i) {
-                const int r = rb * kB + i;
-                a[r] = make_float2(fmaf(wb[r], vb[i].x, va[i].x * wa[r]),
-                                   fmaf(wb[r], vb[i].y, va[i].y * wa[r]));
-            }
-        }
-        if (h) {  // y_1[n] = (...) W_N^n, n = t + 256 r: W_64^r here, W_N^t after the DFT
-#pragma unroll
-            for (int r = 1; r < 32; ++r) a[r] = (r & 1) ? f2mul(a[r], w64c(r)) : f2mul32(a[r], r >> 1);
-        }
-        f2dft32(a);
-        if (h) {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) a[k] = f2mul(a[k], wt);
-        }
-        if (f < 2) WF_STAMP(sb + 1);
-        __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
-#pragma unroll
-        for (int k = 0; k < 32; ++k) sm[32 * t + (k ^ (t & 15))] = a[l32_at(k)];
-        if (f < 2) WF_STAMP(sb + 2);
-        __syncthreads();
-        // P2: two radix-16 butterflies j = t + 256 b, twiddle W_512^(r (t & 31))
-        {
-            const int k = t & 31;
-            const float2* T = sm + K::TW2 + k;
-            float2 c[2][16];
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) c[b][r] = sm[wf_swz32(t + NT * b + 512 * r)];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) {
-                const float2 w = T[(r - 1) * 32];
-                c[0][r] = f2mul(c[0][r], w);
-                c[1][r] = f2mul(c[1][r], w);
-                if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 twiddles live
-            }
-            f2dft<16>(c[0]);
-            f2dft<16>(c[1]);
-            __syncthreads();  // every P2 read before any P2 store
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int base = ((t >> 5) + 8 * b) * 512 + k;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sm[wf_swz32(base + 32 * r)] = c[b][r];
-            }
-        }
-        if (f < 2) WF_STAMP(sb + 3);
-        __syncthreads();
-        // P3: j = t + 256 b, W_8192^(r j) = W_8192^(r t) W_32^(r b)
-        if (f < 2) WF_STAMP(sb + 4);
-        float2 tb[16];
-        tb[1] = tp[0];
-        tb[2] = tp[1];
-        tb[4] = tp[2];
-        tb[8] = tp[3];
-        tb[3] = f2mul(tp[0], tp[1]);
-        tb[5] = f2mul(tp[0], tp[2]);
-        tb[6] = f2mul(tp[1], tp[2]);
-        tb[7] = f2mul(tb[3], tp[2]);
-#pragma unroll
-        for (int r = 9; r < 16; ++r) tb[r] = f2mul(tb[r - 8], tp[3]);
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            float2 c[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) c[r] = sm[wf_swz32(t + NT * b + 512 * r)];
-#pragma unroll
-            for (int r = 1; r < 16; ++r) c[r] = f2mul(c[r], b ? f2mul32(tb[r], r) : tb[r]);
-            f2dft<16>(c);
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                acc[b + 2 * r] = fmaf(c[r].y, c[r].y, fmaf(c[r].x, c[r].x, acc[b + 2 * r]));
-        }
-        if (f < 2) WF_STAMP(sb + 5);
-    }
-    float* out = partial + (int64_t)gi * N + h * M;  // half-major: bin 2k + h at h M + k
-#pragma unroll
-    for (int m = 0; m < 32; ++m) out[t0 + NT * m] = acc[m];
-    WF_STAMP(13);
-    WF_RSTAMP(15);
-}
-
 // ---- FFT sizes above one CU's LDS (32768, 65536): decimation-in-frequency split ------------
 // N = Q * 16384 (Q = 2, 4): X[Q k + j] = sum_n y_j[n] W_16384^(n k) with
 //   y_j[n] = W_N^(n j) * sum_q w[n + 16384 q] x[n + 16384 q] W_Q^(q j),   n < 16384,
@@ -1135,8 +934,8 @@ wf_fft4_rows(const float2* __restrict__ Y, const float2* __restrict__ tw,
 }
 
 // Each thread sums four consecutive positions of the partial rows (16-B loads; a position is
-// bin i's place in a partial row: natural, or j-major after the DIF split / in wf_fft_h2's
-// half-major rows, bin Q k + j at j (N / Q) + k).  The carried accumulator is kept in position
+// bin i's place in a partial row: natural, or j-major after the DIF split, bin Q k + j at
+// j (N / Q) + k).  The carried accumulator is kept in position
 // order too.
 OWRX_DEV float4 f4add(float4 a, float4 b) {
     return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
@@ -1333,22 +1132,20 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
-// N = 16384: the whole-frame radix-32 kernel wf_fft_l32; OWRX_WF_KERNEL=h2 the half-frame kernel
-// (two workgroups per CU: 68 vs 50 us per 960 C3 frames from HBM, its loads exposed) and =r16
-// the radix-16 one (A/B); 1024 <= N <= 8192: radix 16
-static int wf_n16k_kernel() {  // 0: h2, 1: l32, 2: r16
+// N = 16384: the whole-frame radix-32 kernel wf_fft_l32, OWRX_WF_KERNEL=r16 the radix-16 one
+// (A/B); 1024 <= N <= 8192: radix 16.  (A half-frame kernel with two workgroups per CU,
+// wf_fft_h2, measured 68 vs 50 us per 960 C3 frames, its loads exposed: removed, in the history
+// before this file's round-4 cleanup.)
+static int wf_n16k_kernel() {  // 1: l32, 2: r16
     static const int v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
-        if (s && strcmp(s, "r16") == 0) return 2;
-        if (s && strcmp(s, "h2") == 0) return 0;
-        return 1;
+        return s && strcmp(s, "r16") == 0 ? 2 : 1;
     }();
     return v;
 }
 static bool wf_force_r16() { return wf_n16k_kernel() == 2; }
 
 bool wf_uses_l32(int logn) { return logn == 14 && wf_n16k_kernel() != 2; }
-bool wf_uses_h2(int logn) { return logn == 14 && wf_n16k_kernel() == 0; }
 
 // N = 32768, 65536: the DIF split onto wf_fft_l32 (OWRX_WF_KERNEL=fourstep: the four-step, A/B)
 bool wf_uses_split(int logn) {
@@ -1417,30 +1214,12 @@ static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const W
     return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, work, cus, st, QLOG, fpg);
 }
 
-static hipError_t launch_fft_h2(const float2* blk, int64_t blk_start, const WfGroup* groups,
-                                int ngroups, const float* window, const float2* tw,
-                                float* partial, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_h2,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)WfH2::kLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    // runs of 8 groups: blocks 16 q + 8 h + i hold half h of group 8 q + i
-    hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((ngroups + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, st,
-                       blk, blk_start, groups, ngroups, window, tw, partial);
-    return hipGetLastError();
-}
 
 template <int LOGN>
 static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw, float* partial,
                                  int* work, int cus, hipStream_t st, int skip, int tail) {
     if constexpr (LOGN == 14) {
-        if (wf_uses_h2(LOGN))
-            return launch_fft_h2(blk, blk_start, groups, ngroups, window, tw, partial, st);
         if (!wf_force_r16())
             return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
                                   0, 0, skip, tail);
@@ -1483,8 +1262,8 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
                               const WfGroup* groups, int ngroups, int skip) {
     int logn = 0;
     while ((1 << logn) < N) ++logn;
-    // partial rows half- / sub-frame-major: the DIF split's Q = N / 16384, wf_fft_h2's Q = 2
-    const int qlog = wf_uses_split(logn) ? logn - 14 : wf_uses_h2(logn) ? 1 : 0;
+    // partial rows sub-frame-major after the DIF split (Q = N / 16384)
+    const int qlog = wf_uses_split(logn) ? logn - 14 : 0;
     if (N % 4) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wf_finalize, dim3((N / 4 + 255) / 256, nrows), dim3(256), 0, st, partial,
                        rows, carry_in, carry_out, N, add_corr, adpcm, s16_out, f32_out, qlog,

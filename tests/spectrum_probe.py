@@ -80,10 +80,19 @@ def main(ROOT, REF):
                 entry["graph"] = [describe(m) for m in used]
                 # the chain writes into the Buffer SpectrumThread's pump reads
                 entry["writer_format"] = used[-1].writer.getFormat().name
-        entry["pump_threads"] = sum(1 for t in threading.enumerate()
-                                    if t.is_alive() and "pump" in (t.name or "").lower()
-                                    or getattr(t, "_target", None) is not None and
-                                    "pump" in getattr(getattr(t, "_target"), "__qualname__", ""))
+        def pumps():
+            return sum(1 for t in threading.enumerate()
+                       if t.is_alive() and "pump" in (t.name or "").lower()
+                       or getattr(t, "_target", None) is not None and
+                       "pump" in getattr(getattr(t, "_target"), "__qualname__", ""))
+        # a swapped-out chain's pump ends asynchronously once its reader stops: give it a moment
+        # (counting at once raced with that exit now and then)
+        deadline = time.time() + 2.0
+        n = pumps()
+        while n > len(live) and time.time() < deadline:
+            time.sleep(0.01)
+            n = pumps()
+        entry["pump_threads"] = n
         entry["dsp_output_format"] = st.dsp.getOutputFormat().name if st.dsp else None
         steps.append(entry)
 

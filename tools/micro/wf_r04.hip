@@ -151,7 +151,6 @@ int main(int argc, char** argv) {
                            (int)WfL32::kLds));
 #define SETX(v) CK(hipFuncSetAttribute((const void*)wf_fft_l32x<v>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WfL32::kLds))
     SETX(0); SETX(1); SETX(2); SETX(3); SETX(4); SETX(5); SETX(6);
-    CK(hipFuncSetAttribute((const void*)wf_fft_h2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WfH2::kLds));
     printf("N=%d hop=%d, frames from %s\n", N, hop, flush_on() ? "HBM (512 MiB flushed between launches)" : "cache");
     // CU-masked streams (the engine's stream A masks 16 CUs off for the serial streams):
     // bits [0, 240) as create_streams does, and 240 CUs with every 16th bit off instead
@@ -264,10 +263,6 @@ int main(int argc, char** argv) {
                 {"l32 mask-every16", [&] {
                      l32(G, s_even);
                  }, false, false, s_even},
-                {"h2", [&] {
-                     hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx,
-                                        (int64_t)0, dg, G, dwin, dtw, dpart);
-                 }, true, true},
 #define XV(v, nm) {nm, [&] { hipLaunchKernelGGL(wf_fft_l32x<v>, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, dg, dwin, dtw, dpart); }, v == 0}
                 XV(0, "x0"), XV(1, "x-load"), XV(2, "x-lds"), XV(3, "x-ld-lds"), XV(4, "x-math"), XV(5, "x-ld-mth"), XV(6, "x-lds-mth"),
                 {"mem", [&] {
@@ -361,7 +356,6 @@ int main(int argc, char** argv) {
                     printf("\n");
                 }
                 stamps("x0", G, [&] { hipLaunchKernelGGL(wf_fft_l32x<0>, dim3(G), dim3(WfL32::NT), WfL32::kLds, 0, dx, dg, dwin, dtw, dpart); });
-                stamps("h2", 2 * G, [&] { hipLaunchKernelGGL(wf_fft_h2, dim3(16 * ((G + 7) / 8)), dim3(WfH2::NT), WfH2::kLds, 0, dx, (int64_t)0, dg, G, dwin, dtw, dpart); });
             }
 #endif
         }
