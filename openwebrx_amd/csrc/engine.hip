@@ -1947,9 +1947,11 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     }
     const int np = S.np;
     const double t_launch = now_ms();
+    bool in_recorded = false;  // evIn of this block recorded (it doubles as the A -> B event)
     e->stats.host_ms_build += t_launch - t_build;
     // every descriptor of the block in one upload: the groups' DDC descriptors, the posts, the
-    // serial lane lists and the long-bandpass list (stream B / C read them after event evA)
+    // serial lane lists and the long-bandpass list (stream B / C read them after stream A's
+    // block event)
     {
         int nj = 0;
         int64_t maxb = 0;
@@ -2031,7 +2033,10 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                                     S.long_taps, e->sA));
         for (int lg = 0; lg < 32; ++lg)
             if (S.sf_sizes & (1u << lg)) HIPCHK(launch_chain_sfft(lg, S.d_posts, np, S.d_counts, e->sA));
-        HIPCHK(hipEventRecord(S.evA, e->sA));
+        // stream A's last work of the block (the input's last reader too): one event serves both
+        // stream B's wait and the input-retention check (evIn), one HIP call fewer per block
+        HIPCHK(hipEventRecord(e->evIn[e->block_index % kInEv], e->sA));
+        in_recorded = true;
         // serial streams for this block: the CU-masked pair, or past kWideSerialChains chains
         // (more waves than their CUs hold) the unmasked pair; on a switch the new pair first
         // waits for the old pair's last block, so every chain's state stays in block order
@@ -2049,7 +2054,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             HIPCHK(hipEventDestroy(fc));
             e->serial_wide = wide;
         }
-        HIPCHK(hipStreamWaitEvent(sB, S.evA, 0));
+        HIPCHK(hipStreamWaitEvent(sB, e->evIn[e->block_index % kInEv], 0));
         // NoiseFilter resets the rebuild asked for (a fresh NoiseFilter: ClientAudioChain.
         // _updateConverter), on the serial stream in use, before this block's serial work
         for (Chain* c : e->nr_resets) {
@@ -2104,7 +2109,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         HIPCHK(hipEventRecord(S.a3, e->sA));
         S.timed = true;
     }
-    HIPCHK(hipEventRecord(e->evIn[e->block_index % kInEv], e->sA));
+    if (!in_recorded) HIPCHK(hipEventRecord(e->evIn[e->block_index % kInEv], e->sA));
     e->stats.host_ms_launch += now_ms() - t_launch;
     if (!wait_first) {  // the oldest input the caller may reuse now (see the top)
         const double t = now_ms();
