@@ -29,7 +29,7 @@ for st in "$@"; do
     benchab)
       for v in default $AB; do
         if [ "$v" = default ]; then envs=""; else envs="${v//+/ }"; fi
-        eval env $envs timeout -k 10 300 python -u bench.py $SHORT --extra-block 0 ${BARGS} > gpurun_out/${TAG}_ab_${v//[=,+]/_}.json 2> gpurun_out/${TAG}_ab_${v//[=,+]/_}.err || exit $?
+        eval env $envs timeout -k 10 300 python -u bench.py $SHORT --extra-block 0 ${BARGS} > gpurun_out/${TAG}_ab_${v//[=,+.\/]/_}.json 2> gpurun_out/${TAG}_ab_${v//[=,+.\/]/_}.err || exit $?
       done ;;
     prof) eval timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o bench \
         -- python3 -u bench.py $SHORT --steps 20 --warmup 10 ${BARGS} > gpurun_out/${TAG}_prof.json 2> gpurun_out/${TAG}_prof.log || exit $? ;;
