@@ -101,7 +101,7 @@ int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t nsamples);
  * blocks = r the block handed to owrx_process_device (with its history) must stay unmodified
  * until r further owrx_process_device / owrx_commit calls (or owrx_sync) have returned, and the
  * engine waits only for block k - r + 1's stream-A work before returning from block k, so the
- * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 15. */
+ * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 31. */
 int owrx_set_input_retention(owrx_engine* e, int blocks);
 /* Blocks of chain work in flight (streams A -> B -> C -> host rings), 1..16, default 8; only
  * before the first chain and block.  Each one holds pinned and device staging for every chain

@@ -141,7 +141,8 @@ constexpr int kDebugStages = 6;
 #endif
 constexpr int kSlots = OWRX_SLOTS;  // the most blocks of chain work in flight (A -> B -> C)
 constexpr int kDefaultSlots = 8;    // owrx_set_pipeline_depth: the engine's own (e->nslots)
-constexpr int kInEv = 16;          // stream-A completion events kept (block index mod kInEv)
+constexpr int kInEv = 2 * kSlots;   // stream-A completion events kept (block index mod kInEv;
+                                   // > kSlots: the slot-reuse wait reads block k - nslots's)
 constexpr int kRowSlots = 4;  // waterfall row blocks in flight (each on its own stream, R CUs)
 
 #define HIPCHK(expr)                                                                    \
@@ -643,6 +644,12 @@ struct owrx_engine {
     int64_t max_block = 0;
     int cus_a = 0;  // CUs of stream A (DDC launch shape)
     std::vector<float> wf_ms_log;  // timed waterfall launches (OWRX_WF_LOG=1: printed at destroy)
+    // host time of the slot drains (OWRX_HOST_LOG=1: printed at destroy): the wait for the
+    // block's stream-R event and the ring pushes, split by forced (process_block's slot reuse)
+    // and opportunistic (the collect after each block)
+    double hl_wait[2] = {}, hl_push[2] = {};
+    int64_t hl_n[2] = {};
+    bool hl_forced = false;
     int64_t history = kDefaultHistory;
     int64_t pos = 0;  // absolute samples processed
     int64_t block_index = 0;
@@ -991,7 +998,12 @@ static void free_slot_staging(Slot& s) {
 static int drain_slot(owrx_engine* e, int si) {
     Slot& s = e->slots[si];
     if (s.chains_pending) {
+        const int hk = e->hl_forced ? 1 : 0;
+        const double th0 = now_ms();
         RCCHK(wait_ev(e, s.evB));
+        const double th1 = now_ms();
+        e->hl_wait[hk] += th1 - th0;
+        e->hl_n[hk]++;
         s.chains_pending = false;
         if (s.timed) {
             float ms = 0;
@@ -1060,6 +1072,7 @@ static int drain_slot(owrx_engine* e, int si) {
         e->stats.overruns += ov.load();
         e->stats.audio_bytes += ab.load();
         e->stats.ddc_outputs += dd.load();
+        e->hl_push[hk] += now_ms() - th1;
     } else if (s.timed) {
         float ms = 0;
         RCCHK(wait_ev(e, s.a3));
@@ -1868,7 +1881,10 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     // (and its stream-A work done: a block without chain outputs drains without a wait)
     {
         const double t = now_ms();
-        RCCHK(drain_slots(e, true, e->nslots - 1));
+        e->hl_forced = true;
+        const int rc = drain_slots(e, true, e->nslots - 1);
+        e->hl_forced = false;
+        RCCHK(rc);
         RCCHK(wait_input_block(e, e->block_index - e->nslots));
         e->stats.host_ms_wait_slots += now_ms() - t;
     }
@@ -2347,6 +2363,11 @@ int owrx_engine_destroy(owrx_engine* e) {
         for (float v : e->wf_ms_log) fprintf(stderr, " %.3f", v);
         fprintf(stderr, "\n");
     }
+    if (getenv("OWRX_HOST_LOG"))
+        for (int k = 0; k < 2; ++k)
+            fprintf(stderr, "owrx %s slot drains: %lld, wait %.3f ms, pushes %.3f ms (per drain %.4f / %.4f)\n",
+                    k ? "forced" : "collect", (long long)e->hl_n[k], e->hl_wait[k], e->hl_push[k],
+                    e->hl_n[k] ? e->hl_wait[k] / e->hl_n[k] : 0.0, e->hl_n[k] ? e->hl_push[k] / e->hl_n[k] : 0.0);
     // every stream drained, within the stall bound (a stalled engine gets one more bound to
     // finish; if its work still has not completed, its buffers are leaked rather than freed
     // under a running kernel, and the process keeps going)
