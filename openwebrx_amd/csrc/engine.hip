@@ -92,7 +92,7 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st,
                               const WfGroup* groups, int ngroups, int skip);
 hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, int row_bytes,
-                           hipStream_t st);
+                           int wgs, hipStream_t st);
 hipError_t launch_ddc(int P, const float2* blk, int64_t blk_start, int64_t blk_end,
                       const float* taps_poly, const DdcChain* chains, int nchains, int D,
                       int64_t k_begin, int nk, int nseg, float2* partial, hipStream_t st);
@@ -643,6 +643,7 @@ struct owrx_engine {
     double samp_rate = 0;
     int64_t max_block = 0;
     int cus_a = 0;  // CUs of stream A (DDC launch shape)
+    int rows_grid = 0;  // the row encoder's grid (2 x the row queue's CUs; 0: one per row)
     std::vector<float> wf_ms_log;  // timed waterfall launches (OWRX_WF_LOG=1: printed at destroy)
     // host time of the slot drains (OWRX_HOST_LOG=1: printed at destroy): the wait for the
     // block's stream-R event and the ring pushes, split by forced (process_block's slot reuse)
@@ -1617,7 +1618,7 @@ static int run_waterfalls(owrx_engine* e, const float2* blk, int64_t blk_start, 
                 const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
                 if (w->pend_adpcm[ri]) {
                     HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
-                                           R.stream));
+                                           e->rows_grid, R.stream));
                     HIPCHK(kcopy(w->h_bytes[ri], w->d_bytes[ri], rb * nr, R.stream));
                 } else {
                     HIPCHK(kcopy(w->h_bytes[ri], w->d_f32[ri], rb * nr, R.stream));
@@ -2211,6 +2212,7 @@ static hipError_t create_streams(owrx_engine* e) {
         else if (k != 4) nb = nc = nr = 0;
     }
     e->cus_a = ncu;
+    e->rows_grid = 2 * ncu;
     if (nb <= 0 || nc <= 0 || nr <= 0 || nw < 0 || nb + nc + nr + nw > ncu / 2) {
         for (hipStream_t* st : {&e->sA, &e->sB, &e->sC, &e->sR}) {
             err = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
@@ -2230,6 +2232,12 @@ static hipError_t create_streams(owrx_engine* e) {
     };
     const int a_end = ncu - nb - nc - nr - nw;
     e->cus_a = a_end;
+    // the row encoder's grid: twice the row queue's CUs (measured: 2, 3, 4, 6, 8 workgroups on
+    // its 4 CUs took 4.5, 3.1, 2.5, 1.8, 1.5 ms per batch against 1.4 with one per row, which
+    // stalled stream R's gathers; profiles/r04_rows_grid_ab.txt).  OWRX_ROWS_GRID=rows: one
+    // workgroup per row (the round-4 grid), =<n>: n (A/B)
+    e->rows_grid = 2 * (nw > 0 ? nw : nr);
+    if (const char* v = getenv("OWRX_ROWS_GRID")) e->rows_grid = strcmp(v, "rows") == 0 ? 0 : atoi(v);
     const std::vector<uint32_t> mA = mask_range(0, a_end);
     const std::vector<uint32_t> mB = mask_range(a_end, a_end + nb);
     const std::vector<uint32_t> mC = mask_range(a_end + nb, a_end + nb + nc);

@@ -14,8 +14,8 @@
 // wf_fft4_cols / wf_fft4_rows (N = 32768, 65536): four-step FFT through a cf32 scratch frame.
 // wf_finalize: sums each row's group partials in a fixed order onto the carried accumulator
 //   (rows span blocks), 10*log10 + add_db correction, fftshift, quantise (short)(dB*100).
-// wf_adpcm_rows_spec: FftAdpcm (IMA-ADPCM of each padded row), one workgroup per row,
-//   segment-parallel and exact (adpcm_spec.h).
+// wf_adpcm_rows_spec: FftAdpcm (IMA-ADPCM of each padded row), one workgroup per row at a
+//   time, segment-parallel and exact (adpcm_spec.h).
 #include <algorithm>
 #include <stdlib.h>
 #include <string.h>
@@ -1044,10 +1044,11 @@ wf_adpcm_rows_spec(const int16_t* __restrict__ s16, int N, int nrows, uint8_t* _
     extern __shared__ __align__(16) uint8_t smem[];
     SpecLds<kRowWin>& L = *reinterpret_cast<SpecLds<kRowWin>*>(smem);
     const int tid = threadIdx.x;
-    const int row = blockIdx.x;
     for (int i = tid; i < 89; i += kSpecThreads) L.T[i] = kAdpcmStep[i];
     adpcm_tab_fill(L.NS, tid, kSpecThreads);
     const int M = N + 10;
+    // rows dealt round-robin over a grid that fits its CUs at once (launch_wf_adpcm)
+    for (int row = blockIdx.x; row < nrows; row += gridDim.x) {
     const int16_t* x = s16 + (int64_t)row * N;
     uint8_t* o = out + (int64_t)row * row_bytes;
     uint32_t state = 0;  // FftAdpcm restarts every row at (index 0, predictor 0)
@@ -1066,6 +1067,7 @@ wf_adpcm_rows_spec(const int16_t* __restrict__ s16, int N, int nrows, uint8_t* _
             o[w0 / 2 + i] = (uint8_t)((L.code[spec_at(gm, 2 * i)] & 15) |
                                       (L.code[spec_at(gm, 2 * i + 1)] << 4));
         state = L.traj[spec_at(gm, nw - 1)];
+    }
     }
 }
 
@@ -1271,8 +1273,13 @@ hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows
     return hipGetLastError();
 }
 
+// grid: at most `wgs` workgroups (2 x the row queue's CUs), rows looped inside.  A grid of one
+// workgroup per row kept workgroups waiting for CUs, and while they waited the command
+// processor's pipe dispatched nothing else: stream R's output gathers, which share that pipe
+// (engine.hip create_streams), stalled 0.4-0.85 ms once per waterfall batch
+// (profiles/r04_rows_grid_ab.txt).
 hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, int row_bytes,
-                           hipStream_t st) {
+                           int wgs, hipStream_t st) {
     const size_t lds = sizeof(SpecLds<kRowWin>);
     static bool attr = false;
     if (!attr) {
@@ -1281,7 +1288,9 @@ hipError_t launch_wf_adpcm(const int16_t* s16, int N, int nrows, uint8_t* out, i
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(wf_adpcm_rows_spec, dim3(nrows), dim3(kSpecThreads), lds, st, s16, N,
+    if (nrows <= 0) return hipSuccess;
+    const int grid = wgs > 0 ? std::min(nrows, wgs) : nrows;
+    hipLaunchKernelGGL(wf_adpcm_rows_spec, dim3(grid), dim3(kSpecThreads), lds, st, s16, N,
                        nrows, out, row_bytes);
     return hipGetLastError();
 }

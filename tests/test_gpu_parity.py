@@ -379,8 +379,9 @@ def test_waterfall_reconfigure_without_drain(amd):
     ref = np.stack(refs)
     assert rows.shape[0] >= ref.shape[0] - 1 and rows.shape[0] <= ref.shape[0], (rows.shape, ref.shape)
     k = rows.shape[0]
-    err = np.max(np.abs(rows[:k] - ref[:k]))
-    assert err < 2e-3, err
+    per_row = np.max(np.abs(rows[:k] - ref[:k]), axis=1)
+    err = np.max(per_row)
+    assert err < 2e-3, (err, np.nonzero(per_row >= 2e-3)[0].tolist(), k, ref.shape[0], switches)
 
 
 def test_input_retention_same_outputs(amd):
