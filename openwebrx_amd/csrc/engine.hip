@@ -332,6 +332,9 @@ struct Waterfall {
     uint8_t* h_bytes[kRowSlots] = {};
     int pend_rows[kRowSlots] = {};
     int pend_adpcm[kRowSlots] = {};
+    // the host buffer each row slot's copies went to: a reconfiguration (wf_reserve) may replace
+    // h_bytes[ri] while the slot is in flight, and its drain must read the one the GPU wrote
+    uint8_t* pend_h[kRowSlots] = {};
     std::vector<double> pend_t[kRowSlots];  // readiness time of each row in the slot
     ByteRing ring;
     std::vector<WfGroup> groups;
@@ -1120,7 +1123,7 @@ static int drain_rows(owrx_engine* e, bool block, int keep) {
             const int nr = w->pend_rows[ri];
             if (nr <= 0) continue;
             const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
-            w->ring.push(w->h_bytes[ri], (size_t)(rb * nr));
+            w->ring.push(w->pend_h[ri], (size_t)(rb * nr));
             w->rows += nr;
             e->stats.waterfall_rows += nr;
             w->pend_rows[ri] = 0;
@@ -1586,6 +1589,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     e->stats.waterfall_launches++;
     w->pend_rows[ri] = ncomplete;
     w->pend_adpcm[ri] = adpcm_now;
+    w->pend_h[ri] = w->h_bytes[ri];
     *completed = ncomplete;
     return OWRX_OK;
 }
