@@ -754,11 +754,12 @@ def main():
     wf_batch = 0
     if world == 1 and not args.no_waterfall:
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        # eight frames per stream-A CU for the 16384-point kernel (two groups of 4 per
-        # workgroup: its start-up and first frame amortise over twice the frames, 0.187 vs
-        # 0.156 of HBM at C3); two per CU above it (each frame is 4 or 2 sub-frames of that
-        # kernel after the DIF split).  The row-latency cap bounds the wait at real-time rates.
-        per_cu = 8 if n_fft <= 16384 else 2
+        # sixteen frames per stream-A CU for the 16384-point kernel (two groups of 8 per
+        # workgroup: its start-up and first frame amortise over the frames, 0.294 vs 0.259 of
+        # HBM at 8 per CU in the micro, profiles/r05_wf_micro.txt); two per CU above it (each
+        # frame is 4 or 2 sub-frames of wf_fft_l32 after the DIF split).  The row-latency cap
+        # bounds the wait at real-time rates.
+        per_cu = 16 if n_fft <= 16384 else 2
         wf_batch = per_cu * max(1, cus - 16) if args.wf_batch < 0 else args.wf_batch
     history = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
     eng = Engine(fs, max_block=block, device=local, history=history)
@@ -912,13 +913,14 @@ def main():
     wf_ms = d["gpu_ms_waterfall"]
     post_ms = d["gpu_ms_post"]
     wf_launches = d["waterfall_launches"]
+    wf_tlaunches = d["waterfall_timed_launches"]
     # waterfall roofline (HBM-bound, 8 B of cf32 per input sample read once):
     # algorithmic bytes of the frames the timed FFT launches advanced over / their HIP-event time
     wf_fft_ms = d["gpu_ms_waterfall_fft"]
     wf_bytes = 8.0 * d["waterfall_timed_samples"]
     wf_gbs = wf_bytes / (wf_fft_ms / 1e3) / 1e9 if wf_fft_ms > 0 else None
     wf_kernels = (["wf_dif_split", "wf_fft_l32", "wf_finalize"] if n_fft > 16384 else
-                  ["wf_fft_l32", "wf_finalize"])
+                  ["wf_fft_q16", "wf_finalize"])
     wf_traffic, wf_traffic_src = 0, []
     for kname in wf_kernels:
         b, src = pmc_traffic(kname, args.config)
@@ -1061,10 +1063,14 @@ def main():
                     "unit": "GB/s",
                     "frac": round(wf_gbs / HBM_PEAK_GBS, 4),
                     "traffic": wf_traffic,
-                    "algorithmic_bytes_per_launch": round(wf_bytes / max(1, wf_launches)),
-                    "frames_per_launch": round(d["waterfall_frames"] / max(1, wf_launches), 1),
-                    "launches": wf_launches,
-                    "ms_per_launch": round(wf_fft_ms / max(1, wf_launches), 4),
+                    # per TIMED launch (the launches the HIP events covered): the bytes are
+                    # frames x hop x 8 of exactly those launches, as `achieved` uses
+                    "algorithmic_bytes_per_launch": round(wf_bytes / max(1, wf_tlaunches)),
+                    "frames_per_launch": round(d["waterfall_timed_samples"] / hop / max(1, wf_tlaunches), 1),
+                    "launches": wf_tlaunches,
+                    "ms_per_launch": round(wf_fft_ms / max(1, wf_tlaunches), 4),
+                    "all_launches": wf_launches,
+                    "all_frames_per_launch": round(d["waterfall_frames"] / max(1, wf_launches), 1),
                     "note": "achieved = 8 B x the stream samples the timed launches' frames advanced "
                             "over (frames x hop) / the HIP-event time of those launches (FFT + "
                             "finalize) on stream A; traffic from rocprofv3 PMC passes: "

@@ -307,6 +307,8 @@ typedef struct {
      * far: none should happen while blocks stream, since each stalls the GPU's running kernels */
     int64_t pool_allocs;
     double  gpu_ms_waterfall_fft_max;  /* the longest timed waterfall FFT + finalize launch */
+    int64_t waterfall_timed_launches;  /* the launches gpu_ms_waterfall_fft and
+                                          waterfall_timed_samples cover */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

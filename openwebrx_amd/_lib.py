@@ -114,6 +114,7 @@ class Stats(ctypes.Structure):
         ("ddc_mac_kslices_max", ctypes.c_int64),
         ("pool_allocs", ctypes.c_int64),
         ("gpu_ms_waterfall_fft_max", ctypes.c_double),
+        ("waterfall_timed_launches", ctypes.c_int64),
     ]
 
 

@@ -86,7 +86,8 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
                          hipStream_t st, int skip, int tail);
 int wf_tail_split(int logn, int ngroups, int cus);
 bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
-bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_l32 (not r16)
+bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_q16 / l32 (not r16)
+int wf_default_fpg(int logn);
 hipError_t launch_wf_finalize(const float* partial, const WfRow* rows, int nrows,
                               const float* carry_in, float* carry_out, int N, float add_corr,
                               int adpcm, int16_t* s16_out, float* f32_out, hipStream_t st,
@@ -124,9 +125,8 @@ hipError_t launch_chain_sfft(int logn, const ChainPost* posts, int nposts, Chain
                              hipStream_t st);
 hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const int* sel, int nsel,
                             hipStream_t st);
-hipError_t launch_signal_block(int64_t* ready, int64_t v, hipStream_t st);
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
-                              int nsel, const int64_t* ready, int64_t want, hipStream_t st);
+                              int nsel, hipStream_t st);
 
 constexpr int kWfMaxFramesPerGroup = 16;  // frames one FFT workgroup sums (N <= kWfLdsMaxN)
 constexpr int kWfLdsMaxN = 16384;      // largest FFT held in one CU's LDS
@@ -665,7 +665,6 @@ struct owrx_engine {
     double block_interval_ms = 0;    // running estimate of the interval between block calls
     int64_t stall_ms = 20000;        // the longest any host-side wait blocks before failing
     hipEvent_t evSync = nullptr;     // marker for bounded stream synchronisation
-    int64_t* d_ready = nullptr;      // stream B's last published block + 1 (signal_block)
     std::unique_ptr<HostPool> pool;  // host workers for per-chain loops (created on first use)
     bool debug = false;
     int timing = 0;                  // timing events every `timing` blocks (0: off)
@@ -881,6 +880,18 @@ static void rowrel(owrx_engine* e, T*& p, bool pinned) {
     p = nullptr;
 }
 
+// Has stream A finished block j's work?  Non-blocking: evIn[j % kInEv] holds block j or a later
+// block (stream order: a later block done implies j done).
+static bool stream_a_done(owrx_engine* e, int64_t j) {
+    if (j <= e->in_done || j < 0) return true;
+    if (hipEventQuery(e->evIn[j % kInEv]) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    e->in_done = std::max(e->in_done, j);
+    return true;
+}
+
 static void pool_collect(owrx_engine* e) {
     size_t k = 0;
     for (const auto& r : e->pool_retired) {
@@ -891,8 +902,14 @@ static void pool_collect(owrx_engine* e) {
     }
     e->pool_retired.resize(k);
     k = 0;
+    // pinned copy sources (the waterfall's group / row descriptors) are read by stream-A kernel
+    // copies of the blocks before r.block.  A drained slot does not prove that: a block with no
+    // chain outputs and no timing drains without waiting for any event, so slot_tail can pass
+    // blocks whose stream-A copies have not run yet, and a host memcpy into the reused buffer is
+    // not stream-ordered.  So these wait for stream A itself (or an owrx_sync drain, which syncs
+    // it and sets in_done).
     for (const auto& r : e->hpool_retired) {
-        if (r.block <= e->slot_tail)
+        if (r.block <= e->slot_tail && stream_a_done(e, r.block - 1))
             e->hpool_free[e->hpool_size[r.p]].push_back(r.p);
         else
             e->hpool_retired[k++] = r;
@@ -1161,7 +1178,7 @@ static int drain_slots(owrx_engine* e, bool block, int keep) {
         RCCHK(drain_slot(e, si));
         e->slot_tail++;
     }
-    if (!e->pool_retired.empty()) pool_collect(e);
+    if (!e->pool_retired.empty() || !e->hpool_retired.empty()) pool_collect(e);
     return OWRX_OK;
 }
 
@@ -1423,11 +1440,11 @@ static int wf_frames_per_group(const owrx_engine* e, const Waterfall* w) {
         if (!wf_uses_split(w->logn)) return 1;
         fpg = kWfSplitMaxFpg;
     } else if (wf_uses_l32(w->logn)) {
-        static const int l32_fpg = [] {  // OWRX_WF_FPG: frames per group of wf_fft_l32 (A/B)
+        static const int l32_fpg = [] {  // OWRX_WF_FPG: frames per group (A/B)
             const char* v = getenv("OWRX_WF_FPG");
-            return v ? std::max(1, std::min(16, atoi(v))) : 4;
+            return v ? std::max(1, std::min(16, atoi(v))) : 0;
         }();
-        fpg = l32_fpg;
+        fpg = l32_fpg ? l32_fpg : wf_default_fpg(w->logn);
     } else {
         fpg = std::min<int64_t>((frames + cus - 1) / cus, kWfMaxFramesPerGroup);
     }
@@ -1569,6 +1586,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     if (tm) {
         HIPCHK(hipEventRecord(S->w0, e->sA));
         e->stats.waterfall_timed_samples += nfr * w->hop;
+        e->stats.waterfall_timed_launches++;
     }
     HIPCHK(launch_wf_fft(w->logn, blk, blk_start, w->d_groups, ngroups, w->fpg,
                          w->d_window, w->d_ones, w->d_tw, w->d_partial, w->d_y4, w->d_work,
@@ -2094,23 +2112,12 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                                           S.nsel[o][nr], o, dbg, nr, sB));
         if (S.any_nr) HIPCHK(launch_chain_nr(S.d_posts, np, S.d_counts, sB));
         HIPCHK(hipEventRecord(S.evF, sB));
-        // stream C: ADPCM encoders (serial per chain, in block order) and the copies to host,
-        // behind stream B's event.  OWRX_HANDOFF=kernel instead lets the encoder wait for stream
-        // B's block inside the kernel (signal_block / wait_block, no cross-stream event between
-        // back-to-back encoders; B and C on disjoint CUs only).  Off by default: in the C3 bench
-        // one encoder waited out its 10 s bound at the warm-up -> timed transition (twice in two
-        // runs, profiles/r04d_handoff_stall.txt), i.e. stream B's signal was held behind it.
-        static const bool handoff = [] {
-            const char* v = getenv("OWRX_HANDOFF");
-            return v && strcmp(v, "kernel") == 0;
-        }();
+        // stream C: ADPCM encoders (serial per chain, in block order) behind stream B's event.
+        // (Round 4's in-kernel hand-off -- the encoder polling a flag stream B raised -- stalled
+        // for its full 10 s bound and was removed in round 5: DESIGN.md §4, "A stall of our own".)
+        HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
         const int nad = S.nsel[1][0] + S.nsel[1][1];
-        const bool in_kernel = handoff && !wide && e->d_ready && nad > 0;
-        // (the block counter is only read by an in-kernel wait: no launch per block without one)
-        if (e->d_ready && handoff) HIPCHK(launch_signal_block(e->d_ready, e->block_index + 1, sB));
-        if (!in_kernel) HIPCHK(hipStreamWaitEvent(sC, S.evF, 0));
-        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + S.off[1][0], nad,
-                                  in_kernel ? e->d_ready : nullptr, e->block_index + 1, sC));
+        HIPCHK(launch_chain_adpcm(S.d_posts, S.d_counts, S.d_sel + S.off[1][0], nad, sC));
         if (timed) HIPCHK(hipEventRecord(S.b1, sC));
         // the copies to host go on stream R (behind this block's encoder), so stream C runs
         // encoders back to back: its kernel is the pipeline's longest serial stage
@@ -2327,9 +2334,6 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
     };
     if (create_streams(e) != hipSuccess) return fail("stream");
     if (hipEventCreateWithFlags(&e->evSync, hipEventDisableTiming) != hipSuccess) return fail("event");
-    if (hipMalloc(&e->d_ready, sizeof(int64_t)) != hipSuccess ||
-        hipMemset(e->d_ready, 0, sizeof(int64_t)) != hipSuccess)
-        return fail("hand-off flag");
     for (auto& r : e->rslots) {
         if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
@@ -2426,7 +2430,6 @@ int owrx_engine_destroy(owrx_engine* e) {
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamDestroy(st);
     if (e->evSync) hipEventDestroy(e->evSync);
-    if (e->d_ready) hipFree(e->d_ready);
     delete e;
     return OWRX_OK;
 }

@@ -1005,62 +1005,16 @@ constexpr int kAdGroups = kAdChunk / 8;
 
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 
-// Block hand-off from stream B without a stream-level dependency (ready != nullptr): the
-// encoder of block k is enqueued on stream C with no event wait and waits here, in the kernel,
-// until stream B's signal_block has published `want` (= k + 1) -- the next encoder starts as the
-// previous one ends (one in-stream kernel boundary) instead of behind a cross-stream event
-// (10-14 us per block on the loaded chip).  Used only where streams B and C own disjoint CUs
-// (a waiting encoder can never hold the CUs its producer needs).  The wait is bounded: past
-// kHandoffTimeout it gives up (the host's bounded wait then reports the stall).
-constexpr uint64_t kHandoffTimeout = 1000000000ull;  // 10 s of the 100 MHz real-time counter
-
-// the current value of *p through a returning atomic add of 0 (resolved at the memory side,
-// where every XCD's writes meet); inline, so no pass turns the idempotent add into a load
-OWRX_DEV int64_t atomic_peek(const int64_t* p) {
-    int64_t v;
-    const int64_t zero = 0;
-    asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)"
-                 : "=&v"(v) : "v"(p), "v"(zero) : "memory");
-    return v;
-}
-
-OWRX_DEV void wait_block(const int64_t* ready, int64_t want) {
-    if (threadIdx.x == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        // a returning atomic per poll: resolved where every XCD sees the latest value (a plain
-        // or sc1 load can keep hitting a stale copy of the line in this XCD's L2 while the chip
-        // is idle -- measured: one encoder spun to its timeout)
-        while (atomic_peek(ready) < want) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kHandoffTimeout) break;
-        }
-        // stream B's stores (released at its kernels' ends) are read through this CU's L1
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-
-// stream B's publication of block `v - 1`: behind its serial kernels on the stream
-__global__ void __launch_bounds__(64) signal_block(int64_t* ready, int64_t v) {
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_max(ready, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
 template <bool T2>  // T2: the byte-addressed successor table (adpcm_encode_tab2; A/B)
 __global__ void __launch_bounds__(128)
 chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
-            const int* __restrict__ sel, int nsel, const int64_t* ready, int64_t want) {
+            const int* __restrict__ sel, int nsel) {
     __shared__ __align__(16) uint32_t NS[T2 ? kAdpcmTab2Entries : kAdpcmTabEntries];
     __shared__ uint4 ring[2][kAdGroups][64];  // [slot][group][lane]: 8 int16 samples
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     if constexpr (T2) adpcm_tab2_fill(NS, threadIdx.x, 128);
     else adpcm_tab_fill(NS, threadIdx.x, 128);  // (array references: the extent is checked)
-    if (ready) wait_block(ready, want);  // (the tables fill while stream B finishes)
     const SerLane sl = ser_lane(sel, nsel);
     const int c = sl.c;
     const ChainPost* Pp = posts + c;
@@ -1238,13 +1192,8 @@ hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_signal_block(int64_t* ready, int64_t v, hipStream_t st) {
-    hipLaunchKernelGGL(signal_block, dim3(1), dim3(64), 0, st, ready, v);
-    return hipGetLastError();
-}
-
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
-                              int nsel, const int64_t* ready, int64_t want, hipStream_t st) {
+                              int nsel, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
     // the byte-addressed successor table (default: 564-567 vs 573-574 us per C3 block, same box,
     // profiles/r02ab_ab_adpcm_tab2_c3.txt); OWRX_AD_TAB=1: the index-row table (A/B)
@@ -1254,10 +1203,10 @@ hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const
     }();
     if (t2)
         hipLaunchKernelGGL(chain_adpcm<true>, dim3((nsel + 63) / 64), dim3(128), 0, st, posts, counts,
-                           sel, nsel, ready, want);
+                           sel, nsel);
     else
         hipLaunchKernelGGL(chain_adpcm<false>, dim3((nsel + 63) / 64), dim3(128), 0, st, posts,
-                           counts, sel, nsel, ready, want);
+                           counts, sel, nsel);
     return hipGetLastError();
 }
 

@@ -323,11 +323,28 @@ __device__ unsigned long long g_wf_stamp[1024][16];
         if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < 16)                                \
             g_wf_stamp[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();                     \
     } while (0)
+#ifdef OWRX_WF_WSTAMPS
+// per-wave stamps (wf_fft_q16, frame 2 of the first item): [workgroup][wave][slot]
+__device__ unsigned long long g_wf_wstamp[256][16][8];
+// (held in registers during the frame -- a global store per stamp queues behind the frame's
+// loads and would itself delay the wave -- and stored after the frame loop)
+#define WF_WSTAMP(i)                                                                          \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        wst_[i] = __builtin_readcyclecounter();                                               \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+    } while (0)
+#endif
 #else
 #define WF_STAMP(i) \
     do {            \
     } while (0)
 #define WF_RSTAMP(i) \
+    do {             \
+    } while (0)
+#endif
+#ifndef OWRX_WF_WSTAMPS
+#define WF_WSTAMP(i) \
     do {             \
     } while (0)
 #endif
@@ -826,6 +843,318 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     finish();
 }
 
+// ---- wf_fft_q16: N = 16384 as 16 x 16 x 64, 1024 threads of 16 points -------------------------
+// Four waves per SIMD (the LDS exchanges reach their full rate there; at two per SIMD the 8-B
+// stores ran at about half of it) and the window taps resident in registers.
+//   n = n1 + 1024 n2, n1 = n1a + 64 n1b, n1a = q + 4 m;   k = k2 + 16 (k1b + 16 (c + 16 d)).
+//  P1 (thread n1 = t):  x[t + 1024 n2] w -> DFT16 over n2 -> * W_N^(t k2) -> image[k2 1024 + t]
+//  P2 (t = n1a + 64 k2): image[k2 1024 + n1a + 64 n1b] -> DFT16 over n1b -> * W_1024^(n1a k1b)
+//                       -> image[k2 S2 + k1b R2 + n1a]
+//  P3 (t = q + 4 k1b + 64 k2): image[k2 S2 + k1b R2 + q + 4 m] -> DFT16 over m
+//                       -> * W_64^(q c) -> DFT4 over q across the lane quad (DPP) -> |X|^2.
+// Every image access is one conflict-free 8-B LDS instruction per point.  The quad's DFT4 leaves
+// lane q with bin d = {0, 2, 3, 1}[q] up to a sign, which |X|^2 does not see (q16_bin(c 1024 + t)
+// is thread t's bin c).  At a group's end the sums are transposed to bin order through the LDS,
+// so partial rows are natural-order rows like every kernel's.  Frames, groups, the dynamic
+// dealing and the tail split are wf_fft_l32's.
+struct WfQ16 {
+    static constexpr int LOGN = 14, N = 1 << LOGN, NT = 1024;
+    // P2 -> P3 image: rows of 64 padded to R2 = 68 (k1b rows 4 banks apart: P3's reads, a quad
+    // per k1b row, are conflict-free with immediate offsets), k2 blocks of S2
+    // The tables come first: their reads then take immediate offsets from one base register
+    // (the DS offset field is 16 bits).
+    // P1's twiddle W_N^(n1 k2) = TA[k2][n1 & 63] * TB[k2][n1 >> 6] (W_N^(n1a k2) W_256^(n1b k2);
+    // in registers its bases spilled, and a scratch reload's vmcnt wait drains the prefetch)
+    static constexpr int R2 = 68, S2 = 16 * R2;
+    static constexpr int TW3 = 0;          // [16][4]:  W_64^(q c)
+    static constexpr int TW2 = 64;         // [16][64]: W_1024^(n1a k1b)
+    static constexpr int TA = 1088;        // [16][64]: W_N^(n1a k2)
+    static constexpr int TB = 2112;        // [16][16]: W_256^(n1b k2)
+    static constexpr int IMG = 2368;       // the image: 16 S2 entries
+    static constexpr size_t kLds = sizeof(float2) * (IMG + 16 * S2);
+};
+__host__ __device__ constexpr inline int q16_bin(int p) {
+    const int c = p >> 10, t = p & 1023;
+    const int q = t & 3, k1b = (t >> 2) & 15, k2 = t >> 6;
+    const int d = (0x78 >> (2 * q)) & 3;  // {0, 2, 3, 1}
+    return k2 + 16 * k1b + 256 * c + 4096 * d;
+}
+
+// LDS position of bin b in wf_fft_q16's group-end transpose: b with bits 0-4 XORed by bits
+// 4-6 and 12-13 (the lanes of one store differ in those), a bijection
+OWRX_DEV int wf_q16_lswz(int b) { return b ^ (((b >> 4) & 7) | (((b >> 12) & 3) << 3)); }
+
+template <int CTRL>
+OWRX_DEV float dppq(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// ABL: variant and diagnostic bits (tools/micro; the product picks one).  Ablations: 1 no frame
+// loads (the first frame's samples reused), 2 no LDS exchanges, 4 no barriers inside the frame.
+// Variants: 8 the next frame's loads spread over the four phases; 32 16-B loads (two adjacent
+// samples per lane, regrouped across the wave's halves with v_permlane32_swap, so lane L holds
+// n1 = 64 w + 2 (L & 31) + (L >> 5)); 64 the loads issued after the first exchange's LDS stores
+// (LDS stores queued behind a wave's just-issued loads waited ~11k cycles, tools/micro/wf_r05.hip
+// stamps); 128 the swap's operands reversed (semantics check).
+template <int ABL = 0>
+__global__ void __launch_bounds__(WfQ16::NT)
+wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
+           const float* __restrict__ window, const float2* __restrict__ tw,
+           float* __restrict__ partial, int items, int* __restrict__ work, int whole, int skip) {
+    using K = WfQ16;
+    WF_RSTAMP(14);
+    WF_STAMP(12);
+    constexpr int N = K::N, NT = K::NT;
+    constexpr bool kSpread = (ABL & 8) != 0, kW16 = (ABL & 32) != 0, kLate = (ABL & 64) != 0;
+    constexpr bool kSwapRev = (ABL & 128) != 0;
+    constexpr int kUnits = kW16 ? 8 : 16;  // load instructions per thread per frame
+    extern __shared__ __attribute__((aligned(16))) float2 sm[];
+    __shared__ int s_next;
+    const int t0 = threadIdx.x;
+    // P1's point n1 of this thread, and its place in the first image (a swizzle keeps the 16-B
+    // variant's stores conflict-free: its 16-lane store groups hold even or odd n1 only)
+    const int n1 = kW16 ? (t0 & ~63) + 2 * (t0 & 31) + ((t0 >> 5) & 1) : t0;
+    auto swz1 = [](int e) { return kW16 ? e ^ ((e >> 4) & 1) : e; };
+    struct Item {
+        __amdgpu_buffer_rsrc_t xr;
+        int hop, nfr;
+    };
+    auto desc = [&](int i) { return i < whole ? i : i + skip; };
+    auto item = [&](int w) {
+        const WfGroup g = groups[w];
+        Item it;
+        it.hop = __builtin_amdgcn_readfirstlane(g.hop);
+        it.nfr = __builtin_amdgcn_readfirstlane(g.nframes);
+        const int g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
+        it.xr = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float2*>(blk + g0), 0,
+            (int)(sizeof(float2) * ((int64_t)(it.nfr - 1) * it.hop + N)), 0x00020000);
+        return it;
+    };
+    // raw[2 r], raw[2 r + 1]: point r (n = n1 + 1024 r) once regrouped
+    auto load_units = [&](__amdgpu_buffer_rsrc_t xr, int fo, float* raw, int lo, int hi) {
+#pragma unroll
+        for (int u = lo; u < hi; ++u) {
+            if constexpr (kW16) {
+                // 16 B at n = 64 w + 2 (L & 31) + 1024 (2 u + (L >> 5))
+                const int vo = ((t0 & ~63) + 2 * (t0 & 31) + 1024 * ((t0 >> 5) & 1)) * 8 + fo;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    raw[4 * u + c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4 * c, u * 2048 * 8, 0));
+            } else {
+                const int vo = t0 * 8 + fo;
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    raw[2 * u + c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4 * c, u * NT * 8, 0));
+            }
+        }
+    };
+    // L2-resident constants first (vmcnt retires in order)
+    float wv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wv[r] = window[n1 + NT * r];
+    const float2 t2v = tw[((t0 & 63) * (t0 >> 6) * 16) & (N - 1)];          // [k1b][n1a]
+    const float2 t3v = tw[((t0 & 3) * ((t0 >> 2) & 15) * 256) & (N - 1)];   // [c][q], t0 < 64
+    const float2 tav = tw[((t0 & 63) * (t0 >> 6)) & (N - 1)];               // [k2][n1a]
+    const float2 tbv = tw[((t0 & 15) * ((t0 >> 4) & 15) * 64) & (N - 1)];   // [k2][n1b], t0 < 256
+    auto finish = [&]() {
+        __syncthreads();
+        if (t0 == 0 && atomicAdd(work + 1, 1) == (int)gridDim.x - 1) {
+            atomicExch(work, 0);
+            atomicExch(work + 1, 0);
+        }
+    };
+    if (t0 == 0) s_next = atomicAdd(work, 1);
+    __syncthreads();
+    int w = __builtin_amdgcn_readfirstlane(s_next);
+    if (w >= items) {
+        finish();
+        return;
+    }
+    w = desc(w);
+    Item cur = item(w);
+    float nx[32];
+#ifdef OWRX_WF_WSTAMPS
+    unsigned long long wst_[8] = {};
+#endif
+    load_units(cur.xr, 0, nx, 0, kUnits);
+    sm[K::TW2 + t0] = t2v;
+    sm[K::TA + t0] = tav;
+    if (t0 < 256) sm[K::TB + t0] = tbv;
+    if (t0 < 64) sm[K::TW3 + t0] = t3v;
+    float2* const img = sm + K::IMG;
+#pragma unroll 1
+    while (true) {
+        __syncthreads();
+        if (t0 == 0) s_next = atomicAdd(work, 1);
+        __syncthreads();
+        const int wi = __builtin_amdgcn_readfirstlane(s_next);
+        const bool has_next = wi < items;
+        const int wn = has_next ? desc(wi) : w;
+        const Item nxt = item(wn);
+        float acc[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc[m] = 0.0f;
+#pragma unroll 1
+        for (int f = 0; f < cur.nfr; ++f) {
+            int t = threadIdx.x;
+            asm volatile("" : "+v"(t));
+            float2 a[16];
+            if (f == 1) WF_STAMP(0);
+#define WF_WS(i)                     \
+    do {                             \
+        if (f == 2) WF_WSTAMP(i);    \
+    } while (0)
+            WF_WS(0);
+#ifdef OWRX_WF_WSTAMPS
+            if (f == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            WF_WS(1);
+            if constexpr (kW16) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        // X = raw[4u + c] (lanes < 32: n1 even, j = 2u; lanes >= 32: n1 even,
+                        // j = 2u + 1), Y = raw[4u + 2 + c]: swap X's upper half with Y's lower
+                        const unsigned xo = __builtin_bit_cast(unsigned, nx[4 * u + c]);
+                        const unsigned yo = __builtin_bit_cast(unsigned, nx[4 * u + 2 + c]);
+                        if constexpr (!kSwapRev) {
+                            const auto r = __builtin_amdgcn_permlane32_swap(xo, yo, false, false);
+                            nx[4 * u + c] = __builtin_bit_cast(float, (unsigned)r[0]);
+                            nx[4 * u + 2 + c] = __builtin_bit_cast(float, (unsigned)r[1]);
+                        } else {
+                            const auto r = __builtin_amdgcn_permlane32_swap(yo, xo, false, false);
+                            nx[4 * u + 2 + c] = __builtin_bit_cast(float, (unsigned)r[0]);
+                            nx[4 * u + c] = __builtin_bit_cast(float, (unsigned)r[1]);
+                        }
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] = make_float2(nx[2 * r] * wv[r], nx[2 * r + 1] * wv[r]);
+            const bool last = f + 1 == cur.nfr;
+            const auto lxr = last ? nxt.xr : cur.xr;
+            const int lfo = !last ? (f + 1) * cur.hop * 8 : has_next ? 0 : kWfOob;
+            constexpr int kQ = kUnits / 4;  // units per spread phase
+            if (!(ABL & 1) && !kLate) load_units(lxr, lfo, nx, 0, kSpread ? kQ : kUnits);
+            WF_WS(2);
+            if (f == 1) WF_STAMP(1);
+            // P1
+            f2dft<16>(a);
+            {
+                int tn = threadIdx.x;
+                asm volatile("" : "+v"(tn));
+                const int m1 = kW16 ? (tn & ~63) + 2 * (tn & 31) + ((tn >> 5) & 1) : tn;
+                const float2* TA = sm + K::TA + (m1 & 63);
+                const float2* TB = sm + K::TB + (m1 >> 6);
+#pragma unroll
+                for (int r = 1; r < 16; ++r) a[r] = f2mul(a[r], f2mul(TA[64 * r], TB[16 * r]));
+            }
+            if (f == 1) WF_STAMP(2);
+            WF_WS(3);
+            if (!(ABL & 4)) __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
+            WF_WS(4);
+            if (!(ABL & 2)) {
+                const int p1 = swz1(n1);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) img[r * 1024 + p1] = a[r];
+            }
+            WF_WS(5);
+            if (!(ABL & 1) && kLate) load_units(lxr, lfo, nx, 0, kSpread ? kQ : kUnits);
+            if (!(ABL & 4)) __syncthreads();
+            if (f == 1) WF_STAMP(3);
+            WF_WS(6);
+            if (kSpread && !(ABL & 1)) load_units(lxr, lfo, nx, kQ, 2 * kQ);
+            // P2
+            {
+                const int n1a = t & 63, k2 = t >> 6;
+                if (!(ABL & 2)) {
+                    const int p = k2 * 1024 + swz1(n1a);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) a[r] = img[p + 64 * r];
+                }
+                f2dft<16>(a);
+#pragma unroll
+                for (int r = 1; r < 16; ++r) a[r] = f2mul(a[r], sm[K::TW2 + r * 64 + n1a]);
+                if (f == 1) WF_STAMP(4);
+                if (kSpread && !(ABL & 1)) load_units(lxr, lfo, nx, 2 * kQ, 3 * kQ);
+                if (!(ABL & 4)) __syncthreads();  // every P2 read before any P2 store
+                if (!(ABL & 2)) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) img[k2 * K::S2 + r * K::R2 + n1a] = a[r];
+                }
+            }
+            if (!(ABL & 4)) __syncthreads();
+            if (f == 1) WF_STAMP(5);
+            WF_WS(7);
+            if (kSpread && !(ABL & 1)) load_units(lxr, lfo, nx, 3 * kQ, 4 * kQ);
+            // P3
+            {
+                const int q = t & 3;
+                const int k1b = (t >> 2) & 15, k2 = t >> 6;
+                const int base = k2 * K::S2 + k1b * K::R2 + q;
+                if (!(ABL & 2)) {
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) a[m] = img[base + 4 * m];
+                }
+                f2dft<16>(a);
+#pragma unroll
+                for (int c = 1; c < 16; ++c) a[c] = f2mul(a[c], sm[K::TW3 + c * 4 + q]);
+                const float s1 = q < 2 ? 1.0f : -1.0f;
+                const float s2 = (q == 0 || q == 3) ? 1.0f : -1.0f;
+#pragma unroll
+                for (int c = 0; c < 16; ++c) {
+                    float2 v = a[c];
+                    // stage 1: partner q ^ 2
+                    v.x = fmaf(dppq<0x4E>(v.x), s1, v.x);
+                    v.y = fmaf(dppq<0x4E>(v.y), s1, v.y);
+                    // lane 3: * -i
+                    const float vx = q == 3 ? v.y : v.x;
+                    const float vy = q == 3 ? -v.x : v.y;
+                    // stage 2: partner q ^ 1
+                    v.x = fmaf(dppq<0xB1>(vx), s2, vx);
+                    v.y = fmaf(dppq<0xB1>(vy), s2, vy);
+                    acc[c] = acc[c] + fmaf(v.y, v.y, v.x * v.x);
+                }
+            }
+            if (f == 1) WF_STAMP(6);
+#undef WF_WS
+        }
+        // group end: the |X|^2 sums go back to bin order through the (now free) image, so the
+        // partial row is stored coalesced and in natural order (wf_finalize and the tail split
+        // as for every kernel); the swizzle keeps both LDS passes conflict-free
+        __syncthreads();  // every P3 read of the image done
+        {
+            // (an opaque thread index: hoisted out of the frame loop, these addresses spilled)
+            int tt = threadIdx.x;
+            asm volatile("" : "+v"(tt));
+            float* const limg = reinterpret_cast<float*>(img);
+            const int k1b = (tt >> 2) & 15, k2 = tt >> 6;
+            const int d = (0x78 >> (2 * (tt & 3))) & 3;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) limg[wf_q16_lswz(k2 + 16 * k1b + 256 * c + 4096 * d)] = acc[c];
+            __syncthreads();
+            float* out = partial + (int64_t)w * N;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) out[tt + NT * j] = limg[wf_q16_lswz(tt + NT * j)];
+        }
+        if (!has_next) break;
+        w = wn;
+        cur = nxt;
+    }
+    WF_STAMP(13);
+    WF_RSTAMP(15);
+#ifdef OWRX_WF_WSTAMPS
+    if ((t0 & 63) == 0 && blockIdx.x < 256)
+        for (int i = 0; i < 8; ++i) g_wf_wstamp[blockIdx.x][t0 >> 6][i] = wst_[i];
+#endif
+    finish();
+}
+
+// the product's variant: the next frame's loads after the first exchange's stores, spread
+// over the phases (tools/micro/wf_r05.hip: 0.29 vs 0.25 of HBM for wf_fft_l32 at 3840 C3 frames)
+constexpr int kWfQ16 = 72;
+
 // ---- FFT sizes above one CU's LDS (32768, 65536): decimation-in-frequency split ------------
 // N = Q * 16384 (Q = 2, 4): X[Q k + j] = sum_n y_j[n] W_16384^(n k) with
 //   y_j[n] = W_N^(n j) * sum_q w[n + 16384 q] x[n + 16384 q] W_Q^(q j),   n < 16384,
@@ -1134,20 +1463,25 @@ static hipError_t launch_fft4_t(const float2* blk, int64_t blk_start, const WfGr
     return hipGetLastError();
 }
 
-// N = 16384: the whole-frame radix-32 kernel wf_fft_l32, OWRX_WF_KERNEL=r16 the radix-16 one
+// N = 16384: wf_fft_q16 (OWRX_WF_KERNEL=l32: the round-4 radix-32 kernel, =r16 the radix-16 one)
 // (A/B); 1024 <= N <= 8192: radix 16.  (A half-frame kernel with two workgroups per CU,
 // wf_fft_h2, measured 68 vs 50 us per 960 C3 frames, its loads exposed: removed, in the history
 // before this file's round-4 cleanup.)
-static int wf_n16k_kernel() {  // 1: l32, 2: r16
+static int wf_n16k_kernel() {  // 0: q16 (default), 1: l32, 2: r16
     static const int v = [] {
         const char* s = getenv("OWRX_WF_KERNEL");
-        return s && strcmp(s, "r16") == 0 ? 2 : 1;
+        return s && strcmp(s, "r16") == 0 ? 2 : s && strcmp(s, "l32") == 0 ? 1 : 0;
     }();
     return v;
 }
 static bool wf_force_r16() { return wf_n16k_kernel() == 2; }
 
+// N = 16384 on a dealt whole-frame kernel (q16 or l32: groups, tail split)
 bool wf_uses_l32(int logn) { return logn == 14 && wf_n16k_kernel() != 2; }
+// frames per group of the N = 16384 dealt kernels: 8 for q16 (its group-end transpose and partial
+// row amortise over twice the frames; 0.291 vs 0.275 of HBM at 3840 C3 frames in the micro), 4
+// for l32
+int wf_default_fpg(int logn) { return logn == 14 && wf_n16k_kernel() == 0 ? 8 : 4; }
 
 // N = 32768, 65536: the DIF split onto wf_fft_l32 (OWRX_WF_KERNEL=fourstep: the four-step, A/B)
 bool wf_uses_split(int logn) {
@@ -1188,7 +1522,7 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
 // (89 vs 52 us per 960 C3 frames); the groups that would start a partial last round, plus a
 // 16th of a round, are dealt as single frames instead.  0 for the other kernels.
 int wf_tail_split(int logn, int ngroups, int cus) {
-    if (logn != 14 || wf_n16k_kernel() != 1 || cus < 8 || ngroups < 2) return 0;
+    if (logn != 14 || wf_n16k_kernel() == 2 || cus < 8 || ngroups < 2) return 0;
     static const int mode = [] {
         const char* s = getenv("OWRX_WF_TAIL");
         return s ? atoi(s) : -1;
@@ -1217,11 +1551,36 @@ static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const W
 }
 
 
+static hipError_t launch_fft_q16(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                 int ngroups, const float* window, const float2* tw,
+                                 float* partial, int* work, int cus, hipStream_t st, int skip,
+                                 int tail) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_q16<kWfQ16>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)WfQ16::kLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    if (!work || skip < 0 || skip > ngroups || tail < 0) return hipErrorInvalidValue;
+    const int whole = ngroups - skip;
+    const int items = whole + tail;
+    // one 1024-thread workgroup per CU (the 147 KiB LDS image), at most one per item
+    const int grid = std::max(1, std::min(items, cus));
+    hipLaunchKernelGGL(wf_fft_q16<kWfQ16>, dim3(grid), dim3(WfQ16::NT), WfQ16::kLds, st, blk,
+                       blk_start, groups, window, tw, partial, items, work, whole, skip);
+    return hipGetLastError();
+}
+
 template <int LOGN>
 static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw, float* partial,
                                  int* work, int cus, hipStream_t st, int skip, int tail) {
     if constexpr (LOGN == 14) {
+        if (wf_n16k_kernel() == 0)
+            return launch_fft_q16(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
+                                  skip, tail);
         if (!wf_force_r16())
             return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
                                   0, 0, skip, tail);

@@ -285,8 +285,8 @@ def test_waterfall_batched_launches(amd):
 
 
 def test_waterfall_tail_split_rows_bit_identical(amd):
-    """wf_fft_l32's tail split (a launch's last groups dealt frame by frame, their frames folded
-    in order by wf_finalize): C3's waterfall (16384 bins, avg 97, hop 11454) over 1 100 frames,
+    """The tail split of the dealt N = 16384 kernels (wf_fft_q16, wf_fft_l32: a launch's last
+    groups dealt frame by frame, their frames folded in order by wf_finalize): C3's waterfall (16384 bins, avg 97, hop 11454) over 1 100 frames,
     once batched into launches of ~1 000 frames (over 7/8 of a launch's groups per CU, so the
     split is on) and once per 2^20-sample block (~91 frames per launch: no split).  The rows
     are bit-identical, and equal the oracle's to 2e-3 dB on the first rows."""
@@ -432,12 +432,13 @@ def test_engine_ring_ingest_commit(amd):
     assert a.shape[0] == 3 and np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("variant,sizes", [("r16", 5), ("fourstep", 2)])
+@pytest.mark.parametrize("variant,sizes", [("r16", 5), ("l32", 5), ("fourstep", 2)])
 def test_waterfall_kernel_variants(variant, sizes):
     """The A/B waterfall kernels (OWRX_WF_KERNEL=r16: the radix-16 kernel at N = 16384 instead of
-    wf_fft_l32; =fourstep: the four-step FFT at N = 32768 / 65536 instead of the DIF split onto
-    wf_fft_l32) give the oracle's rows (<= 2e-3 dB, as the production kernels); each runs in a
-    child process since the selection is read once per process."""
+    wf_fft_q16; =l32: round 4's 512-thread radix-32 kernel; =fourstep: the four-step FFT at
+    N = 32768 / 65536 instead of the DIF split onto wf_fft_l32) give the oracle's rows (<= 2e-3
+    dB, as the production kernels); each runs in a child process since the selection is read
+    once per process."""
     import json
     import os
     import subprocess
