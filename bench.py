@@ -752,7 +752,7 @@ def main():
     # waterfall batching (rank 0 of a one-GPU run): the engine keeps enough history for the
     # batch's frames, and the FFT runs once per batch instead of once per block
     wf_batch = 0
-    if world == 1 and not args.no_waterfall:
+    if rank == 0 and not args.no_waterfall:  # the waterfall runs on rank 0 at every N
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # sixteen frames per stream-A CU for the 16384-point kernel (two groups of 8 per
         # workgroup: its start-up and first frame amortise over the frames, 0.294 vs 0.259 of
@@ -764,10 +764,12 @@ def main():
     history = (wf_batch + 16) * hop + 2 * n_fft + block if wf_batch > 1 else 0
     eng = Engine(fs, max_block=block, device=local, history=history)
     eng.set_ddc_mode(args.ddc)
-    if world == 1:
-        # the stream is a resident recording: every block stays valid, so the host may run
-        # ahead of stream A (owrx_set_input_retention); the N>1 windows alternate two buffers
-        eng.set_input_retention(int(os.environ.get("OWRX_BENCH_RETENTION", "8")))
+    # the stream is a resident recording on rank 0 and a ring of broadcast windows on the other
+    # ranks (IqBroadcast sizes its ring to the retention): every block stays valid for
+    # `retention` further blocks, so the host may run that far ahead of stream A
+    # (owrx_set_input_retention), at every N
+    retention = int(os.environ.get("OWRX_BENCH_RETENTION", "8"))
+    eng.set_input_retention(retention)
     # 16 blocks in flight for the headline engine (256 chains: a few MB of staging per block);
     # the capacity ladder's engines keep the default 8 (their staging grows with the chains)
     eng.set_pipeline_depth(int(os.environ.get("OWRX_BENCH_DEPTH", "16")))
@@ -794,7 +796,16 @@ def main():
     if rank == 0:
         stream = gen_stream_torch(torch, dev, fs, hist + span, modes, offs)
         base = stream.data_ptr() + 8 * hist
-    bcast = IqBroadcast(torch, dist, dev, hist, block, stream=stream) if dist else None
+    bcast = None
+    if dist:
+        # the broadcast windows carry the chains' history (the engine default on ranks > 0, the
+        # same on every rank: the collectives must match); rank 0 keeps its own, longer
+        # waterfall-batch history in front of the recording, so its view starts that much later
+        t = torch.tensor([float(hist if rank else 0)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        hist_b = int(t.item())
+        src_view = stream[hist - hist_b:] if rank == 0 else None
+        bcast = IqBroadcast(torch, dist, dev, hist_b, block, stream=src_view, retention=retention)
     torch.cuda.synchronize(dev)
 
     def drain():
@@ -831,11 +842,11 @@ def main():
                 if j + 1 < nsteps * bps:
                     bcast.issue(j + 1)
                 t, off = bcast.wait(j)
-                # wait for this broadcast only (an event behind it on torch's stream), not for
-                # the device: the engine's own streams keep earlier blocks in flight meanwhile
-                arrived = torch.cuda.Event()
-                arrived.record()
-                arrived.synchronize()
+                # stream A waits on the GPU for this broadcast (owrx_wait_stream on torch's
+                # stream, which the collective's wait() ordered behind it): no host wait, the
+                # engine's streams keep earlier blocks in flight
+                if rank != 0:
+                    eng.wait_stream(torch.cuda.current_stream(dev).cuda_stream)
                 eng.process_device(t.data_ptr() + 8 * off, block)
         return drain()
 

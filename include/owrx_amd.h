@@ -97,6 +97,11 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq_cs16, int64_t nsamples, 
  * the block (with its history) must stay unmodified until the next owrx_process_device /
  * owrx_commit / owrx_push_iq / owrx_sync call on this engine has returned. */
 int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t nsamples);
+/* The engine's work from the next block on waits, on the GPU, for everything enqueued so far on
+ * `stream` (a hipStream_t of the same device; NULL: the null stream), e.g. the collective that
+ * writes the next owrx_process_device window (multi-GPU IQ broadcast).  The host
+ * does not wait. */
+int owrx_wait_stream(owrx_engine* e, void* stream);
 /* Callers whose input blocks stay valid longer (a resident recording, a ring of windows): with
  * blocks = r the block handed to owrx_process_device (with its history) must stay unmodified
  * until r further owrx_process_device / owrx_commit calls (or owrx_sync) have returned, and the
@@ -117,8 +122,9 @@ int owrx_set_pipeline_depth(owrx_engine* e, int blocks);
  * waits one more bound for the streams and then leaks the engine's buffers rather than free them
  * under a running kernel. */
 int owrx_set_stall_timeout(owrx_engine* e, int64_t ms);
-/* Test hook: enqueues a kernel that occupies stream 0 (A: FFT / DDC), 1 (B) or 2 (C) for `us`
- * microseconds and then exits (stall injection for the bounded-wait path). */
+/* Test hook: enqueues a kernel that occupies stream 0 (A: FFT / DDC), 1 (B), 2 (C), 3 (R: the
+ * output gathers) or 4 (the next waterfall row slot's stream) for `us` microseconds and then
+ * exits (stall injection for the bounded-wait path; held copies for the reconfiguration tests). */
 int owrx_debug_stall(owrx_engine* e, int stream, int64_t us);
 /* Host self-test (no GPU needed): the fast-convolution DDC's tiled filter-spectrum layout maps
  * every (member slot < cap, branch < Dp) inside its bin's row of cap * Dp entries, one entry per
@@ -203,6 +209,11 @@ typedef struct {
                                 (RawAm, RawSAm: 100, analog.py:29, :165); 0 => Agc */
 } owrx_chain_params;
 
+/* Chains with the same FirDecimate design share one fast-convolution group; every output is
+ * deterministic for a given membership, but the GEMM's K split across workgroups follows the
+ * group's size (kernels_fcddc.hip fc_kslices), so a chain's DDC output can change at the float
+ * rounding level (<= 1e-6 rel-RMS, tests/test_gpu_parity.py
+ * test_ddc_group_size_changes_rounding_only) when other clients of its design join or leave. */
 int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle);
 int owrx_chain_destroy(owrx_engine* e, int handle);
 int owrx_chain_set_shift_rate(owrx_engine* e, int handle, float rate);
@@ -220,7 +231,8 @@ int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t m
 /* Batched forms for a server pump that serves many clients from one thread (the reference runs
  * one pump thread per output, owrx/dsp.py:846-863): chain handles[i]'s available bytes / values
  * are appended to dst in order until max_bytes / max_values; lens[i] / counts[i] receive each
- * chain's share.  Returns the total. */
+ * chain's share.  Returns the total.  Every handle may appear once: a repeated or unknown
+ * handle returns OWRX_EINVAL and reads nothing. */
 int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
                                int64_t max_bytes, int64_t* lens);
 int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float* dst,

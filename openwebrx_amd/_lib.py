@@ -139,6 +139,7 @@ PROTOTYPES = {
     "owrx_push_iq": (_i32, [_vp, _vp, _i64]),
     "owrx_push_iq_cs16": (_i32, [_vp, _vp, _i64, _f32]),
     "owrx_process_device": (_i32, [_vp, _vp, _i64]),
+    "owrx_wait_stream": (_i32, [_vp, _vp]),
     "owrx_ingest_buffer": (_i32, [_vp, ctypes.POINTER(_vp), _pi64]),
     "owrx_commit": (_i32, [_vp, _i64]),
     "owrx_sync": (_i32, [_vp]),

@@ -380,6 +380,7 @@ static int64_t out_region(int64_t cap) { return (cap + 255) & ~(int64_t)255; }
 
 struct Chain {
     owrx_chain_params prm;
+    uint64_t read_mark = 0;  // batched reads: the call that listed it last (duplicate check)
     ChainGroup* group = nullptr;
     int64_t origin = 0;   // absolute sample index of chain sample 0
     int64_t k_first = 0;  // absolute output index of chain output 0
@@ -572,6 +573,23 @@ copy_jobs(const CopyJob* __restrict__ jobs) {
     }
 }
 
+// Zeroing of newly taken pool buffers, all of them in one launch: job y (read from the pinned
+// upload ring) zeroes its bytes, 16 B per lane (pool sizes are multiples of 256 B).  One
+// hipMemsetAsync per buffer was 21 972 fillBufferAligned dispatches in a C3 bench profile, a
+// quarter of its GPU time, and 13-20 s of setup for 98 304-131 072 chains.
+struct ZeroJob {
+    void* dst;
+    int64_t bytes;
+};
+__global__ void __launch_bounds__(256)
+zero_jobs(const ZeroJob* __restrict__ jobs) {
+    const ZeroJob j = jobs[blockIdx.y];
+    const int64_t n16 = j.bytes >> 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (int64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<uint4*>(j.dst)[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 static hipError_t kcopy(void* dst, const void* src, size_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
     const bool v16 = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
@@ -665,12 +683,14 @@ struct owrx_engine {
     double block_interval_ms = 0;    // running estimate of the interval between block calls
     int64_t stall_ms = 20000;        // the longest any host-side wait blocks before failing
     hipEvent_t evSync = nullptr;     // marker for bounded stream synchronisation
+    hipEvent_t evExt = nullptr;      // owrx_wait_stream: the caller's stream position
     std::unique_ptr<HostPool> pool;  // host workers for per-chain loops (created on first use)
     bool debug = false;
     int timing = 0;                  // timing events every `timing` blocks (0: off)
     std::vector<GroupWork> work;     // per-block scratch: the groups with outputs
     std::vector<Chain*> nr_resets;   // NoiseFilter states to zero before the next serial work
     uint64_t chain_epoch = 0;        // bumped by every change of a chain's post descriptor
+    uint64_t read_epoch = 0;         // bumped by every batched read (Chain::read_mark)
     int ddc_mode = OWRX_DDC_FAST;
     std::recursive_mutex mu;
     // push-path ring: blocks are appended at wp with `history` samples before them; when the
@@ -734,6 +754,7 @@ struct owrx_engine {
     std::vector<RowRetired> row_retired;
     uint8_t* h_up = nullptr;  // pinned staging of those uploads (a ring; wraps after stream A)
     size_t up_cap = 0, up_head = 0;
+    std::vector<ZeroJob> zero_pending;  // pool buffers taken but not yet zeroed (flush_zero)
     // post staging needs of the current chains (kept as chains come and go)
     int64_t need_out = 256, need_sm = 4, need_dbg = 64;
 };
@@ -826,7 +847,8 @@ static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
         e->stats.pool_allocs++;
     }
     *p = static_cast<T*>(q);
-    return hipMemsetAsync(q, 0, bytes, e->sA);
+    e->zero_pending.push_back({q, (int64_t)bytes});  // zeroed on stream A by flush_zero
+    return hipSuccess;
 }
 
 // release to the pool once the blocks enqueued so far have drained
@@ -932,8 +954,8 @@ static void row_collect(owrx_engine* e) {
 
 // n bytes from the host to device memory on stream A, through the pinned upload ring: the
 // caller's buffer is free on return, and the copy runs before any later stream-A work
-static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
-    if (n == 0) return OWRX_OK;
+// n bytes of the pinned upload ring for a stream-A consumer enqueued right after
+static int ring_take(owrx_engine* e, size_t n, uint8_t** h) {
     const size_t a = (n + 255) & ~(size_t)255;
     if (a > e->up_cap) {
         if (e->h_up) RCCHK(sync_stream(e, e->sA));
@@ -946,9 +968,38 @@ static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
         RCCHK(sync_stream(e, e->sA));
         e->up_head = 0;
     }
-    memcpy(e->h_up + e->up_head, src, n);
-    HIPCHK(kcopy(dst, e->h_up + e->up_head, n, e->sA));
+    *h = e->h_up + e->up_head;
     e->up_head += a;
+    return OWRX_OK;
+}
+
+// Zero every pool buffer taken since the last flush, in one launch on stream A.  Called before
+// any stream-A work that may touch them: uploads (initial states), the filter-spectra builds and
+// moves, and each block.
+static int flush_zero(owrx_engine* e) {
+    while (!e->zero_pending.empty()) {
+        const size_t nj = std::min<size_t>(e->zero_pending.size(), 65535);
+        uint8_t* h = nullptr;
+        RCCHK(ring_take(e, sizeof(ZeroJob) * nj, &h));
+        memcpy(h, e->zero_pending.data(), sizeof(ZeroJob) * nj);
+        int64_t most = 0;
+        for (size_t i = 0; i < nj; ++i) most = std::max(most, e->zero_pending[i].bytes);
+        const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(64, (most / 16 + 255) / 256));
+        hipLaunchKernelGGL(zero_jobs, dim3(gx, (unsigned)nj), dim3(256), 0, e->sA,
+                           reinterpret_cast<const ZeroJob*>(h));
+        HIPCHK(hipGetLastError());
+        e->zero_pending.erase(e->zero_pending.begin(), e->zero_pending.begin() + nj);
+    }
+    return OWRX_OK;
+}
+
+static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
+    if (n == 0) return OWRX_OK;
+    RCCHK(flush_zero(e));
+    uint8_t* h = nullptr;
+    RCCHK(ring_take(e, n, &h));
+    memcpy(h, src, n);
+    HIPCHK(kcopy(dst, h, n, e->sA));
     return OWRX_OK;
 }
 
@@ -1388,6 +1439,7 @@ static int fc_choose_m(int D, int P, int64_t nk_max) {
 static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
     ChainGroup* g = c->group;
     if (!g->fc_M) return OWRX_OK;
+    RCCHK(flush_zero(e));
     HIPCHK(launch_fc_make_w(g->fc_M, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P, c->rate_fx,
                             g->d_fc_w + fc_w_chain_offset(slot, g->fc_Dp), g->fc_w_ks(), e->sA));
     return OWRX_OK;
@@ -1404,6 +1456,7 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
     float2* nw = nullptr;
     // on stream A behind the blocks that read the old spectra (those release it when drained)
     HIPCHK(palloc(e, &nw, (size_t)M * cap * g->fc_Dp));
+    RCCHK(flush_zero(e));  // zeroed before the rows are copied in
     if (g->d_fc_w && g->fc_w_cap > 0) {
         const size_t row = sizeof(float2) * (size_t)g->fc_w_cap * g->fc_Dp;
         HIPCHK(hipMemcpy2DAsync(nw, sizeof(float2) * (size_t)cap * g->fc_Dp, g->d_fc_w, row, row,
@@ -1871,6 +1924,7 @@ static int wait_input_block(owrx_engine* e, int64_t j) {
 
 static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     const double t_enter = now_ms();
+    RCCHK(flush_zero(e));  // pool buffers of chains / waterfalls created since the last block
     // Block k's pinned descriptors are staged per slot (reused by block k + kSlots, after the
     // slot drained and block k's stream-A work is known done).  The caller's input: blocks
     // k - retention + 1 .. k may still be read on stream A when this call returns, block
@@ -2333,7 +2387,9 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
         return OWRX_EIO;
     };
     if (create_streams(e) != hipSuccess) return fail("stream");
-    if (hipEventCreateWithFlags(&e->evSync, hipEventDisableTiming) != hipSuccess) return fail("event");
+    if (hipEventCreateWithFlags(&e->evSync, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->evExt, hipEventDisableTiming) != hipSuccess)
+        return fail("event");
     for (auto& r : e->rslots) {
         if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
@@ -2387,13 +2443,15 @@ int owrx_engine_destroy(owrx_engine* e) {
     // every stream drained, within the stall bound (a stalled engine gets one more bound to
     // finish; if its work still has not completed, its buffers are leaked rather than freed
     // under a running kernel, and the process keeps going)
+    // The first stream still stuck after its bound ends the wait: the engine is leaked anyway,
+    // and bounding every stream (or a shared row stream once per slot) in turn would block the
+    // OpenWebRX process for many stall bounds.
     if (e->stalled) e->failed = false;
-    bool stuck = false;
-    for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
-        if (st && e->evSync && sync_stream(e, st) == OWRX_ETIMEDOUT) stuck = true;
+    std::vector<hipStream_t> streams = {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw};
     for (auto& r : e->rslots)
-        if (r.stream && e->evSync && sync_stream(e, r.stream) == OWRX_ETIMEDOUT) stuck = true;
-    if (stuck) return OWRX_ETIMEDOUT;
+        if (std::find(streams.begin(), streams.end(), r.stream) == streams.end()) streams.push_back(r.stream);
+    for (hipStream_t st : streams)
+        if (st && e->evSync && sync_stream(e, st) == OWRX_ETIMEDOUT) return OWRX_ETIMEDOUT;
     for (auto& kv : e->chains) free_chain(e, kv.second.get());
     for (auto& kv : e->wfs) free_wf(e, kv.second.get());
     for (auto& g : e->groups) {
@@ -2430,6 +2488,7 @@ int owrx_engine_destroy(owrx_engine* e) {
     for (hipStream_t st : {e->sA, e->sB, e->sC, e->sR, e->sBw, e->sCw})
         if (st) hipStreamDestroy(st);
     if (e->evSync) hipEventDestroy(e->evSync);
+    if (e->evExt) hipEventDestroy(e->evExt);
     delete e;
     return OWRX_OK;
 }
@@ -2479,12 +2538,23 @@ int owrx_set_stall_timeout(owrx_engine* e, int64_t ms) {
 
 int owrx_debug_stall(owrx_engine* e, int stream, int64_t us) {
     ENGINE_GUARD(e);
-    hipStream_t st = stream == 0 ? e->sA : stream == 1 ? e->sB : stream == 2 ? e->sC : nullptr;
+    hipStream_t st = stream == 0 ? e->sA : stream == 1 ? e->sB : stream == 2 ? e->sC
+                   : stream == 3 ? e->sR : stream == 4 ? e->rslots[e->row_head % kRowSlots].stream
+                   : nullptr;
     if (!st || us < 0 || us > 60000000) {
-        set_last_error("owrx_debug_stall: stream 0..2, 0 <= us <= 60 s");
+        set_last_error("owrx_debug_stall: stream 0..4, 0 <= us <= 60 s");
         return OWRX_EINVAL;
     }
     HIPCHK(launch_debug_sleep(us, st));
+    return OWRX_OK;
+}
+
+// Stream A waits, on the GPU, for the work enqueued so far on the caller's stream (a collective
+// that writes the next block's window: the broadcast of multi.IqBroadcast); no host wait.
+int owrx_wait_stream(owrx_engine* e, void* stream) {
+    ENGINE_GUARD(e);
+    HIPCHK(hipEventRecord(e->evExt, (hipStream_t)stream));
+    HIPCHK(hipStreamWaitEvent(e->sA, e->evExt, 0));
     return OWRX_OK;
 }
 
@@ -2999,8 +3069,10 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     // swap-remove: the last member takes the slot (and its filter spectra move with it)
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
     const int last = (int)g->members.size() - 1;
-    if (slot != last && g->fc_M)
+    if (slot != last && g->fc_M) {
+        RC_FAIL(e, flush_zero(e));
         HIPCHK(launch_fc_move_w(g->fc_M, g->d_fc_w, g->fc_w_ks(), g->fc_Dp, last, slot, e->sA));
+    }
     g->members[slot] = g->members[last];
     g->members.pop_back();
     g->chains_stale = true;
@@ -3072,6 +3144,20 @@ int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t m
            (int64_t)sizeof(float);
 }
 
+// A handle listed twice would have two host workers pop one ring at once: rejected (serial
+// O(n) pass over the chains the lookups found)
+static bool batched_duplicates(owrx_engine* e, const std::vector<Chain*>& cs) {
+    const uint64_t ep = ++e->read_epoch;
+    for (Chain* c : cs) {
+        if (c->read_mark == ep) {
+            set_last_error("owrx_chains_read_*: a chain handle is listed twice");
+            return true;
+        }
+        c->read_mark = ep;
+    }
+    return false;
+}
+
 int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
                                int64_t max_bytes, int64_t* lens) {
     ENGINE_GUARD(e);
@@ -3088,7 +3174,7 @@ int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_
             lens[i] = (int64_t)cs[i]->audio.avail();
         }
     });
-    if (bad) return OWRX_EINVAL;
+    if (bad || batched_duplicates(e, cs)) return OWRX_EINVAL;
     std::vector<int64_t> offs((size_t)n);
     int64_t off = 0;
     for (int i = 0; i < n; ++i) {
@@ -3116,7 +3202,7 @@ int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float
             counts[i] = (int64_t)(cs[i]->smeter.avail() / sizeof(float));
         }
     });
-    if (bad) return OWRX_EINVAL;
+    if (bad || batched_duplicates(e, cs)) return OWRX_EINVAL;
     std::vector<int64_t> offs((size_t)n);
     int64_t off = 0;
     for (int i = 0; i < n; ++i) {

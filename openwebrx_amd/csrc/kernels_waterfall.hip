@@ -325,7 +325,7 @@ __device__ unsigned long long g_wf_stamp[1024][16];
     } while (0)
 #ifdef OWRX_WF_WSTAMPS
 // per-wave stamps (wf_fft_q16, frame 2 of the first item): [workgroup][wave][slot]
-__device__ unsigned long long g_wf_wstamp[256][16][8];
+__device__ unsigned long long g_wf_wstamp[256][16][12];
 // (held in registers during the frame -- a global store per stamp queues behind the frame's
 // loads and would itself delay the wave -- and stored after the frame loop)
 #define WF_WSTAMP(i)                                                                          \
@@ -975,7 +975,7 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     Item cur = item(w);
     float nx[32];
 #ifdef OWRX_WF_WSTAMPS
-    unsigned long long wst_[8] = {};
+    unsigned long long wst_[12] = {};
 #endif
     load_units(cur.xr, 0, nx, 0, kUnits);
     sm[K::TW2 + t0] = t2v;
@@ -1005,6 +1005,20 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     do {                             \
         if (f == 2) WF_WSTAMP(i);    \
     } while (0)
+// (diagnostic builds: the values computed so far are forced before a stamp, or the compiler
+// sinks the arithmetic past it)
+#ifdef OWRX_WF_WSTAMPS
+#define WF_PIN(arr)                                                          \
+    do {                                                                     \
+        if (f == 2)                                                          \
+            for (int pr_ = 0; pr_ < 16; ++pr_)                               \
+                asm volatile("" : "+v"(arr[pr_].x), "+v"(arr[pr_].y));        \
+    } while (0)
+#else
+#define WF_PIN(arr) \
+    do {            \
+    } while (0)
+#endif
             WF_WS(0);
 #ifdef OWRX_WF_WSTAMPS
             if (f == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1051,6 +1065,7 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
                 for (int r = 1; r < 16; ++r) a[r] = f2mul(a[r], f2mul(TA[64 * r], TB[16 * r]));
             }
             if (f == 1) WF_STAMP(2);
+            WF_PIN(a);
             WF_WS(3);
             if (!(ABL & 4)) __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
             WF_WS(4);
@@ -1061,6 +1076,7 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
             }
             WF_WS(5);
             if (!(ABL & 1) && kLate) load_units(lxr, lfo, nx, 0, kSpread ? kQ : kUnits);
+            WF_WS(8);
             if (!(ABL & 4)) __syncthreads();
             if (f == 1) WF_STAMP(3);
             WF_WS(6);
@@ -1077,6 +1093,8 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 #pragma unroll
                 for (int r = 1; r < 16; ++r) a[r] = f2mul(a[r], sm[K::TW2 + r * 64 + n1a]);
                 if (f == 1) WF_STAMP(4);
+                WF_PIN(a);
+                WF_WS(9);
                 if (kSpread && !(ABL & 1)) load_units(lxr, lfo, nx, 2 * kQ, 3 * kQ);
                 if (!(ABL & 4)) __syncthreads();  // every P2 read before any P2 store
                 if (!(ABL & 2)) {
@@ -1118,6 +1136,11 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
                 }
             }
             if (f == 1) WF_STAMP(6);
+#ifdef OWRX_WF_WSTAMPS
+            if (f == 2)
+                for (int pr_ = 0; pr_ < 16; ++pr_) asm volatile("" : "+v"(acc[pr_]));
+#endif
+            WF_WS(10);
 #undef WF_WS
         }
         // group end: the |X|^2 sums go back to bin order through the (now free) image, so the
@@ -1146,7 +1169,7 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     WF_RSTAMP(15);
 #ifdef OWRX_WF_WSTAMPS
     if ((t0 & 63) == 0 && blockIdx.x < 256)
-        for (int i = 0; i < 8; ++i) g_wf_wstamp[blockIdx.x][t0 >> 6][i] = wst_[i];
+        for (int i = 0; i < 12; ++i) g_wf_wstamp[blockIdx.x][t0 >> 6][i] = wst_[i];
 #endif
     finish();
 }

@@ -102,13 +102,20 @@ class Engine:
     def sync(self):
         check(lib.owrx_sync(self._h), "owrx_sync")
 
+    def wait_stream(self, stream_handle):
+        """The engine's next blocks wait on the GPU for the work enqueued so far on the given
+        hipStream_t (e.g. torch.cuda.current_stream().cuda_stream after a broadcast)."""
+        check(lib.owrx_wait_stream(self._h, ctypes.c_void_p(int(stream_handle or 0))),
+              "owrx_wait_stream")
+
     def set_stall_timeout(self, ms):
         """Longest any call waits on the GPU before the engine fails with TimeoutError
         (owrx_set_stall_timeout; default 20 s)."""
         check(lib.owrx_set_stall_timeout(self._h, int(ms)), "owrx_set_stall_timeout")
 
     def debug_stall(self, stream, us):
-        """Test hook: occupy stream 0 (A), 1 (B) or 2 (C) for `us` microseconds."""
+        """Test hook: occupy stream 0 (A), 1 (B), 2 (C), 3 (R) or 4 (the next waterfall row
+        slot's stream) for `us` microseconds."""
         check(lib.owrx_debug_stall(self._h, int(stream), int(us)), "owrx_debug_stall")
 
     def set_input_retention(self, blocks):

@@ -60,29 +60,33 @@ class IqBroadcast:
 
     Pipelined use (issue / wait): issue(i + 1) is enqueued before block i is processed, so the
     broadcast of the next block overlaps this block's host and GPU work.  Ranks > 0 therefore
-    rotate three windows: issue(i + 1) rewrites block i - 2's window, which the engine has
-    finished once owrx_process_device(i - 1) returned (its contract: the caller may reuse the
-    block before the one just passed)."""
+    rotate retention + 2 windows (three at retention 1): issue(i + 1) rewrites block
+    i + 1 - nwin's window, which the engine has finished once owrx_process_device(i) returned
+    (owrx_set_input_retention's contract: blocks before k - retention + 1 are released)."""
 
     NWIN = 3
 
-    def __init__(self, torch, dist, device, history, block, src=0, stream=None):
+    def __init__(self, torch, dist, device, history, block, src=0, stream=None, retention=1):
         self.torch, self.dist = torch, dist
         self.history, self.block, self.src = history, block, src
         self.rank = dist.get_rank()
         self.stream = stream  # rank src: complex64 tensor [history | blocks...]
         self.pending = {}     # block -> async broadcast handle
         self.next_issue = 0   # broadcasts are enqueued in block order on every rank
+        # an engine with input retention r still reads blocks k - r + 1 .. k after
+        # owrx_process_device(k) returned, and block k + 1's broadcast is issued before block k is
+        # processed: r + 2 windows (3 for r = 1)
+        self.nwin = max(self.NWIN, int(retention) + 2)
         if self.rank != src:
             self.windows = [torch.zeros(history + block, dtype=torch.complex64, device=device)
-                            for _ in range(self.NWIN)]
+                            for _ in range(self.nwin)]
 
     def _view(self, i):
         h, b = self.history, self.block
         lo = 0 if i == 0 else h  # the first broadcast also carries the initial history
         if self.rank == self.src:
             return self.stream[lo + i * b if i else 0: h + (i + 1) * b], self.stream, h + i * b
-        w = self.windows[i % self.NWIN]
+        w = self.windows[i % self.nwin]
         return w[lo:h + b], w, h
 
     def issue(self, i):
@@ -100,7 +104,7 @@ class IqBroadcast:
             prev = self.pending.get(i - 1)
             if prev is not None:
                 prev.wait()
-            w, pw = self.windows[i % self.NWIN], self.windows[(i - 1) % self.NWIN]
+            w, pw = self.windows[i % self.nwin], self.windows[(i - 1) % self.nwin]
             w[:h].copy_(pw[b:b + h])
         part, _, _ = self._view(i)
         self.pending[i] = self.dist.broadcast(self.torch.view_as_real(part), src=self.src,

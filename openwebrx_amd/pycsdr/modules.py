@@ -46,17 +46,22 @@ class Writer:
 
 
 class Buffer(Writer):
-    """Multi-reader ring buffer.  Buffer(format, size=None); size in items."""
+    """Multi-reader ring buffer.  Buffer(format, size=None); size in items.
+
+    A preallocated byte ring: write() copies the data in (at most two slices, no per-write
+    allocation), each reader keeps its own stream offset, and a reader that falls more than
+    the ring's capacity behind loses the oldest data (as csdr's ring buffer).  Every call is
+    O(bytes moved), independent of the number of readers and of the chunks written so far."""
 
     def __init__(self, format, size=None):
         if not isinstance(format, Format):
             raise ValueError("Buffer format must be a pycsdr.types.Format")
         self._format = format
         item = format.itemsize
-        self._cap = int(size) * item if size else _DEFAULT_BUFFER_BYTES
+        cap = int(size) * item if size else _DEFAULT_BUFFER_BYTES
+        self._cap = max(item, cap - cap % item)
+        self._ring = np.empty(self._cap, dtype=np.uint8)
         self._cond = threading.Condition()
-        self._chunks = []        # (start offset, bytes)
-        self._start = 0          # stream offset of the first retained byte
         self._end = 0            # stream offset past the last written byte
         self._readers = []
         self._ended = False
@@ -80,54 +85,55 @@ class Buffer(Writer):
             self._cond.notify_all()
 
     def write(self, data):
-        b = bytes(data)
-        if not b:
+        src = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) \
+            else data.reshape(-1).view(np.uint8)
+        n = src.size
+        if n == 0:
             return
+        cap = self._cap
         with self._cond:
-            self._chunks.append((self._end, b))
-            self._end += len(b)
-            self._trim()
+            if n > cap:  # only the newest `cap` bytes can be kept
+                self._end += n - cap
+                src = src[n - cap:]
+                n = cap
+            off = self._end % cap
+            first = min(n, cap - off)
+            self._ring[off:off + first] = src[:first]
+            if first < n:
+                self._ring[:n - first] = src[first:]
+            self._end += n
             self._cond.notify_all()
 
-    def _trim(self):
-        live = [r._pos for r in self._readers if not (r._detached or r._stopped)]
-        keep = min(live) if live else self._end
-        keep = max(keep, self._end - self._cap)  # lagging readers lose the oldest data
-        while self._chunks and self._chunks[0][0] + len(self._chunks[0][1]) <= keep:
-            self._chunks.pop(0)
-        self._start = self._chunks[0][0] if self._chunks else self._end
-
     def _take(self, reader):
-        """Called with the condition held: bytes available to `reader`, item aligned."""
-        pos = max(reader._pos, self._start)
+        """Called with the condition held: the bytes available to `reader` (item aligned),
+        copied into the reader's own buffer; a memoryview of it (valid until its next read)."""
+        cap = self._cap
+        pos = max(reader._pos, self._end - cap)
         n = self._end - pos
         n -= n % self._format.itemsize
         if n <= 0:
-            return b""
-        parts = []
-        for off, b in self._chunks:
-            if off + len(b) <= pos:
-                continue
-            if off >= pos + n:
-                break
-            lo = max(0, pos - off)
-            hi = min(len(b), pos + n - off)
-            parts.append(b[lo:hi])
+            return None
+        if reader._out.size < n:
+            reader._out = np.empty(max(n, 2 * reader._out.size), dtype=np.uint8)
+        off = pos % cap
+        first = min(n, cap - off)
+        reader._out[:first] = self._ring[off:off + first]
+        if first < n:
+            reader._out[first:n] = self._ring[:n - first]
         reader._pos = pos + n
-        self._trim()
-        return b"".join(parts)
+        return memoryview(reader._out[:n])
 
     def _remove_reader(self, reader):
         with self._cond:
             if reader in self._readers:
                 self._readers.remove(reader)
-            self._trim()
 
 
 class Reader:
     def __init__(self, buffer):
         self._buffer = buffer
         self._pos = 0
+        self._out = np.empty(0, dtype=np.uint8)  # read()'s memoryview points here
         self._stopped = False
         self._detached = False   # a fused engine reads this buffer instead of this reader
         self.module = None       # native module reading here (graph planning)
@@ -142,8 +148,8 @@ class Reader:
                 if self._stopped:
                     return None
                 data = b._take(self)
-                if data:
-                    return memoryview(data)
+                if data is not None:
+                    return data
                 if b._ended:
                     return None
                 b._cond.wait(0.5)
@@ -151,7 +157,7 @@ class Reader:
     def available(self):
         b = self._buffer
         with b._cond:
-            return b._end - max(self._pos, b._start)
+            return b._end - max(self._pos, b._end - b._cap)
 
     def stop(self):
         self._stopped = True
@@ -165,7 +171,6 @@ class Reader:
         with self._buffer._cond:
             self._detached = True
             self._pos = self._buffer._end
-            self._buffer._trim()
 
 
 class Module:

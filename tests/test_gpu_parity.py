@@ -384,6 +384,104 @@ def test_waterfall_reconfigure_without_drain(amd):
     assert err < 2e-3, (err, np.nonzero(per_row >= 2e-3)[0].tolist(), k, ref.shape[0], switches)
 
 
+def test_waterfall_grow_with_row_copies_held(amd):
+    """The round-4 race, forced: a live fps change (owrx_waterfall_set, FftChain.setFps,
+    csdr/chain/fft.py:57-85) grows the row buffers while the row stream is held by a 300 ms
+    kernel (owrx_debug_stall on stream 4), so the row slots staged before the change still have
+    their copies in flight when their pinned destinations are replaced.  Every row equals the
+    oracle's under its own settings (<= 2e-3 dB), before and after the switch."""
+    import time
+    from openwebrx_amd import synth
+    fs, N, B = 2400000, 4096, 1 << 16
+    fft = amd.params.fft_parameters
+    (a0, h0), (a1, h1) = fft(fs, N, 9, 0.3), fft(fs, N, 30, 0.3)
+    rows0 = 6
+    switch = rows0 * a0 * h0            # the first setting's rows end here (whole blocks below)
+    n = switch + 8 * a1 * h1 + N
+    iq, _ = synth.make_iq(fs, n, ["nfm"])
+    eng = amd.Engine(fs, max_block=B)
+    wf = eng.waterfall(N, h0, a0, adpcm=False)
+    pos, held, r_sw = 0, None, None
+    while pos < n:
+        m = min(B, n - pos)
+        if held is None and pos + m > switch - 2 * a0 * h0:
+            eng.debug_stall(4, 300000)   # the next row slots' copies wait behind this
+            held = time.perf_counter()
+        eng.push(iq[pos:pos + m])
+        pos += m
+        if held is not None and held is not False and pos >= switch:
+            # applies at the end of the row in progress: the frames launched so far decide it
+            launched = (pos - N) // h0 + 1
+            r_sw = -(-launched // a0)
+            wf.set(h1, a1, False)
+            assert time.perf_counter() - held < 0.25, "the change waited for the held copies"
+            held = False
+    eng.sync()
+    rows = wf.read_rows()
+    eng.close()
+    s0 = r_sw * a0 * h0
+    ref = [oracle.fftswap(x) for x in oracle.waterfall_rows(iq[:s0 + N - h0], N, h0, a0)][:r_sw]
+    ref += [oracle.fftswap(x) for x in oracle.waterfall_rows(iq[s0:], N, h1, a1)]
+    ref = np.stack(ref)
+    k = min(rows.shape[0], ref.shape[0])
+    assert k >= r_sw + 4, (rows.shape, ref.shape, r_sw)
+    assert np.max(np.abs(rows[:k] - ref[:k])) < 2e-3
+
+
+def test_waterfall_recreate_without_chains_rows_identical(amd):
+    """A waterfall destroyed and created again on an engine with no chains (blocks drain without
+    waiting for any event, so the slot tail passes blocks whose stream-A copies of the pinned
+    group descriptors may not have run: those pinned buffers go back to the pool only after
+    stream A ran them): the new FftChain's rows equal a fresh engine's, bit for bit."""
+    from openwebrx_amd import synth
+    fs, N, B = 2400000, 4096, 1 << 16
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+    n = 40 * B
+    iq, _ = synth.make_iq(fs, n, ["nfm", "am"])
+    eng = amd.Engine(fs, max_block=B)
+    wf = eng.waterfall(N, hop, avg, adpcm=False)
+    half = 20 * B
+    for i in range(0, half, B):
+        eng.push(iq[i:i + B])
+        if i == 10 * B:               # destroy and recreate mid-stream, several times
+            for _ in range(3):
+                wf.close()
+                wf = eng.waterfall(N, hop, avg, adpcm=False)
+    start = 11 * B
+    for i in range(half, n, B):
+        eng.push(iq[i:i + B])
+    eng.sync()
+    got = wf.read_rows()
+    eng.close()
+    ref_eng = amd.Engine(fs, max_block=B)
+    ref_wf = ref_eng.waterfall(N, hop, avg, adpcm=False)
+    for i in range(start, n, B):
+        ref_eng.push(iq[i:i + B])
+    ref_eng.sync()
+    want = ref_wf.read_rows()
+    ref_eng.close()
+    assert got.shape == want.shape and got.shape[0] > 5, (got.shape, want.shape)
+    assert np.array_equal(got, want)
+
+
+def test_read_chains_rejects_duplicate_handles(amd):
+    """owrx_chains_read_audio / _smeter pop each listed chain's ring on host workers: a handle
+    listed twice is refused (OWRX_EINVAL) and nothing is read."""
+    from openwebrx_amd import synth
+    fs = 2400000
+    iq, offs = synth.make_iq(fs, 1 << 18, ["nfm", "am"])
+    eng = amd.Engine(fs, max_block=1 << 16)
+    a, b = (eng.chain(amd.params.chain_params(fs, o, m)) for o, m in zip(offs, ["nfm", "am"]))
+    for i in range(0, iq.size, 1 << 16):
+        eng.push(iq[i:i + (1 << 16)])
+    eng.sync()
+    with pytest.raises(Exception):
+        eng.read_chains([a, b, a])
+    audio, lens, _, _ = eng.read_chains([a, b])
+    assert lens[0] > 0 and lens[1] > 0
+    eng.close()
+
+
 def test_input_retention_same_outputs(amd):
     """owrx_set_input_retention: with a resident recording the host runs up to r blocks ahead of
     stream A (no wait for block k - 1 before returning); audio, s-meter and waterfall rows are
@@ -784,6 +882,33 @@ def test_ddc_fast_convolution_frame_lengths(amd, m, monkeypatch):
         assert got.size == ref["ddc"].size, (c, got.size, ref["ddc"].size)
         assert rel_rms(got, ref["ddc"]) < 1e-5, (m, c, rel_rms(got, ref["ddc"]))
     eng.close()
+
+
+def test_ddc_group_size_changes_rounding_only(amd):
+    """The fast DDC splits K over workgroups when its tile grid would leave CUs idle
+    (kernels_fcddc.hip fc_kslices), and the slice count follows the group's chain count: a
+    chain alone gets K slices, the same chain among 200 none.  The slices are summed in a fixed
+    order, so each output is deterministic for a given group size; across group sizes the
+    association differs, i.e. a chain's DDC output may change at the rounding level when other
+    clients join or leave (include/owrx_amd.h owrx_chain_create).  Pinned here: the same chain
+    alone and in a 200-chain group agree to 1e-6 rel-RMS, both <= 1e-5 vs the oracle."""
+    from openwebrx_amd import synth
+    fs = 10000000
+    modes = ["nfm", "usb", "am", "cw"] * 50
+    n = 2 * (1 << 20)
+    iq, offs = synth.make_iq(fs, n, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_S16) for o, m in zip(offs, modes)]
+    eng1, (a,) = _run_chains(amd, iq, fs, plist[:1], 1 << 20, ddc_mode="fast")
+    eng2, many = _run_chains(amd, iq, fs, plist, 1 << 20, ddc_mode="fast")
+    ks1, ks2 = eng1.stats()["ddc_mac_kslices_max"], eng2.stats()["ddc_mac_kslices_max"]
+    x, y = a.read_debug(0), many[0].read_debug(0)
+    ref = oracle.stages(iq, plist[0])["ddc"]
+    eng1.close()
+    eng2.close()
+    assert ks1 > ks2 >= 0, (ks1, ks2)  # the two group sizes do take different slice counts
+    assert x.size == y.size == ref.size > 0
+    assert rel_rms(x, y) < 1e-6, rel_rms(x, y)
+    assert rel_rms(x, ref) < 1e-5 and rel_rms(y, ref) < 1e-5
 
 
 def test_ddc_fast_convolution_membership_churn(amd):

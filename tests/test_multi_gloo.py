@@ -37,36 +37,42 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False):
+def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retention=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = torch.Generator().manual_seed(7)
     full = torch.complex(torch.randn(hist + nblocks * block, generator=g),
                          torch.randn(hist + nblocks * block, generator=g))
-    bc = IqBroadcast(torch, dist, "cpu", hist, block, stream=full if rank == 0 else None)
+    bc = IqBroadcast(torch, dist, "cpu", hist, block, stream=full if rank == 0 else None,
+                     retention=retention)
     ok = True
+    live = []  # the windows an engine with this input retention may still read
     for i in range(nblocks):
         if pipelined and i + 1 < nblocks:
             bc.issue(i + 1)  # the next block's broadcast is in flight while block i is used
         t, off = bc.wait(i) if pipelined else bc.step(i)
-        got = t[off - hist: off + block]
-        want = full[i * block: i * block + hist + block]
-        ok &= bool(torch.equal(got, want))
+        live = (live + [(i, t, off)])[-retention:]
+        for k, tk, ok_off in live:  # none of them rewritten yet
+            got = tk[ok_off - hist: ok_off + block]
+            want = full[k * block: k * block + hist + block]
+            ok &= bool(torch.equal(got, want))
     # every rank demodulates its own shard: no reduction, only a barrier for the timing
     dist.barrier()
     q.put((rank, ok))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
-def test_iq_broadcast_world2_gloo(pipelined):
+@pytest.mark.parametrize("pipelined,retention", [(False, 1), (True, 1), (True, 8)])
+def test_iq_broadcast_world2_gloo(pipelined, retention):
     """Every rank reconstructs [history | block] windows equal to rank 0's stream, with the
-    broadcasts one at a time or pipelined one block ahead (bench.py's N > 1 loop)."""
+    broadcasts one at a time or pipelined one block ahead (bench.py's N > 1 loop); with input
+    retention r (bench.py sets 8 at every N) the last r blocks' windows stay intact while the
+    next broadcasts land."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 7, q, pipelined))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 14, q, pipelined, retention))
              for r in range(2)]
     for p in procs:
         p.start()

@@ -135,6 +135,45 @@ def test_buffer_multireader_and_stop():
     assert got == [None]
 
 
+def test_buffer_ring_wraps_and_lagging_reader_loses_oldest():
+    """The byte ring (owrx/dsp.py:846-863 pumps read what writers put in): writes of random
+    sizes wrap the ring; readers at different paces see exactly the stream, item aligned, and
+    one that falls more than the capacity behind resumes at the oldest byte still held."""
+    rng = np.random.default_rng(3)
+    b = M.Buffer(Format.COMPLEX_FLOAT, size=1000)  # 8000 bytes
+    fast, slow = b.getReader(), b.getReader()
+    stream = rng.standard_normal(2 * 30000).astype(np.float32).view(np.complex64)
+    got_fast, pos = [], 0
+    while pos < stream.size:
+        m = min(int(rng.integers(1, 700)), stream.size - pos)
+        b.write(stream[pos:pos + m].tobytes())
+        pos += m
+        got_fast.append(np.frombuffer(bytes(fast.read()), np.complex64))
+    assert np.array_equal(np.concatenate(got_fast), stream[:pos])
+    tail = np.frombuffer(bytes(slow.read()), np.complex64)   # fell far behind: the last 1000
+    assert np.array_equal(tail, stream[pos - 1000:pos])
+    b.write(stream[:3].tobytes())
+    assert np.array_equal(np.frombuffer(bytes(slow.read()), np.complex64), stream[:3])
+
+
+def test_buffer_write_cost_independent_of_history():
+    """write() / read() do not scan earlier chunks or all readers: 20 000 small writes with a
+    reader that never reads (it only loses the oldest data) cost about what 2 000 do, per write."""
+    def run(nw):
+        b = M.Buffer(Format.CHAR, size=1 << 16)
+        idle = [b.getReader() for _ in range(8)]
+        r = b.getReader()
+        t0 = time.perf_counter()
+        for i in range(nw):
+            b.write(b"x" * 100)
+            if i % 16 == 0:
+                r.read()
+        return (time.perf_counter() - t0) / nw
+    run(500)
+    small, large = run(2000), run(20000)
+    assert large < 3 * small + 2e-5, (small, large)
+
+
 def test_reader_stop_drops_unread_bytes():
     """Reader.stop() (csdr/module/__init__.py:36-53 pumps exit on None): read() returns None at
     once, whatever the buffer still holds for this reader -- unread bytes are dropped, which is
