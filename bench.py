@@ -412,7 +412,48 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
                     "not (first_failing_level) or the time budget"}
 
 
-def _dropin_run(fs, C, blocks, paced, pump_limit):
+def _scaled_steps(fs, n_fft):
+    """The recorded NFM client graph (tests/golden/dsp_graph.json, 10 Msps) and FftChain graph
+    (tests/golden/spectrum_graph.json) at another input rate: the Selector's FirDecimate /
+    FractionalDecimator parameters from params.decimation (Decimator._getDecimation, golden-
+    pinned by tests/test_params.py; no FractionalDecimator where the rate divides, as
+    selector.py:32 builds none) and the FftChain's from params.fft_parameters; the rest of the
+    graph (12 kHz Bandpass, Squelch, demodulator, ClientAudioChain) is rate independent."""
+    import copy
+    import dsp_replay
+    from openwebrx_amd import params
+    s = copy.deepcopy(dsp_replay.steps()["nfm"])
+    d, frac, tbw, cutoff = params.decimation(fs, 12000)
+    keep, remap = [], {}
+    for i, g, src in s["graph"]:
+        if g["class"] == "FractionalDecimator" and frac == 1.0:
+            remap[i] = remap[src]  # its readers read its input
+            continue
+        remap[i] = len(keep)
+        keep.append((i, g, src))
+    graph = []
+    for i, g, src in keep:
+        if g["class"] == "FirDecimate":
+            g.update(decimation=d, transition=tbw, cutoff=cutoff)
+        if g["class"] == "FractionalDecimator":
+            g["rate"] = frac
+        graph.append([remap[i], g, remap[src] if src >= 0 else src])
+    s["graph"] = graph
+    avg, hop = params.fft_parameters(fs, n_fft, 9, 0.3)
+    with open(os.path.join(ROOT, "tests", "golden", "spectrum_graph.json")) as f:
+        sg = copy.deepcopy({x["step"]: x for x in json.load(f)}["start_adpcm"])
+    for g in sg["graph"]:
+        for k in ("size", "fft_size"):
+            if k in g:
+                g[k] = n_fft
+        if "every_n_samples" in g:
+            g["every_n_samples"] = hop
+        if "avg_number" in g:
+            g["avg_number"] = avg
+    return s, sg
+
+
+def _dropin_run(fs, C, blocks, paced, pump_limit, steps=None):
     """One drop-in run: C ClientDemodulatorChain graphs as the reference builds them
     (tests/golden/dsp_graph.json "nfm": Shift -> FirDecimate -> ... -> AdpcmEncoder, one Shift
     rate per client) plus the SpectrumThread's FftChain (tests/golden/spectrum_graph.json
@@ -429,7 +470,7 @@ def _dropin_run(fs, C, blocks, paced, pump_limit):
     from openwebrx_amd.pycsdr.types import Format
     if 2 * C + 1 > pump_limit:
         raise ValueError("%d pump threads over the limit %d" % (2 * C + 1, pump_limit))
-    s = dsp_replay.steps()["nfm"]
+    s = steps[0] if steps else dsp_replay.steps()["nfm"]
     offs = synth.carrier_offsets(fs, C)
     wide = M.Buffer(Format.COMPLEX_FLOAT, size=1 << 23)
     pumps, got = [], {}
@@ -468,8 +509,11 @@ def _dropin_run(fs, C, blocks, paced, pump_limit):
                 m.stop()
         pump("audio%d" % c, outs[cls.index("AdpcmEncoder")])
         pump("smeter%d" % c, power)
-    with open(os.path.join(ROOT, "tests", "golden", "spectrum_graph.json")) as f:
-        sg = {x["step"]: x for x in json.load(f)}["start_adpcm"]
+    if steps:
+        sg = steps[1]
+    else:
+        with open(os.path.join(ROOT, "tests", "golden", "spectrum_graph.json")) as f:
+            sg = {x["step"]: x for x in json.load(f)}["start_adpcm"]
     fmods = [dsp_replay._make(d) for d in sg["graph"]]
     allmods += fmods
     for a, b in zip(fmods, fmods[1:]):
@@ -550,6 +594,25 @@ def _dropin_run(fs, C, blocks, paced, pump_limit):
         res["msps"] = round(blocks * blk / (t_end - t0) / 1e6, 2)
         res["seconds"] = round(t_end - t0, 3)
     return res
+
+
+def dropin_c4(clients, seconds, pump_limit):
+    """The drop-in at C4's rate on one GPU: 61.44 Msps into the 65 536-bin
+    FftChain plus `clients` NFM ClientDemodulatorChain graphs (the recorded graphs at that rate,
+    _scaled_steps), paced at the stream's wall-clock rate, every output on its own pump."""
+    fs = 61440000
+    _log("drop-in C4: %d clients paced at 61.44 Msps" % clients)
+    from openwebrx_amd.pycsdr import _graph
+    blk = _graph.BLOCK
+    try:
+        r = _dropin_run(fs, clients, max(8, int(seconds * fs / blk)), True, pump_limit,
+                        steps=_scaled_steps(fs, 65536))
+    except Exception as exc:
+        r = {"clients": clients, "error": str(exc)[:200], "keeps_up": False}
+    r["stream_msps"] = fs / 1e6
+    r["fft_size"] = 65536
+    _log("  " + json.dumps(r))
+    return r
 
 
 def dropin_check(fs, clients, ladder, seconds, budget_s, pump_limit):
@@ -709,6 +772,9 @@ def main():
     ap.add_argument("--dropin-ladder", default="256,384,448",
                     help="client counts of the drop-in's paced ladder (2 pump threads each)")
     ap.add_argument("--dropin-seconds", type=float, default=3.0)
+    ap.add_argument("--dropin-c4-clients", type=int, default=128,
+                    help="clients of the drop-in run at C4's rate (61.44 Msps, 65536-bin "
+                         "FftChain, paced; 0: skip)")
     ap.add_argument("--loop-blocks", type=int, default=0,
                     help="A/B: the recording holds this many blocks and the stream loops over "
                          "them (0: one recording as long as the run)")
@@ -994,6 +1060,8 @@ def main():
         dropin = dropin_check(fs, args.dropin_clients,
                               [int(v) for v in args.dropin_ladder.split(",") if v],
                               args.dropin_seconds, 60.0, 900)
+        if args.dropin_c4_clients > 0:
+            dropin["c4"] = dropin_c4(args.dropin_c4_clients, args.dropin_seconds, 900)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:

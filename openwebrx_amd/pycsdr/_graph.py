@@ -609,7 +609,14 @@ class EngineDriver:
             if not self.engines:
                 continue
             x = np.frombuffer(data, dtype=np.complex64)
-            pending.append(x)
+            if not pending and x.size >= BLOCK:
+                # a whole block in one read: pushed straight from the reader's buffer (valid
+                # until its next read; the push copies it into the engine's staging)
+                with _lock:
+                    self._push(x)
+                    self._drain()
+                continue
+            pending.append(x.copy())  # the reader's buffer is reused by the next read
             npend += x.size
             if npend < BLOCK:
                 continue

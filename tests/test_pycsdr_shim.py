@@ -305,6 +305,44 @@ def test_planner_matches_reference_chain_params(mode):
     _graph.finish(wide)
 
 
+def test_bench_c4_dropin_graphs_plan_like_the_reference():
+    """bench.py's drop-in at C4's rate rebuilds the recorded NFM client graph and FftChain at
+    61.44 Msps (_scaled_steps): the planner fuses them into exactly the chain parameters the
+    reference chain code implies at that rate (params.chain_params: D = 5120, no
+    FractionalDecimator) and the 65 536-bin FftChain's (avg 149, hop 45 816)."""
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    import bench
+    import dsp_replay
+    fs = 61440000
+    s, sg = bench._scaled_steps(fs, 65536)
+    wide, mods, outs, power = dsp_replay.build(s)
+    mods[0].setRate(params.shift_rate(123456, fs))
+    seg = _graph.plan_segment(mods[0])
+    assert seg is not None and seg[0] == "chain"
+    got = _graph.chain_params_struct(seg[1])
+    want = params.chain_params(fs, 123456, "nfm", output=_lib.OUT_ADPCM)
+    assert want.decimation == 5120
+    for name, _ in _lib.ChainParams._fields_:
+        g, w = getattr(got, name), getattr(want, name)
+        assert g == pytest.approx(w, rel=1e-6, abs=1e-12), name
+    fmods = [dsp_replay._make(d) for d in sg["graph"]]
+    for a, b in zip(fmods, fmods[1:]):
+        buf = M.Buffer(a.getOutputFormat())
+        a.setWriter(buf)
+        b.setReader(buf.getReader())
+    fmods[-1].setWriter(M.Buffer(Format.CHAR))
+    fmods[0].setReader(wide.getReader())
+    kind, p, _ = _graph.plan_segment(fmods[0])
+    avg, hop = params.fft_parameters(fs, 65536, 9, 0.3)
+    assert kind == "waterfall" and p == dict(fft_size=65536, hop=hop, avg=avg, add_db=-70.0,
+                                             adpcm=True) and (avg, hop) == (149, 45816)
+    _graph.finish(wide)
+
+
 def test_planner_waterfall_and_rewire():
     wide = M.Buffer(Format.COMPLEX_FLOAT)
     mods = fft_chain(4096, 2867, 93)
