@@ -838,7 +838,8 @@ def main():
     eng.set_input_retention(retention)
     # 16 blocks in flight for the headline engine (256 chains: a few MB of staging per block);
     # the capacity ladder's engines keep the default 8 (their staging grows with the chains)
-    eng.set_pipeline_depth(int(os.environ.get("OWRX_BENCH_DEPTH", "16")))
+    depth = int(os.environ.get("OWRX_BENCH_DEPTH", "16"))
+    eng.set_pipeline_depth(depth)
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:
@@ -1091,6 +1092,10 @@ def main():
                 "step_samples": bps * block,
                 "parallelism": "1 GPU" if world == 1 else
                 "IQ broadcast over RCCL from rank 0, %d chains per rank" % C,
+                # the same engine set-up at every N (rank 0 holds the waterfall)
+                "input_retention_blocks": retention,
+                "pipeline_depth_blocks": depth,
+                "waterfall_batch_frames_rank0": wf_batch,
             },
             "value_definition": ("Msamples/s of the ONE wideband IQ stream ingested, at any N: "
                                  "each GPU runs the whole stream (broadcast from rank 0; waterfall "
