@@ -1120,19 +1120,36 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
                 for (int c = 1; c < 16; ++c) a[c] = f2mul(a[c], sm[K::TW3 + c * 4 + q]);
                 const float s1 = q < 2 ? 1.0f : -1.0f;
                 const float s2 = (q == 0 || q == 3) ? 1.0f : -1.0f;
+                const bool q3 = q == 3;
+                // four bins at a time, each step over all four: the cross-lane moves of one bin
+                // fill the others' DPP hazard slots (one bin at a time was a dependent chain of
+                // ~10 instructions with s_nops between)
 #pragma unroll
-                for (int c = 0; c < 16; ++c) {
-                    float2 v = a[c];
-                    // stage 1: partner q ^ 2
-                    v.x = fmaf(dppq<0x4E>(v.x), s1, v.x);
-                    v.y = fmaf(dppq<0x4E>(v.y), s1, v.y);
-                    // lane 3: * -i
-                    const float vx = q == 3 ? v.y : v.x;
-                    const float vy = q == 3 ? -v.x : v.y;
-                    // stage 2: partner q ^ 1
-                    v.x = fmaf(dppq<0xB1>(vx), s2, vx);
-                    v.y = fmaf(dppq<0xB1>(vy), s2, vy);
-                    acc[c] = acc[c] + fmaf(v.y, v.y, v.x * v.x);
+                for (int c0 = 0; c0 < 16; c0 += 4) {
+                    float vx[4], vy[4], px[4], py[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {  // stage 1: partner q ^ 2
+                        px[u] = dppq<0x4E>(a[c0 + u].x);
+                        py[u] = dppq<0x4E>(a[c0 + u].y);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float x = fmaf(px[u], s1, a[c0 + u].x);
+                        const float y = fmaf(py[u], s1, a[c0 + u].y);
+                        vx[u] = q3 ? y : x;  // lane 3: * -i
+                        vy[u] = q3 ? -x : y;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {  // stage 2: partner q ^ 1
+                        px[u] = dppq<0xB1>(vx[u]);
+                        py[u] = dppq<0xB1>(vy[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float x = fmaf(px[u], s2, vx[u]);
+                        const float y = fmaf(py[u], s2, vy[u]);
+                        acc[c0 + u] = acc[c0 + u] + fmaf(y, y, x * x);
+                    }
                 }
             }
             if (f == 1) WF_STAMP(6);
