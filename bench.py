@@ -747,6 +747,8 @@ def main():
                          "metric's; the others are reported for reference)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-waterfall", action="store_true")
+    ap.add_argument("--no-pairing", action="store_true",
+                    help="one engine block per 2^20-sample block (owrx_set_block_pairing off)")
     ap.add_argument("--realtime-seconds", type=float, default=3.0,
                     help="paced real-time check at 10 Msps through the host push path (0: skip)")
     ap.add_argument("--no-timing", action="store_true",
@@ -840,6 +842,13 @@ def main():
     # the capacity ladder's engines keep the default 8 (their staging grows with the chains)
     depth = int(os.environ.get("OWRX_BENCH_DEPTH", "16"))
     eng.set_pipeline_depth(depth)
+    # block pairing (owrx_set_block_pairing) where consecutive blocks are contiguous in memory
+    # (rank 0's recording; the broadcast windows of ranks > 0 are not): two 2^20-sample blocks per
+    # engine launch sequence, the DDC GEMM reading the filter spectra once for both, outputs
+    # byte-identical (test_block_pairing_same_outputs)
+    pairing = rank == 0 and not args.no_pairing and retention >= 4
+    if pairing:
+        eng.set_block_pairing(True)
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:
@@ -969,6 +978,9 @@ def main():
     T += 1 - (T % 2)
     d = {k: s1[k] - s0[k] for k in s1}
     tsteps = max(1, d["timed_blocks"])  # the gpu_ms_* sums cover the timed blocks only
+    # caller blocks per engine block (2 when every pair formed: owrx_set_block_pairing)
+    per_engine = max(1.0, d["samples_in"] / block / max(1, d["blocks"]))
+    tblocks = tsteps * per_engine
     launches = d["ddc_launches"]
     ddc_ms = d["gpu_ms_ddc"]
     nk_total = d["ddc_outputs"] / max(1, C)
@@ -1096,6 +1108,7 @@ def main():
                 "input_retention_blocks": retention,
                 "pipeline_depth_blocks": depth,
                 "waterfall_batch_frames_rank0": wf_batch,
+                "block_pairing_rank0": bool(pairing),
             },
             "value_definition": ("Msamples/s of the ONE wideband IQ stream ingested, at any N: "
                                  "each GPU runs the whole stream (broadcast from rank 0; waterfall "
@@ -1121,6 +1134,10 @@ def main():
                 "k_slices": mac_kslices,
                 "algorithmic_bytes_per_launch": round(mac_bytes_launch) if mac_bytes_launch else None,
                 "algorithmic_flop_per_launch": round(mac_flop_launch) if mac_flop_launch else None,
+                # per input sample of the stream: W is read once per launch, so pairing halves it
+                "algorithmic_bytes_per_input_sample": (round(mac_bytes_launch / (per_engine * block), 2)
+                                                       if mac_bytes_launch else None),
+                "blocks_per_launch": round(per_engine, 3),
                 "arithmetic_intensity_flop_per_byte": round(mac_ai, 2) if mac_ai else None,
                 "ridge_flop_per_byte": round(RIDGE, 2),
                 "achieved_tflops": round(achieved_tf, 3),
@@ -1131,8 +1148,9 @@ def main():
                         "MAC over the frames that carry outputs: 8 M Dp C F) over its algorithmic "
                         "bytes (filter spectra W, unique per chain and bin, + branch spectra U + "
                         "products Y, each moved once) against the ridge 157.3 TFLOP/s / 8 TB/s; "
-                        "W's bytes do not depend on the frames per block, so 2^20-sample blocks "
-                        "(F ~ 10) sit under the ridge (HBM) and 2^22 (F ~ 31) over it (MFMA).  "
+                        "W's bytes do not depend on the frames per launch, so a 2^20-sample block "
+                        "(F ~ 13) sits under the ridge (HBM), a pair of them (block pairing, F ~ 26) "
+                        "closer to it and 2^22 (F ~ 31) over it (MFMA).  "
                         "achieved = that bound's quantity / the average launch time from HIP "
                         "events around the kernel on the engine stream; the other figure beside "
                         "it.  traffic = HBM bytes per launch from separate rocprofv3 --pmc "
@@ -1190,13 +1208,15 @@ def main():
                         "flop count of the direct form it replaces (C outputs (4T + 6D), SURVEY "
                         "8d): what the same outputs would need at that rate",
             },
+            # per 2^20-sample block: a timed engine block of a paired engine holds two of them
             "kernels_ms_per_block": {
-                "ddc": round(ddc_ms / tsteps, 3),
-                "ddc_mac": round(mac_ms / tsteps, 3),
-                "waterfall_incl_descriptors": round(wf_ms / tsteps, 3),
-                "post_stream_a": round(post_ms / tsteps, 3),
+                "ddc": round(ddc_ms / tblocks, 3),
+                "ddc_mac": round(mac_ms / tblocks, 3),
+                "waterfall_incl_descriptors": round(wf_ms / tblocks, 3),
+                "post_stream_a": round(post_ms / tblocks, 3),
                 "post_to_encoder_end": round(d["gpu_ms_serial"] / tsteps, 3),
                 "timed_blocks": d["timed_blocks"],
+                "blocks_per_engine_block": round(per_engine, 3),
             },
             "pool_allocs_timed": int(d["pool_allocs"]),
             "host_ms_per_block": {k[8:]: round(d[k] / (args.steps * bps), 3) for k in

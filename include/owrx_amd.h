@@ -108,6 +108,16 @@ int owrx_wait_stream(owrx_engine* e, void* stream);
  * engine waits only for block k - r + 1's stream-A work before returning from block k, so the
  * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 31. */
 int owrx_set_input_retention(owrx_engine* e, int blocks);
+/* Block pairing (enable = 1; input retention >= 4, before the first chain, waterfall and block):
+ * owrx_process_device holds a block until the next call; when the next block follows it in
+ * memory (block + nsamples == next) both run as one engine block, otherwise the held one runs
+ * alone.  Every stage runs once per pair and the DDC's filter spectra are read once for both
+ * blocks' frames; each block keeps its own DDC frames and zero padding, so every output is
+ * byte-identical to unpaired processing.  A held block runs at the latest on the next call that
+ * is not a read (owrx_sync, chain or waterfall changes, push / commit) or owrx_wait_stream's
+ * successor, so it adds one block of latency: for callers that are blocks ahead of the stream
+ * (a recording), not for a live source.  Staging is sized for 2 x max_block. */
+int owrx_set_block_pairing(owrx_engine* e, int enable);
 /* Blocks of chain work in flight (streams A -> B -> C -> host rings), 1..16, default 8; only
  * before the first chain and block.  Each one holds pinned and device staging for every chain
  * (at 98 304 chains ~0.5 GB pinned per block), so deeper pipelines are for few-chain, high-rate

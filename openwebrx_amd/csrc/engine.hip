@@ -108,7 +108,7 @@ int64_t fc_w_chain_offset(int c, int Dp);  // chain c's first entry in a bin's r
 int fc_w_tile();                           // chains per W tile: capacities are multiples of it
 int fc_w_layout_check(int Dp, int cap);    // host self-test of the tiled W layout
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
-                         const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
+                         int64_t blk_end1, int nk1, const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
                          hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form);
@@ -647,6 +647,7 @@ struct GroupWork {
     int64_t k_end;
     int nk;
     bool fast;
+    int nk1;  // outputs of the first caller block of a pair (= nk unpaired)
 };
 
 struct owrx_engine {
@@ -708,6 +709,11 @@ struct owrx_engine {
     hipEvent_t evIn[kInEv] = {};
     int64_t in_done = -1;
     int retention = 1;
+    // block pairing (owrx_set_block_pairing): a caller block held until the next one arrives,
+    // then both run as one engine block (pend_n: the held block's samples, 0 = none)
+    bool pair = false;
+    const float2* pend_blk = nullptr;
+    int64_t pend_n = 0;
     // blocks of chain work in flight (owrx_set_pipeline_depth, <= kSlots): every slot holds
     // pinned and device staging for all chains, so the depth is the caller's memory trade
     int nslots = kDefaultSlots;
@@ -821,8 +827,11 @@ static int sync_stream(owrx_engine* e, hipStream_t st) {
     return wait_ev(e, e->evSync);
 }
 
+// the largest engine block: two caller blocks when pairing
+static int64_t proc_block(const owrx_engine* e) { return e->pair ? 2 * e->max_block : e->max_block; }
+
 static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
-    int64_t nk = e->max_block / D + 4;
+    int64_t nk = proc_block(e) / D + 4;
     if (frac > 0 && frac < 1.0) nk = (int64_t)std::ceil(nk / frac) + 4;
     return nk;
 }
@@ -1294,7 +1303,7 @@ static int wf_reserve(owrx_engine* e, Waterfall* w, int groups, int rows, int bp
 // space, and the launches around one ran several times slower, measured 0.5-1 ms of stalled
 // kernels per allocation).  Descriptors: the groups plus the tail split's single frames.
 static int wf_initial_reserve(owrx_engine* e, Waterfall* w) {
-    const int64_t span = w->batch_min > 1 ? e->history + e->max_block : e->max_block;
+    const int64_t span = w->batch_min > 1 ? e->history + proc_block(e) : proc_block(e);
     const int hop = std::max(1, w->pending ? std::min(w->hop, w->new_hop) : w->hop);
     const int avg = std::max(1, w->pending ? std::min(w->avg, w->new_avg) : w->avg);
     const int64_t frames = span / hop + 2;
@@ -1360,7 +1369,7 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         HIPCHK(dalloc(&g->d_chains, (size_t)g->chains_cap));
         for (auto& h : g->h_chains) HIPCHK(halloc(&h, (size_t)g->chains_cap));
     }
-    const int64_t nk_max = e->max_block / g->D + 4;
+    const int64_t nk_max = proc_block(e) / g->D + 4;
     // Launch shape: each tile group's D phases are split into nseg segments, one 4-wave
     // workgroup each (kernels_ddc.hip); stream A's CUs hold ddc_blocks_per_cu of them.
     const int R = 32;
@@ -1667,9 +1676,11 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
 
 
 // Every waterfall's ready frames (batching rule, or all of them with `force`) on stream A, then
-// the completed rows' FftAdpcm + copy on a row slot's stream.
+// the completed rows' FftAdpcm + copy on a row slot's stream, or with `rows_on_a` on stream A
+// behind their FFT, one workgroup per row (owrx_sync's flush: A has no block behind it, and the
+// row queue's 4 CUs take ~3 ms for a 3 840-frame batch's 40 rows).
 static int run_waterfalls(owrx_engine* e, const float2* blk, int64_t blk_start, int64_t blk_end,
-                          bool force, bool timed, Slot* S) {
+                          bool force, bool timed, Slot* S, bool rows_on_a = false) {
     bool any_rows = false;
     if (!e->wfs.empty()) {
         const double t = now_ms();
@@ -1684,8 +1695,11 @@ static int run_waterfalls(owrx_engine* e, const float2* blk, int64_t blk_start, 
             any_rows |= done > 0;
         }
         if (any_rows) {
-            HIPCHK(hipEventRecord(R.evWf, e->sA));
-            HIPCHK(hipStreamWaitEvent(R.stream, R.evWf, 0));
+            const hipStream_t rs = rows_on_a ? e->sA : R.stream;
+            if (!rows_on_a) {
+                HIPCHK(hipEventRecord(R.evWf, e->sA));
+                HIPCHK(hipStreamWaitEvent(R.stream, R.evWf, 0));
+            }
             for (auto& kv : e->wfs) {
                 Waterfall* w = kv.second.get();
                 const int nr = w->pend_rows[ri];
@@ -1693,13 +1707,13 @@ static int run_waterfalls(owrx_engine* e, const float2* blk, int64_t blk_start, 
                 const int64_t rb = w->row_bytes_for(w->pend_adpcm[ri]);
                 if (w->pend_adpcm[ri]) {
                     HIPCHK(launch_wf_adpcm(w->d_s16[ri], w->N, nr, w->d_bytes[ri], (int)rb,
-                                           e->rows_grid, R.stream));
-                    HIPCHK(kcopy(w->h_bytes[ri], w->d_bytes[ri], rb * nr, R.stream));
+                                           rows_on_a ? 0 : e->rows_grid, rs));
+                    HIPCHK(kcopy(w->h_bytes[ri], w->d_bytes[ri], rb * nr, rs));
                 } else {
-                    HIPCHK(kcopy(w->h_bytes[ri], w->d_f32[ri], rb * nr, R.stream));
+                    HIPCHK(kcopy(w->h_bytes[ri], w->d_f32[ri], rb * nr, rs));
                 }
             }
-            HIPCHK(hipEventRecord(R.evC, R.stream));
+            HIPCHK(hipEventRecord(R.evC, rs));
             R.pending = true;
             e->row_head++;
         }
@@ -1915,6 +1929,10 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
 }
 
 // Wait until block j's stream-A work (which read its input and its staged descriptors) is done.
+// engine blocks after which the caller's oldest retained input is read: `retention` caller
+// blocks, each engine block of a paired engine holding up to two of them
+static int in_keep(const owrx_engine* e) { return e->pair ? (e->retention - 1) / 2 : e->retention; }
+
 static int wait_input_block(owrx_engine* e, int64_t j) {
     if (j <= e->in_done || j < 0) return OWRX_OK;
     RCCHK(wait_ev(e, e->evIn[j % kInEv]));
@@ -1922,7 +1940,9 @@ static int wait_input_block(owrx_engine* e, int64_t j) {
     return OWRX_OK;
 }
 
-static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
+// `split` > 0: a pair of caller blocks, the first `split` samples long (owrx_set_block_pairing);
+// every stage runs once over both, the fast DDC with each block's own frame placement
+static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t split = 0) {
     const double t_enter = now_ms();
     RCCHK(flush_zero(e));  // pool buffers of chains / waterfalls created since the last block
     // Block k's pinned descriptors are staged per slot (reused by block k + kSlots, after the
@@ -1938,7 +1958,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     }();
     if (wait_first) {
         const double t = now_ms();
-        RCCHK(wait_input_block(e, e->block_index - e->retention));
+        RCCHK(wait_input_block(e, e->block_index - in_keep(e)));
         e->stats.host_ms_wait_input += now_ms() - t;
     }
     const int bp = (int)(e->block_index % e->nslots);
@@ -2011,8 +2031,15 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             }
         }
         g->chains_stale = stale;  // consumed by this block's upload below
+        // a pair's first block: the outputs its own call would have produced
+        int64_t nk1 = nk64;
+        if (split > 0) {
+            const int64_t e1 = blk_start + split;
+            const int64_t k1 = e1 < g->T ? g->k_next : (e1 - g->T) / g->D + 1;
+            nk1 = std::min(nk64, std::max<int64_t>(0, k1 - g->k_next));
+        }
         work.push_back(GroupWork{g, k_end, (int)nk64,
-                                 g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST});
+                                 g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST, (int)nk1});
     }
     // the slot's post descriptors and lane lists: as built for its last block unless a chain
     // changed since (or the groups with outputs differ); then this block's nk / k_begin
@@ -2090,7 +2117,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
             // the first fast group's GEMM is timed (one group in the benchmark configurations)
             const bool tm = timed && !S.timed_mac;
             int form = 0;
-            HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, blk_end, g->d_chains, g->d_fc_w,
+            HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, blk_end, split > 0 ? blk_start + split : blk_end, gw.nk1,
+                                 g->d_chains, g->d_fc_w,
                                  g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
                                  g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
                                  g->d_fc_y, (int64_t)g->fc_y_elems, g->d_partial[si], e->sA,
@@ -2102,7 +2130,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
                 // algorithmic work of that GEMM: 8 flop per complex MAC over the frames that
                 // carry outputs; bytes = W (every member's spectra) + U + Y, each moved once
                 const double M = (double)g->fc_M;
-                const double F = (double)((nk + g->fc_V - 1) / g->fc_V);
+                const double F = (double)((gw.nk1 + g->fc_V - 1) / g->fc_V +
+                                          (nk - gw.nk1 + g->fc_V - 1) / g->fc_V);
                 const double C = (double)g->members.size();
                 e->stats.ddc_mac_flop += 8.0 * M * g->fc_Dp * C * F;
                 e->stats.ddc_mac_bytes += 8.0 * M * g->fc_Dp * (C + F) + 8.0 * C * F * M;
@@ -2195,7 +2224,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     e->stats.host_ms_launch += now_ms() - t_launch;
     if (!wait_first) {  // the oldest input the caller may reuse now (see the top)
         const double t = now_ms();
-        RCCHK(wait_input_block(e, e->block_index - e->retention));
+        RCCHK(wait_input_block(e, e->block_index - in_keep(e)));
         e->stats.host_ms_wait_input += now_ms() - t;
     }
     e->pos = blk_end;
@@ -2211,11 +2240,20 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
     return OWRX_OK;
 }
 
+// the held caller block alone (owrx_set_block_pairing)
+static int pair_flush(owrx_engine* e) {
+    const float2* b = e->pend_blk;
+    const int64_t n = e->pend_n;
+    e->pend_n = 0;
+    e->pend_blk = nullptr;
+    return process_block(e, b, n);
+}
+
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
 
-#define ENGINE_GUARD(e)                                              \
+#define ENGINE_GUARD_HELD(e)                                         \
     if (!(e)) {                                                      \
         set_last_error("null engine");                               \
         return OWRX_EINVAL;                                          \
@@ -2227,6 +2265,18 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n) {
         return (e)->stalled ? OWRX_ETIMEDOUT : OWRX_EIO;             \
     }                                                                \
     hipSetDevice((e)->device);
+
+// every entry point except owrx_process_device, the reads and the stats: a held caller block
+// (owrx_set_block_pairing) runs first, so the call sees the engine as after that block alone
+#define ENGINE_GUARD(e)                                              \
+    ENGINE_GUARD_HELD(e)                                             \
+    if ((e)->pend_n > 0) {                                           \
+        const int _prc = pair_flush(e);                              \
+        if (_prc < 0) {                                              \
+            if (_prc == OWRX_EIO || _prc == OWRX_ETIMEDOUT) (e)->failed = true; \
+            return _prc;                                             \
+        }                                                            \
+    }
 
 #define RC_FAIL(e, expr)                             \
     do {                                             \
@@ -2552,21 +2602,58 @@ int owrx_debug_stall(owrx_engine* e, int stream, int64_t us) {
 // Stream A waits, on the GPU, for the work enqueued so far on the caller's stream (a collective
 // that writes the next block's window: the broadcast of multi.IqBroadcast); no host wait.
 int owrx_wait_stream(owrx_engine* e, void* stream) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     HIPCHK(hipEventRecord(e->evExt, (hipStream_t)stream));
     HIPCHK(hipStreamWaitEvent(e->sA, e->evExt, 0));
     return OWRX_OK;
 }
 
 int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t n) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     if (!iq_dev || n < 0 || n > e->max_block) {
         set_last_error("owrx_process_device: bad block (n=%lld, max %lld)", (long long)n,
                        (long long)e->max_block);
         return OWRX_EINVAL;
     }
     if (n == 0) return OWRX_OK;
-    RC_FAIL(e, process_block(e, (const float2*)iq_dev, n));
+    const float2* blk = (const float2*)iq_dev;
+    if (!e->pair) {
+        RC_FAIL(e, process_block(e, blk, n));
+        return OWRX_OK;
+    }
+    // pairing: the held block and this one, contiguous, run as one engine block; otherwise the
+    // held one alone, and this one is held
+    if (e->pend_n > 0) {
+        if (blk == e->pend_blk + e->pend_n) {
+            const float2* b = e->pend_blk;
+            const int64_t n1 = e->pend_n;
+            e->pend_n = 0;
+            e->pend_blk = nullptr;
+            RC_FAIL(e, process_block(e, b, n1 + n, n1));
+            return OWRX_OK;
+        }
+        RC_FAIL(e, pair_flush(e));
+    }
+    e->pend_blk = blk;
+    e->pend_n = n;
+    // input retention while held: the caller's block k - retention has been read (each engine
+    // block holds at most two caller blocks, so engine block b - (retention - 1) / 2 covers it)
+    const double t = now_ms();
+    RC_FAIL(e, wait_input_block(e, e->block_index - 1 - (e->retention - 1) / 2));
+    e->stats.host_ms_wait_input += now_ms() - t;
+    return OWRX_OK;
+}
+
+int owrx_set_block_pairing(owrx_engine* e, int enable) {
+    ENGINE_GUARD(e);
+    // a paired engine sizes its staging for two caller blocks: before the first chain and block
+    if (enable < 0 || enable > 1 || e->block_index != 0 || !e->chains.empty() || !e->wfs.empty() ||
+        e->post_cap > 0 || (enable && e->retention < 4)) {
+        set_last_error("owrx_set_block_pairing: 0 or 1, before the first chain, waterfall and "
+                       "block, with input retention >= 4");
+        return OWRX_EINVAL;
+    }
+    e->pair = enable != 0;
     return OWRX_OK;
 }
 
@@ -2673,10 +2760,13 @@ int owrx_push_iq_cs16(owrx_engine* e, const int16_t* iq, int64_t n, float gain) 
 int owrx_sync(owrx_engine* e) {
     ENGINE_GUARD(e);
     // batched waterfalls: launch what is pending on the newest block's window (still valid:
-    // owrx_process_device's contract, or the ring); every slot drained first (the flush stages
-    // its descriptors in the next block's slot)
-    RC_FAIL(e, drain_all(e));
-    if (e->last_blk) RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr));
+    // owrx_process_device's contract, or the ring).  The flush stages its descriptors in the
+    // next block's slot, so only that slot's previous block must have drained; the rest of the
+    // pipeline (B's and C's last blocks) drains behind the flush instead of before it.
+    if (e->last_blk) {
+        RC_FAIL(e, drain_slots(e, true, e->nslots - 1));
+        RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr, true));
+    }
     RC_FAIL(e, drain_all(e));
     return OWRX_OK;
 }
@@ -2807,14 +2897,14 @@ int owrx_waterfall_destroy(owrx_engine* e, int handle) {
 }
 
 int64_t owrx_waterfall_row_bytes(owrx_engine* e, int handle) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->wfs.find(handle);
     if (it == e->wfs.end()) return OWRX_EINVAL;
     return it->second->row_bytes();
 }
 
 int64_t owrx_waterfall_read(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->wfs.find(handle);
     if (it == e->wfs.end() || !dst || max_bytes < 0) return OWRX_EINVAL;
     Waterfall* w = it->second.get();
@@ -2941,6 +3031,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
                          hipMemcpyHostToDevice));
         // fast-convolution form: frame length, branch padding, U and twiddles
         ng->fc_P = (T + D - 1) / D;
+        // the frame length from the caller's block (a paired engine keeps the unpaired design)
         const int64_t nk_max = e->max_block / D + 4;
         ng->fc_M = ng->fc_P <= 64 ? fc_choose_m(D, ng->fc_P, nk_max) : 0;
         if (const char* v = getenv("OWRX_FC_M")) {  // A/B: force the frame length
@@ -2951,7 +3042,10 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
             const int M = ng->fc_M;
             ng->fc_V = M - ng->fc_P + 1;
             ng->fc_Dp = (D + 95) / 96 * 96;  // kFcDpAlign (kernels_fcddc.hip)
-            ng->fc_Fs = (int)((nk_max + ng->fc_V - 1) / ng->fc_V + 15) & ~15;
+            // frames of the largest engine block; a pair cuts its frames at the caller blocks'
+            // boundary, one frame more
+            const int64_t nk_proc = proc_block(e) / D + 4;
+            ng->fc_Fs = (int)((nk_proc + ng->fc_V - 1) / ng->fc_V + (e->pair ? 1 : 0) + 15) & ~15;
             HIPCHK(dalloc(&ng->d_h, (size_t)T));
             HIPCHK(hipMemcpy(ng->d_h, h.data(), sizeof(float) * T, hipMemcpyHostToDevice));
             std::vector<float> tw = fft_twiddles(M);
@@ -3130,14 +3224,14 @@ int owrx_chain_set_noise_filter(owrx_engine* e, int handle, int enabled, float t
 }
 
 int64_t owrx_chain_read_audio(owrx_engine* e, int handle, uint8_t* dst, int64_t max_bytes) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || !dst || max_bytes < 0) return OWRX_EINVAL;
     return (int64_t)it->second->audio.pop(dst, (size_t)max_bytes);
 }
 
 int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t max_values) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || !dst || max_values < 0) return OWRX_EINVAL;
     return (int64_t)it->second->smeter.pop((uint8_t*)dst, sizeof(float) * (size_t)max_values) /
@@ -3160,7 +3254,7 @@ static bool batched_duplicates(owrx_engine* e, const std::vector<Chain*>& cs) {
 
 int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
                                int64_t max_bytes, int64_t* lens) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     if (n < 0 || (n > 0 && (!handles || !dst || !lens)) || max_bytes < 0) return OWRX_EINVAL;
     // sizes first (each chain's ring, on the host workers), offsets (in order, up to max_bytes),
     // then the copies (workers again)
@@ -3190,7 +3284,7 @@ int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_
 
 int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float* dst,
                                 int64_t max_values, int64_t* counts) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     if (n < 0 || (n > 0 && (!handles || !dst || !counts)) || max_values < 0) return OWRX_EINVAL;
     std::vector<Chain*> cs((size_t)n);
     std::atomic<bool> bad{false};
@@ -3242,7 +3336,7 @@ int owrx_chain_set_taps(owrx_engine* e, int handle, int selector, int audio) {
 
 int64_t owrx_chain_read_tap(owrx_engine* e, int handle, int which, uint8_t* dst,
                             int64_t max_bytes) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || !dst || max_bytes < 0 || which < 0 || which > 1)
         return OWRX_EINVAL;
@@ -3312,7 +3406,7 @@ int owrx_chain_set_secondary_fft(owrx_engine* e, int handle, int fft_size, int e
 }
 
 int64_t owrx_chain_secondary_fft_row_bytes(owrx_engine* e, int handle) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || it->second->sf_n == 0) return OWRX_EINVAL;
     return it->second->sf_row_bytes();
@@ -3320,7 +3414,7 @@ int64_t owrx_chain_secondary_fft_row_bytes(owrx_engine* e, int handle) {
 
 int64_t owrx_chain_read_secondary_fft(owrx_engine* e, int handle, uint8_t* dst,
                                       int64_t max_bytes) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || !dst || max_bytes < 0) return OWRX_EINVAL;
     Chain* c = it->second.get();
@@ -3330,7 +3424,7 @@ int64_t owrx_chain_read_secondary_fft(owrx_engine* e, int handle, uint8_t* dst,
 }
 
 int64_t owrx_chain_origin(owrx_engine* e, int handle) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end()) return OWRX_EINVAL;
     return it->second->origin;
@@ -3348,7 +3442,7 @@ int owrx_set_debug(owrx_engine* e, int enable) {
 
 int64_t owrx_chain_read_debug(owrx_engine* e, int handle, int stage, void* dst,
                               int64_t max_bytes) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     auto it = e->chains.find(handle);
     if (it == e->chains.end() || stage < 0 || stage >= kDebugStages || !dst || max_bytes < 0)
         return OWRX_EINVAL;
@@ -3356,7 +3450,7 @@ int64_t owrx_chain_read_debug(owrx_engine* e, int handle, int stage, void* dst,
 }
 
 int owrx_get_stats(owrx_engine* e, owrx_stats* s) {
-    ENGINE_GUARD(e);
+    ENGINE_GUARD_HELD(e);
     if (!s) return OWRX_EINVAL;
     *s = e->stats;
     int64_t dropped = 0;

@@ -160,17 +160,24 @@ fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rat
 
 // ---- U[kappa][f][r]: M-point DFT of every branch frame --------------------------------------
 // grid: (Dp / kFcRT, F); block 256.  tw: M-point table e^{-j 2 pi m / M}.
+// A pair of caller blocks (owrx_set_block_pairing): frames f < F1 are the first block's, from
+// k_begin and zero past blk_end1, the rest the second block's from k_begin + nk1 -- the frames
+// and zero padding each block's own launch would have had, so U is bit-identical to two
+// launches.  Unpaired: F1 = F, blk_end1 = blk_end.
 template <int M>
 __global__ void __launch_bounds__(256)
-fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64_t k_begin,
-       int V, int D, int Dp, int Fs, const float2* __restrict__ tw, float2* __restrict__ U) {
+fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64_t blk_end1,
+       int64_t k_begin, int nk1, int F1, int V, int D, int Dp, int Fs,
+       const float2* __restrict__ tw, float2* __restrict__ U) {
     using FM = FcM<M>;
     constexpr int RS = FM::RS;         // LDS row stride (float2): column writes hit distinct banks
     __shared__ float2 sm[kFcRT * RS];
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * kFcRT;
     const int f = blockIdx.y;
-    const int64_t k0 = k_begin + (int64_t)f * V;
+    const bool second = f >= F1;
+    const int64_t k0 = second ? k_begin + nk1 + (int64_t)(f - F1) * V : k_begin + (int64_t)f * V;
+    if (!second) blk_end = blk_end1;
     const int j = tid % kFcRT;
     const int r = r0 + j;
     // rows i of the frame: 16 consecutive branches = one 128-B run per row
@@ -559,8 +566,8 @@ OWRX_DEV float2 fc_rotator(const DdcChain& ch, int64_t n) {
 template <int M>
 __global__ void __launch_bounds__(256)
 fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nchains, int Fs,
-       int F, int V, int D, int64_t k_begin, int nk, const float2* __restrict__ tw,
-       float2* __restrict__ out, int ks, int64_t y_slice) {
+       int F, int V, int D, int64_t k_begin, int nk, int nk1, int F1,
+       const float2* __restrict__ tw, float2* __restrict__ out, int ks, int64_t y_slice) {
     using FM = FcM<M>;
     constexpr int RW = FM::R3 ? 3072 / M : 1024 / M;
     constexpr int RS = FM::RS;
@@ -592,8 +599,9 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
         const int row = row0 + rr;
         if (row >= nrows || m >= V) continue;
         const int c = row / F, f = row % F;
-        const int kk = f * V + m;
-        if (kk >= nk) continue;
+        // the frame's block (fc_fwd): outputs [0, nk1) from frames < F1, then [nk1, nk)
+        const int kk = f < F1 ? f * V + m : nk1 + (f - F1) * V + m;
+        if (kk >= (f < F1 ? nk1 : nk)) continue;
         const float2 z = sm[rr * RS + FM::kpos(m)];
         const float2 y = make_float2(z.x * inv, -z.y * inv);
         const float2 rot = fc_rotator(chains[c], (k_begin + kk) * (int64_t)D);
@@ -655,16 +663,20 @@ hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
     return hipGetLastError();
 }
 
-// frames per block F = ceil(nk / V); U: [M][Fs][Dp], Y: [nchains][Fs][M], out: [nchains][nk]
+// frames per block F = ceil(nk / V); U: [M][Fs][Dp], Y: [nchains][Fs][M], out: [nchains][nk].
+// A pair of caller blocks: the first's nk1 outputs (input up to blk_end1) in ceil(nk1 / V)
+// frames, the second's in their own; one GEMM over both (W read once for the two blocks).
 hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
-                         const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
+                         int64_t blk_end1, int nk1, const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
                          hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form) {
-    const int F = (nk + V - 1) / V;
+    if (nk1 < 0 || nk1 > nk) return hipErrorInvalidValue;
+    const int F1 = (nk1 + V - 1) / V;
+    const int F = F1 + (nk - nk1 + V - 1) / V;
     if (F > Fs || nk <= 0 || nchains <= 0) return hipErrorInvalidValue;
     const dim3 gf(Dp / kFcRT, F);
-#define OWRX_FC_F(MM) hipLaunchKernelGGL(fc_fwd<MM>, gf, dim3(256), 0, st, blk, blk_start, blk_end, k_begin, V, D, Dp, Fs, tw, U)
+#define OWRX_FC_F(MM) hipLaunchKernelGGL(fc_fwd<MM>, gf, dim3(256), 0, st, blk, blk_start, blk_end, blk_end1, k_begin, nk1, F1, V, D, Dp, Fs, tw, U)
     OWRX_FC_SWITCH(M, OWRX_FC_F)
 #undef OWRX_FC_F
     HIPCHK_RET(hipGetLastError());
@@ -718,7 +730,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
     if (mac1) HIPCHK_RET(hipEventRecord(mac1, st));
     const int rw = (M % 3 == 0) ? 3072 / M : 1024 / M;
     const dim3 go((nchains * F + rw - 1) / rw);
-#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, tw, out, ring ? ks : 1, y_slice)
+#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, nk1, F1, tw, out, ring ? ks : 1, y_slice)
     OWRX_FC_SWITCH(M, OWRX_FC_O)
 #undef OWRX_FC_O
     return hipGetLastError();

@@ -123,6 +123,12 @@ class Engine:
         resident recording): the host may then run that many blocks ahead of the GPU."""
         check(lib.owrx_set_input_retention(self._h, int(blocks)), "owrx_set_input_retention")
 
+    def set_block_pairing(self, enable=True):
+        """Run contiguous process_device blocks two at a time (owrx_set_block_pairing; input
+        retention >= 4, before the first chain, waterfall and block): outputs byte-identical,
+        one block more latency."""
+        check(lib.owrx_set_block_pairing(self._h, 1 if enable else 0), "owrx_set_block_pairing")
+
     def set_pipeline_depth(self, blocks):
         """Blocks of chain work in flight (1..16, default 8), before the first chain and block."""
         check(lib.owrx_set_pipeline_depth(self._h, int(blocks)), "owrx_set_pipeline_depth")

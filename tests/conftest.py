@@ -13,6 +13,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run on the MI355X box)")
 
 
+def pytest_collection_modifyitems(config, items):
+    # torch bundles its own HIP runtime under the same soname as the engine's (/opt/rocm): the
+    # first one loaded serves both, and torch does not initialise on ROCm 7.2's.  GPU tests use
+    # torch for device buffers, so it loads before any test loads libowrx_amd.so.
+    if any(item.get_closest_marker("gpu") for item in items):
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN

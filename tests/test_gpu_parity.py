@@ -517,6 +517,70 @@ def test_input_retention_same_outputs(amd):
     assert all(len(x) > 0 for x in a[0]) and len(a[2]) > 0
 
 
+@pytest.mark.parametrize("fs,modes,B", [
+    (2400000, ["nfm", "usb", "am", "cw"] * 3, 1 << 17),
+    (10000000, ["nfm", "usb", "cw"] * 4, 1 << 18),  # C3's design: D = 833, fast convolution
+])
+def test_block_pairing_same_outputs(amd, fs, modes, B):
+    """owrx_set_block_pairing: contiguous blocks run two at a time (one DDC GEMM over both
+    blocks' frames); audio, s-meter and waterfall rows byte-identical to unpaired processing.
+    An odd block count (owrx_sync runs the held block), a block from another buffer (the held one
+    runs alone) and a chain created mid-stream (the guard runs the held block first)."""
+    import torch
+    from openwebrx_amd import synth
+    # blocks: 0+1 and 2+3 paired, 4 alone (chain created after it), 5 alone (6 is from another
+    # buffer), 6 alone, 7+8, 9+10 paired, 11 held until owrx_sync
+    nb = 12
+    iq, offs = synth.make_iq(fs, nb * B, modes)
+    plist = [amd.params.chain_params(fs, o, m) for o, m in zip(offs, modes)]
+    N = 4096
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+
+    def run(pair):
+        eng = amd.Engine(fs, max_block=B)
+        eng.set_input_retention(8)
+        if pair:
+            eng.set_block_pairing(True)
+        wf = eng.waterfall(N, hop, avg, adpcm=True)
+        chains = [eng.chain(p) for p in plist[:-1]]
+        h = eng.history
+        buf = torch.zeros(h + iq.size, dtype=torch.complex64, device="cuda")
+        buf[h:] = torch.from_numpy(iq).to("cuda")
+        # block 6 from a copy of the stream (same samples and history, another address)
+        alt = buf[6 * B:h + 7 * B].clone()
+        torch.cuda.synchronize()
+        for k in range(nb):
+            if k == 5:
+                chains.append(eng.chain(plist[-1]))
+            ptr = alt.data_ptr() + 8 * h if k == 6 else buf.data_ptr() + 8 * (h + k * B)
+            eng.process_device(ptr, B)
+        eng.sync()
+        st = eng.stats()
+        out = ([c.read_audio() for c in chains], [c.read_smeter().tobytes() for c in chains],
+               wf.read())
+        eng.close()
+        return out, st
+
+    (a, sa), (b, sb) = run(False), run(True)
+    assert sa["blocks"] == nb and sb["blocks"] == nb - 4  # four pairs
+    assert all(len(x) > 0 for x in a[0]) and len(a[2]) > 0
+    for i in range(len(a[0])):
+        assert a[0][i] == b[0][i] and a[1][i] == b[1][i], i
+    assert a[2] == b[2]
+
+
+def test_block_pairing_rejects_bad_state(amd):
+    """Pairing needs input retention >= 4 and an engine with no chain, waterfall or block yet."""
+    eng = amd.Engine(2400000, max_block=1 << 16)
+    with pytest.raises(Exception):
+        eng.set_block_pairing(True)  # retention 1
+    eng.set_input_retention(4)
+    eng.chain(amd.params.chain_params(2400000, 100000, "nfm"))
+    with pytest.raises(Exception):
+        eng.set_block_pairing(True)  # a chain exists
+    eng.close()
+
+
 def test_engine_ring_ingest_commit(amd):
     """The caller-written ring slot (owrx_ingest_buffer / owrx_commit, e.g. an RCCL broadcast)
     gives the same rows as owrx_push_iq through the ring's wraps."""
