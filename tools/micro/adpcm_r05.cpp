@@ -1,0 +1,191 @@
+// IMA-ADPCM serial encoder microbenchmark, round 5 (diagnostic; not part of the product):
+// cycles per sample of the production byte-addressed successor table (adpcm_encode_tab2)
+// against a successor table whose 64-B records carry the successor step's compare thresholds
+// (step, h, step + h, q, h + q, step + q, step + h + q) and dq terms, so that after a record
+// arrives the magnitude needs three compares and two selects and no subtractions.  One lane per
+// stream, 64 streams x 5000 samples; the codes of both encoders are compared.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 adpcm_r05.cpp -o adpcm_r05
+#include "../../openwebrx_amd/csrc/owrx_dev.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+using namespace owrx;
+
+constexpr int kThRec = 64;                 // bytes per record
+constexpr int kThEntries = 89 * 8;         // (index, magnitude) -> the successor's record
+
+struct ThState {
+    uint32_t T4, T2, T6, T1, T3, T5, T7, S3, S3mQ, row;  // row: byte offset of TH[index][0]
+    int pred;
+};
+
+__device__ void th_rec(uint32_t* r, int ni) {
+    const uint32_t st = (uint32_t)kAdpcmStep[ni], h = st >> 1, q = st >> 2, s3 = st >> 3;
+    r[0] = st; r[1] = h; r[2] = st + h; r[3] = q;
+    r[4] = h + q; r[5] = st + q; r[6] = st + h + q; r[7] = s3;
+    r[8] = s3 - q; r[9] = (uint32_t)(ni * 8 * kThRec);
+}
+
+__device__ void th_fill(uint32_t* TH, int tid, int nt) {
+    for (int e = tid; e < kThEntries; e += nt) {
+        const int i = e >> 3, m = e & 7;
+        int ni = i + kAdpcmIndex[m];
+        ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
+        th_rec(TH + e * (kThRec / 4), ni);
+    }
+}
+
+__device__ ThState th_state(int index, int pred) {
+    uint32_t r[10];
+    th_rec(r, index);
+    return ThState{r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[9], pred};
+}
+
+__device__ __forceinline__ int th_encode(ThState& s, int x, const uint32_t* TH) {
+    const int d = x - s.pred;
+    const int sgn = d >> 31;
+    const int a0 = max(d, -d);
+    const bool m4 = a0 >= (int)s.T4;
+    const int t2 = m4 ? (int)s.T6 : (int)s.T2;
+    const uint32_t r4 = m4 ? s.row + 4 * kThRec : s.row;
+    const int t1a = m4 ? (int)s.T5 : (int)s.T1;
+    const int t1b = m4 ? (int)s.T7 : (int)s.T3;
+    const bool m2 = a0 >= t2;
+    const int t1 = m2 ? t1b : t1a;
+    const uint32_t r42 = m2 ? r4 + 2 * kThRec : r4;
+    const bool m1 = a0 >= t1;
+    const uint32_t addr = m1 ? r42 + kThRec : r42;
+    const char* base = reinterpret_cast<const char*>(TH) + addr;
+    const uint4 q0 = *reinterpret_cast<const uint4*>(base);
+    const uint4 q1 = *reinterpret_cast<const uint4*>(base + 16);
+    const uint2 q2 = *reinterpret_cast<const uint2*>(base + 32);
+    const int dq = t1 + (int)(m1 ? s.S3 : s.S3mQ);
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    const int code = (int)((addr - s.row) / kThRec) | (sgn & 8);
+    s.T4 = q0.x; s.T2 = q0.y; s.T6 = q0.z; s.T1 = q0.w;
+    s.T3 = q1.x; s.T5 = q1.y; s.T7 = q1.z; s.S3 = q1.w;
+    s.S3mQ = q2.x; s.row = q2.y;
+    return code;
+}
+
+// V == 2: the index in a register, the step fetched across lanes (ds_bpermute) from two VGPRs
+// holding STEP[-1 .. 62] and STEP[63 .. 96] (ends clamped), so the index's clamp is off the path
+struct BpState {
+    int idx, step, pred;
+};
+
+__device__ __forceinline__ int bp_encode(BpState& s, int x, int tabA, int tabB) {
+    const int d = x - s.pred;
+    const int sgn = d >> 31;
+    const int a0 = max(d, -d);
+    const int step = s.step, h = step >> 1, q = step >> 2, s3 = step >> 3;
+    const bool m4 = a0 >= step;
+    const int a1 = m4 ? a0 - step : a0;
+    const bool m2 = a1 >= h;
+    const int a2 = m2 ? a1 - h : a1;
+    const bool m1 = a2 >= q;
+    const int nb = s.idx + (m4 ? (m2 ? 6 : 2) : -1);
+    const int nr = nb + ((m4 && m1) ? 2 : 0);  // -1 .. 96
+    const int slot = nr + 1;                    // 0 .. 97: tabA lanes 0..63, tabB lanes 0..33
+    const int va = __builtin_amdgcn_ds_bpermute((slot & 63) << 2, tabA);
+    const int vb = __builtin_amdgcn_ds_bpermute((slot & 63) << 2, tabB);
+    s.step = slot >= 64 ? vb : va;
+    s.idx = min(max(nr, 0), 88);
+    const int dq = s3 + (m4 ? step : 0) + (m2 ? h : 0) + (m1 ? q : 0);
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    return (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0) | (sgn & 8);
+}
+
+template <int V>
+__global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n, uint8_t* __restrict__ out,
+                                           long long* cyc) {
+    __shared__ __align__(16) uint32_t NS[V == 0 ? kAdpcmTab2Entries : kThEntries * (kThRec / 4)];
+    if constexpr (V == 0) adpcm_tab2_fill(NS, threadIdx.x, 64);
+    else th_fill(NS, threadIdx.x, 64);
+    __syncthreads();
+    const int lane = threadIdx.x;
+    const int16_t* src = x + (size_t)lane * (n + 16);
+    uint8_t* o = out + (size_t)lane * n;
+    auto ad2 = adpcm_tab2_state(AdpcmState{0, 0});
+    ThState th = th_state(0, 0);
+    BpState bp{0, kAdpcmStep[0], 0};
+    const int la = lane - 1, lb = lane + 63;
+    const int tabA = kAdpcmStep[la < 0 ? 0 : la];
+    const int tabB = kAdpcmStep[lb > 88 ? 88 : lb];
+    int cur[8], nxt[8];
+    for (int q = 0; q < 8; ++q) cur[q] = src[q];
+    const long long t0 = clock64();
+    for (int j = 0; j < n; j += 8) {
+        for (int q = 0; q < 8; ++q) nxt[q] = src[j + 8 + q];
+        uint32_t w = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            int c;
+            if constexpr (V == 0) c = adpcm_encode_tab2(ad2, cur[u], NS);
+            else if constexpr (V == 1) c = th_encode(th, cur[u], NS);
+            else c = bp_encode(bp, cur[u], tabA, tabB);
+            w |= (uint32_t)c << (4 * u);
+        }
+        *reinterpret_cast<uint32_t*>(o + (j >> 1)) = w;
+        for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+    }
+    const long long t1 = clock64();
+    if (lane == 0) *cyc = t1 - t0;
+}
+
+int main() {
+    const int S = 64, n = 5000;
+    std::vector<int16_t> h((size_t)S * (n + 16));
+    srand(3);
+    for (int c = 0; c < S; ++c) {
+        double y = 0, amp = 2000 + 15000.0 * (c % 7) / 6.0;
+        for (int i = 0; i < n + 16; ++i) {
+            y = 0.9 * y + (rand() / (double)RAND_MAX - 0.5);
+            double v = amp * (0.6 * sin(0.05 * i * (1 + c % 11) + c) + 0.25 * y);
+            if (c % 3 == 0) v = (rand() % 65536) - 32768;  // full-scale noise: large steps
+            v = v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
+            h[(size_t)c * (n + 16) + i] = (int16_t)v;
+        }
+    }
+    int16_t* dx;
+    uint8_t *d0, *d1;
+    long long* dc;
+    hipMalloc(&dx, h.size() * 2);
+    hipMemcpy(dx, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+    hipMalloc(&d0, (size_t)S * n);
+    hipMalloc(&d1, (size_t)S * n);
+    hipMalloc(&dc, 8);
+    auto run = [&](const char* name, void (*k)(const int16_t*, int, uint8_t*, long long*), uint8_t* o) {
+        long long cyc = 0;
+        for (int rep = 0; rep < 5; ++rep) {
+            hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, dx, n, o, dc);
+            hipDeviceSynchronize();
+        }
+        hipMemcpy(&cyc, dc, 8, hipMemcpyDeviceToHost);
+        printf("%-44s %7.1f cycles/sample (%s)\n", name, cyc / (double)n, hipGetErrorString(hipGetLastError()));
+    };
+    run("tab2 (production chain_adpcm encoder)", kern<0>, d0);
+    run("threshold records (64 B successor records)", kern<1>, d1);
+    uint8_t* d2;
+    hipMalloc(&d2, (size_t)S * n);
+    run("index register + ds_bpermute step", kern<2>, d2);
+    std::vector<uint8_t> a((size_t)S * n / 2 * 2), b(a.size());
+    hipMemcpy(a.data(), d0, a.size(), hipMemcpyDeviceToHost);
+    hipMemcpy(b.data(), d1, b.size(), hipMemcpyDeviceToHost);
+    size_t diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    hipMemcpy(b.data(), d2, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("bpermute codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    return 0;
+}
