@@ -111,7 +111,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
                          int64_t blk_end1, int nk1, const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
-                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form);
+                         int ncu, hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form);
 int fc_kslices_max(int M, int nchains, int Dp, int ncu);  // Y slices a group may need
 hipError_t launch_post_parallel(const ChainPost* posts, int nchains, ChainCounts* counts,
                                 const StepTable& steps, hipStream_t st);
@@ -2121,7 +2121,8 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t s
                                  g->d_chains, g->d_fc_w,
                                  g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
                                  g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
-                                 g->d_fc_y, (int64_t)g->fc_y_elems, g->d_partial[si], e->sA,
+                                 g->d_fc_y, (int64_t)g->fc_y_elems, g->d_partial[si],
+                                 std::max(1, e->cus_a), e->sA,
                                  tm ? S.m0 : nullptr,
                                  tm ? S.m1 : nullptr, &form));
             if (form > 0) e->stats.ddc_mac_lds_launches++;

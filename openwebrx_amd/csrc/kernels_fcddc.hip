@@ -623,10 +623,11 @@ int fc_kslices(int tiles, int Dp, int ncu) {
     const int per_wave = (Dp >> 3) / kFcKSplit;  // K-blocks per wave, unsliced
     auto ok = [&](int k) { return k >= 1 && k <= kFcMaxKSlices && per_wave % k == 0; };
     if (forced > 0) return ok(forced) ? forced : 1;
-    // a grid that already covers the CUs once keeps whole K: C3's 384 tiles on 228 CUs ran 0.53
+    // a grid that already covers the CUs twice keeps whole K: C3's 384 tiles on 228 CUs ran 0.53
     // of HBM unsliced vs 0.51 with 3 slices (profiles/r04_fc_kslices_c3.txt); C4's 128 and C5's
-    // 64 tiles gain 0.32 -> 0.48 and 0.25 -> 0.36 from slicing
-    if (tiles >= ncu) return 1;
+    // 64 tiles gain 0.32 -> 0.48 and 0.25 -> 0.36 from slicing, and a paired C5 GEMM's 256 tiles
+    // (1.1 per CU) 0.26 -> 0.33 with 3 slices (profiles/r05_c5_kslices.txt)
+    if (tiles >= 2 * ncu) return 1;
     int best = 1;
     for (int k = 2; k <= kFcMaxKSlices; ++k) {
         if (!ok(k)) continue;
@@ -670,7 +671,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
                          int64_t blk_end1, int nk1, const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
-                         hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form) {
+                         int ncu, hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form) {
     if (nk1 < 0 || nk1 > nk) return hipErrorInvalidValue;
     const int F1 = (nk1 + V - 1) / V;
     const int F = F1 + (nk - nk1 + V - 1) / V;
@@ -701,14 +702,10 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
     }();
     // the ring where the grid needs two or more workgroups per CU (C3: 512); a grid one round of
     // single workgroups holds (C4's per-GPU share: 128, long K) keeps register operands, which
-    // measured 6 % faster there than the ring at 2 or 4 slots (profiles/r03ap_ab_fc_mac_c4.txt)
-    static const int ncu = [] {
-        int d = 0, n = 0;
-        if (hipGetDevice(&d) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-            return 256;
-        return n;
-    }();
+    // measured 6 % faster there than the ring at 2 or 4 slots (profiles/r03ap_ab_fc_mac_c4.txt).
+    // ncu: the CUs of the launching stream (stream A's mask, not the device's 256: a paired C5
+    // GEMM's 256 workgroups took the register form and two rounds on A's 228 CUs)
+    ncu = ncu > 0 ? ncu : 256;
     // K slices across workgroups where the tile grid leaves CUs idle (fc_kslices)
     const int64_t y_slice = (int64_t)nchains * Fs * M;
     int ks = lds_ring ? fc_kslices((int)gm.x, Dp, ncu) : 1;
