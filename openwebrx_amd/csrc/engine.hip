@@ -2438,19 +2438,29 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
         return OWRX_EIO;
     };
     if (create_streams(e) != hipSuccess) return fail("stream");
+    // Events that only order streams of this device (A -> B, B -> C, C -> R, A -> row queue) and
+    // the input-retention poll (the host learns that stream A finished reading; it reads no data
+    // through them) release at device scope; evB and the row slots' evC, after which the host
+    // reads what the GPU wrote into pinned memory, keep the system-scope release.
+    // OWRX_EVENT_FENCE=system: every event system-scope (A/B).
+    static const unsigned dev_fence = [] {
+        const char* v = getenv("OWRX_EVENT_FENCE");
+        return (v && strcmp(v, "system") == 0) ? (unsigned)hipEventDisableTiming
+                                               : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
+    }();
     if (hipEventCreateWithFlags(&e->evSync, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e->evExt, hipEventDisableTiming) != hipSuccess)
         return fail("event");
     for (auto& r : e->rslots) {
-        if (hipEventCreateWithFlags(&r.evWf, hipEventDisableTiming) != hipSuccess ||
+        if (hipEventCreateWithFlags(&r.evWf, dev_fence) != hipSuccess ||
             hipEventCreateWithFlags(&r.evC, hipEventDisableTiming) != hipSuccess)
             return fail("row stream");
     }
     for (auto& s : e->slots) {
-        if (hipEventCreateWithFlags(&s.evA, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s.evF, hipEventDisableTiming) != hipSuccess ||
+        if (hipEventCreateWithFlags(&s.evA, dev_fence) != hipSuccess ||
+            hipEventCreateWithFlags(&s.evF, dev_fence) != hipSuccess ||
             hipEventCreateWithFlags(&s.evB, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&s.evC, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&s.evC, dev_fence) != hipSuccess ||
             // timing-only events: no system-scope fence, so the markers bracketing a kernel
             // do not add cache write-backs to the interval they measure
             hipEventCreateWithFlags(&s.a0, hipEventDisableSystemFence) != hipSuccess ||
@@ -2473,7 +2483,7 @@ int owrx_engine_create_ex(int device, double samp_rate, int64_t max_block, int64
     e->wp = e->history;
     if (halloc(&e->h_in, 4 * (size_t)max_block) != hipSuccess) return fail("pinned input");
     for (hipEvent_t& ev : e->evIn)
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail("event");
+        if (hipEventCreateWithFlags(&ev, dev_fence) != hipSuccess) return fail("event");
     *out = e;
     return OWRX_OK;
 }
