@@ -853,6 +853,12 @@ def main():
     wf = None
     if rank == 0 and not args.no_waterfall:
         wf = eng.waterfall(n_fft, hop, avg, adpcm=True)
+        # two whole rounds of the FFT launch where the engine deals it in rounds (16384 bins:
+        # stream A's resident workgroups x 8 frames; no idle last round and no tail split,
+        # profiles/r05_wf_tail_batch_ab.txt); the history above was sized for the larger default
+        rnd = wf.round_frames()
+        if wf_batch > 1 and args.wf_batch < 0 and rnd > 0 and 2 * rnd <= wf_batch:
+            wf_batch = 2 * rnd
         if wf_batch > 1:
             wf.set_batch(wf_batch)
             wf.set_latency(args.wf_latency_ms)

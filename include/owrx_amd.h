@@ -176,6 +176,10 @@ int owrx_waterfall_set_batch(owrx_engine* e, int handle, int min_frames, int64_t
 int owrx_waterfall_set_latency(owrx_engine* e, int handle, double max_wall_ms);
 int owrx_waterfall_destroy(owrx_engine* e, int handle);
 /* bytes of one output row: (fft_size+10)/2 with ADPCM, 4*fft_size without */
+/* Frames one full round of this waterfall's FFT launch deals (stream A's resident workgroups x
+ * frames per group; 0 where launches are not dealt in rounds): a caller that batches frames
+ * (owrx_waterfall_set_batch) in whole rounds leaves no partial last round. */
+int owrx_waterfall_round_frames(owrx_engine* e, int handle);
 int64_t owrx_waterfall_row_bytes(owrx_engine* e, int handle);
 /* copies whole rows (<= max_bytes) from the row ring; 0 when none; Reader.read() of the
  * spectrum buffer (owrx/fft.py:70-73) */

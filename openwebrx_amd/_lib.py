@@ -155,6 +155,7 @@ PROTOTYPES = {
     "owrx_selftest_w_layout": (_i32, [_i32, _i32]),
     "owrx_waterfall_destroy": (_i32, [_vp, _i32]),
     "owrx_waterfall_row_bytes": (_i64, [_vp, _i32]),
+    "owrx_waterfall_round_frames": (_i32, [_vp, _i32]),
     "owrx_waterfall_read": (_i64, [_vp, _i32, _vp, _i64]),
     "owrx_chain_create": (_i32, [_vp, ctypes.POINTER(ChainParams), _pi32]),
     "owrx_chain_destroy": (_i32, [_vp, _i32]),

@@ -84,7 +84,8 @@ hipError_t launch_wf_fft(int logn, const float2* blk, int64_t blk_start, const W
                          int ngroups, int fpg, const float* window, const float* ones,
                          const float2* tw, float* partial, float2* scratch, int* work, int cus,
                          hipStream_t st, int skip, int tail);
-int wf_tail_split(int logn, int ngroups, int cus);
+int wf_tail_split(int logn, int ngroups, int cus, int64_t frames, int fpg);
+int wf_round_frames(int logn, int cus, int fpg);  // frames one full round of a launch deals
 bool wf_uses_split(int logn);  // kernels_waterfall.hip: N = 32768 / 65536 via the DIF split
 bool wf_uses_l32(int logn);  // kernels_waterfall.hip: N = 16384 on wf_fft_q16 / l32 (not r16)
 int wf_default_fpg(int logn);
@@ -1396,7 +1397,7 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
     if (need > g->partial_elems) {
         RCCHK(drain_all(e));
         const size_t alloc = need + need / 2;
-        for (int i = 0; i < kSlots; ++i) {
+        for (int i = 0; i < e->nslots; ++i) {  // the depth is fixed before the first chain
             dfree(g->d_partial[i]);
             HIPCHK(dalloc(&g->d_partial[i], alloc));
         }
@@ -1621,7 +1622,7 @@ static int process_waterfall(owrx_engine* e, Waterfall* w, const float2* blk, in
     // tail split (wf_fft_l32): the last `skip` groups are also listed frame by frame after the
     // groups, and the kernel deals those frames instead (the rows do not change)
     const int ngroups = (int)w->groups.size();
-    const int skip = wf_tail_split(w->logn, ngroups, std::max(1, e->cus_a));
+    const int skip = wf_tail_split(w->logn, ngroups, std::max(1, e->cus_a), nfr, w->fpg);
     int tail = 0;
     for (int gi = ngroups - skip; gi < ngroups; ++gi) {
         const WfGroup g = w->groups[gi];
@@ -2782,6 +2783,15 @@ int owrx_sync(owrx_engine* e) {
     return OWRX_OK;
 }
 
+// Chains per DDC group (see owrx_chain_create); OWRX_GROUP_CAP overrides (A/B).
+static int group_cap() {
+    static const int v = [] {
+        const char* s = getenv("OWRX_GROUP_CAP");
+        return s ? std::max(1, atoi(s)) : 16384;
+    }();
+    return v;
+}
+
 // ---- waterfall --------------------------------------------------------------------------
 
 int owrx_waterfall_create(owrx_engine* e, int fft_size, int every_n_samples, int avg_number,
@@ -2907,6 +2917,13 @@ int owrx_waterfall_destroy(owrx_engine* e, int handle) {
     return OWRX_OK;
 }
 
+int owrx_waterfall_round_frames(owrx_engine* e, int handle) {
+    ENGINE_GUARD_HELD(e);
+    auto it = e->wfs.find(handle);
+    if (it == e->wfs.end()) return OWRX_EINVAL;
+    return wf_round_frames(it->second->logn, std::max(1, e->cus_a), it->second->fpg);
+}
+
 int64_t owrx_waterfall_row_bytes(owrx_engine* e, int handle) {
     ENGINE_GUARD_HELD(e);
     auto it = e->wfs.find(handle);
@@ -3017,9 +3034,16 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     uint32_t tb, cb;
     memcpy(&tb, &p->transition, 4);
     memcpy(&cb, &p->cutoff, 4);
+    // A group holds at most group_cap() chains; past that the design opens another group.  The
+    // filter spectra W of a group double as it grows and a regrown W returns to the engine's
+    // exact-size pool, so one unbounded group kept every earlier capacity allocated (131 072
+    // chains: ~115 GB of dead spectra) and needed old + new W at once; bounded groups grow
+    // through the same sizes, reusing each other's pooled buffers (tools/dbg/mem_per_chain.py)
     ChainGroup* g = nullptr;
     for (auto& gp : e->groups)
-        if (gp->D == D && gp->tbw_bits == tb && gp->cutoff_bits == cb) g = gp.get();
+        if (gp->D == D && gp->tbw_bits == tb && gp->cutoff_bits == cb &&
+            (int)gp->members.size() < group_cap())
+            g = gp.get();
     const int64_t aligned = ((e->pos + D - 1) / D) * D;
     if (!g) {
         auto ng = std::make_unique<ChainGroup>();

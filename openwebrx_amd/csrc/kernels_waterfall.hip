@@ -1561,16 +1561,31 @@ static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfG
 // share), so a launch of one item per CU ran its last items in a second round, doubling its time
 // (89 vs 52 us per 960 C3 frames); the groups that would start a partial last round, plus a
 // 16th of a round, are dealt as single frames instead.  0 for the other kernels.
-int wf_tail_split(int logn, int ngroups, int cus) {
+// the workgroups a masked queue holds at once: ~15/16 of its CUs (measured 227-230 of 240)
+static int wf_held(int cus) { return cus - cus / 16; }
+
+int wf_round_frames(int logn, int cus, int fpg) {
+    return logn == 14 && wf_n16k_kernel() != 2 ? wf_held(cus) * std::max(1, fpg) : 0;
+}
+
+int wf_tail_split(int logn, int ngroups, int cus, int64_t frames, int fpg) {
     if (logn != 14 || wf_n16k_kernel() == 2 || cus < 8 || ngroups < 2) return 0;
     static const int mode = [] {
         const char* s = getenv("OWRX_WF_TAIL");
         return s ? atoi(s) : -1;
     }();
     if (mode == 0) return 0;
-    // the workgroups a masked queue holds at once: ~15/16 of its CUs (measured 227-230 of 240);
-    // the groups past the last full round of those, plus a 16th of a round, go frame by frame
-    const int held = cus - cus / 16;
+    // the groups past the last full round of the held workgroups, plus a 16th of a round, go
+    // frame by frame.  A launch whose frames end within an eighth of a round of a whole number of
+    // rounds keeps its groups whole: its last round is nearly full, and the split's per-frame
+    // partial rows (wf_finalize reads them all back) cost more than the idle tail (3 480 frames
+    // in situ at C3: 0.245 of HBM whole vs 0.22 split; 3 848 frames: 0.206 whole vs 0.233 split,
+    // profiles/r05_wf_tail_batch_ab.txt)
+    const int held = wf_held(cus);
+    if (mode < 0 && frames > 0 && fpg > 0) {
+        const double r = (double)frames / ((double)held * fpg);
+        if (r >= 1.0 && r - std::floor(r) < 0.125) return 0;
+    }
     const int lo = held - cus / 16;
     if (ngroups <= lo) return 0;
     const int s = ngroups <= held ? ngroups - lo : ngroups % held + cus / 16;

@@ -225,6 +225,10 @@ class Waterfall:
     def row_bytes(self):
         return check(lib.owrx_waterfall_row_bytes(self.engine.handle, self.id), "row_bytes")
 
+    def round_frames(self):
+        """Frames one full round of the FFT launch deals (owrx_waterfall_round_frames; 0: n/a)."""
+        return check(lib.owrx_waterfall_round_frames(self.engine.handle, self.id), "round_frames")
+
     def read(self, max_bytes=None):
         """Whole rows produced so far (or at most max_bytes worth of rows)."""
         rb = self.row_bytes()
