@@ -32,11 +32,11 @@ for st in "$@"; do
         eval env $envs timeout -k 10 300 python -u bench.py $SHORT --extra-block 0 ${BARGS} > gpurun_out/${TAG}_ab_${v//[=,+.\/]/_}.json 2> gpurun_out/${TAG}_ab_${v//[=,+.\/]/_}.err || exit $?
       done ;;
     prof) eval timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o bench \
-        -- python3 -u bench.py $SHORT --steps 20 --warmup 10 ${BARGS} > gpurun_out/${TAG}_prof.json 2> gpurun_out/${TAG}_prof.log || exit $? ;;
+        -- python3 -u bench.py $SHORT --steps 20 --warmup 5 --extra-block 0 ${BARGS} > gpurun_out/${TAG}_prof.json 2> gpurun_out/${TAG}_prof.log || exit $? ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         eval timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_${CFG}_$c -o pmc \
-          -- python3 -u bench.py $SHORT --steps 5 --warmup 3 --no-timing --extra-block 0 ${BARGS} > gpurun_out/${TAG}_pmc_${CFG}_$c.log 2>&1 || exit $?
+          -- python3 -u bench.py $SHORT --steps 20 --warmup 5 --no-timing --extra-block 0 ${BARGS} > gpurun_out/${TAG}_pmc_${CFG}_$c.log 2>&1 || exit $?
       done ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac

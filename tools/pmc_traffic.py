@@ -15,6 +15,9 @@ import os
 import sys
 
 tag, config, fdir, wdir = sys.argv[1:5]
+# per kernel and counter: (grid size, value) of every dispatch; a kernel's figure is the mean over
+# its dispatches at its largest grid (full launches: a batched waterfall's owrx_sync flush is a
+# smaller launch of the same kernel and would pull an all-dispatch mean down)
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in (fdir, wdir):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -23,17 +26,29 @@ for d in (fdir, wdir):
             if "owrx::" not in name:
                 continue
             short = name.split("(")[0].replace("void ", "").replace("owrx::", "")
-            vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            vals[short][r["Counter_Name"]].append((int(r.get("Grid_Size") or 0), float(r["Counter_Value"])))
+
+
+def full(pairs):
+    if not pairs:
+        return []
+    g = max(p[0] for p in pairs)
+    return [v for gs, v in pairs if gs == g]
 out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
-                 "'python bench.py --config %s --steps 5 --warmup 3 --no-cpu-baseline --no-timing'" % config,
+                 "'python bench.py --config %s --steps 20 --warmup 5 --no-cpu-baseline --no-timing "
+                 "--extra-block 0' (tools/gpu_steps.sh pmc); per kernel the dispatches at its largest "
+                 "grid" % config,
        "config": config,
        "correction": "fetch_bytes = 2 x FETCH_SIZE (gfx950), write_bytes = WRITE_SIZE",
        "kernels": {}}
 for k, cs in sorted(vals.items()):
-    f = sum(cs["FETCH_SIZE"]) / max(1, len(cs["FETCH_SIZE"]))
-    w = sum(cs["WRITE_SIZE"]) / max(1, len(cs["WRITE_SIZE"]))
+    fv, wv = full(cs["FETCH_SIZE"]), full(cs["WRITE_SIZE"])
+    f = sum(fv) / max(1, len(fv))
+    w = sum(wv) / max(1, len(wv))
     out["kernels"][k] = {"fetch_size_kb": round(f, 1), "write_size_kb": round(w, 1),
-                         "hbm_bytes_per_launch": int(round((2 * f + w) * 1024))}
+                         "hbm_bytes_per_launch": int(round((2 * f + w) * 1024)),
+                         "dispatches": [len(fv), len(wv)],
+                         "grid": max(p[0] for p in cs["FETCH_SIZE"]) if cs["FETCH_SIZE"] else None}
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                     "%s_pmc_traffic_%s.json" % (tag, config))
 json.dump(out, open(path, "w"), indent=1)
