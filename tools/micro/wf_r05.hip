@@ -335,17 +335,17 @@ int main(int argc, char** argv) {
                 fflush(stdout);
             }
 #ifdef OWRX_WF_WSTAMPS
-            for (int abl : {0, 1, 72, 8}) {
+            for (int abl : {72, 0}) {
                 time_us([&] { q16(0, 0, abl); }, s_a);
-                std::vector<unsigned long long> st((size_t)256 * 16 * 8);
+                std::vector<unsigned long long> st((size_t)256 * 16 * 12);
                 CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wf_wstamp), sizeof(unsigned long long) * st.size()));
                 const int nwg = std::min(G, cus);
-                auto at = [&](int g, int w, int i) { return (long long)st[((size_t)g * 16 + w) * 8 + i]; };
-                std::vector<long long> mn[8], mx[8];
+                auto at = [&](int g, int w, int i) { return (long long)st[((size_t)g * 16 + w) * 12 + i]; };
+                std::vector<long long> mn[12], mx[12];
                 for (int g = 0; g < nwg; ++g) {
                     long long t0 = at(g, 0, 0);
                     for (int w = 0; w < 16; ++w) t0 = std::min(t0, at(g, w, 0));
-                    for (int i = 0; i < 8; ++i) {
+                    for (int i = 0; i < 11; ++i) {
                         long long a = 1LL << 60, b = 0;
                         for (int w = 0; w < 16; ++w) {
                             a = std::min(a, at(g, w, i) - t0);
@@ -355,10 +355,11 @@ int main(int argc, char** argv) {
                         mx[i].push_back(b);
                     }
                 }
-                const char* nm[] = {"frame start", "data arrived", "loads issued", "P1 done", "barrier 1 out",
-                                    "writes issued", "P2 start", "P3 start"};
+                const char* nm[] = {"frame start", "data arrived", "loads issued(early)", "P1 done", "barrier 1 out",
+                                    "ex1 writes issued", "barrier 2 out", "barrier 4 out", "loads issued(late)",
+                                    "P2 done", "P3 done"};
                 printf("   q16<%d> per-wave stamps, frame 2 (cycles from the first wave's frame start; median over workgroups of first / last wave):\n", abl);
-                for (int i = 0; i < 8; ++i) {
+                for (int i = 0; i < 11; ++i) {
                     std::sort(mn[i].begin(), mn[i].end());
                     std::sort(mx[i].begin(), mx[i].end());
                     printf("     %-14s %7lld %7lld\n", nm[i], mn[i][mn[i].size() / 2], mx[i][mx[i].size() / 2]);
