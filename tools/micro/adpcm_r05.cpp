@@ -102,11 +102,39 @@ __device__ __forceinline__ int bp_encode(BpState& s, int x, int tabA, int tabB) 
     return (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0) | (sgn & 8);
 }
 
+// V == 3: the production table (adpcm_tab2), but the row of 8 successor records for the
+// current (index, sign) is read (two ds_read_b128) as soon as the current record arrives, beside
+// the magnitude compares; the next record is then selected by m4, m2, m1 (three select levels)
+__device__ __forceinline__ int row_encode(AdpcmTab2& s, int x, const uint32_t* NS2) {
+    const int d = x - s.pred;
+    const int sgn = d >> 31;
+    const int a0 = max(d, -d);
+    const uint32_t rec = s.rec;
+    const int rb = (int)(rec >> 16) + (sgn & 32);
+    const uint4 q0 = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(NS2) + rb);
+    const uint4 q1 = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(NS2) + rb + 16);
+    const int step = (int)(rec & 0xffffu);
+    const int h = step >> 1, q = step >> 2, s3 = step >> 3;
+    const bool m4 = a0 >= step;
+    const int a1 = m4 ? a0 - step : a0;
+    const bool m2 = a1 >= h;
+    const int a2 = m2 ? a1 - h : a1;
+    const bool m1 = a2 >= q;
+    const int dq = s3 + (m4 ? step : 0) + (m2 ? h : 0) + (m1 ? q : 0);
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    const uint32_t e0 = m4 ? q1.x : q0.x, e1 = m4 ? q1.y : q0.y;
+    const uint32_t e2 = m4 ? q1.z : q0.z, e3 = m4 ? q1.w : q0.w;
+    const uint32_t f0 = m2 ? e2 : e0, f1 = m2 ? e3 : e1;
+    s.rec = m1 ? f1 : f0;
+    return (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0) | (sgn & 8);
+}
+
 template <int V>
 __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n, uint8_t* __restrict__ out,
                                            long long* cyc) {
-    __shared__ __align__(16) uint32_t NS[V == 0 ? kAdpcmTab2Entries : kThEntries * (kThRec / 4)];
-    if constexpr (V == 0) adpcm_tab2_fill(NS, threadIdx.x, 64);
+    __shared__ __align__(16) uint32_t NS[(V == 0 || V == 3) ? kAdpcmTab2Entries : kThEntries * (kThRec / 4)];
+    if constexpr (V == 0 || V == 3) adpcm_tab2_fill(NS, threadIdx.x, 64);
     else th_fill(NS, threadIdx.x, 64);
     __syncthreads();
     const int lane = threadIdx.x;
@@ -129,6 +157,7 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
             int c;
             if constexpr (V == 0) c = adpcm_encode_tab2(ad2, cur[u], NS);
             else if constexpr (V == 1) c = th_encode(th, cur[u], NS);
+            else if constexpr (V == 3) c = row_encode(ad2, cur[u], NS);
             else c = bp_encode(bp, cur[u], tabA, tabB);
             w |= (uint32_t)c << (4 * u);
         }
@@ -175,6 +204,9 @@ int main() {
     uint8_t* d2;
     hipMalloc(&d2, (size_t)S * n);
     run("index register + ds_bpermute step", kern<2>, d2);
+    uint8_t* d3;
+    hipMalloc(&d3, (size_t)S * n);
+    run("tab2 + successor row read beside the compares", kern<3>, d3);
     std::vector<uint8_t> a((size_t)S * n / 2 * 2), b(a.size());
     hipMemcpy(a.data(), d0, a.size(), hipMemcpyDeviceToHost);
     hipMemcpy(b.data(), d1, b.size(), hipMemcpyDeviceToHost);
@@ -187,5 +219,10 @@ int main() {
     for (int c = 0; c < S; ++c)
         for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
     printf("bpermute codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    hipMemcpy(b.data(), d3, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("row-prefetch codes differing: %zu of %d bytes\n", diff, S * n / 2);
     return 0;
 }
