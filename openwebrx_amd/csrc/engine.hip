@@ -25,6 +25,7 @@
 #include <deque>
 #include <map>
 #include <unordered_map>
+#include <unordered_set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -105,6 +106,9 @@ int fc_frame_supported(int m);  // kernels_fcddc.hip
 hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
                             uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st);
 hipError_t launch_fc_move_w(int M, float2* W, int64_t w_ks, int Dp, int src, int dst, hipStream_t st);
+hipError_t launch_fc_make_w_jobs(int m, const float* h, int T, int D, int Dp, int P,
+                                 const FcWJob* jobs, int njobs, float2* W, int64_t w_ks,
+                                 hipStream_t st);
 int64_t fc_w_chain_offset(int c, int Dp);  // chain c's first entry in a bin's row of the tiled W
 int fc_w_tile();                           // chains per W tile: capacities are multiples of it
 int fc_w_layout_check(int Dp, int cap);    // host self-test of the tiled W layout
@@ -373,6 +377,7 @@ struct ChainGroup {
     // destroyed member's slot is refilled by the last member's)
     float2* d_fc_w = nullptr;
     int fc_w_cap = 0;             // slots
+    std::vector<FcWJob> w_pending;  // joins' spectra builds not yet launched (flush_uploads)
     int64_t fc_w_ks() const { return (int64_t)fc_w_cap * fc_Dp; }
 };
 
@@ -672,6 +677,9 @@ struct owrx_engine {
     // block's stream-R event and the ring pushes, split by forced (process_block's slot reuse)
     // and opportunistic (the collect after each block)
     double hl_wait[2] = {}, hl_push[2] = {};
+    // host time of owrx_chain_create by section (OWRX_HOST_LOG=1: printed at destroy):
+    // setup, buffers + state uploads, bandpass taps, W reserve + build, group refresh, staging
+    double cc_ms[6] = {};
     int64_t hl_n[2] = {};
     bool hl_forced = false;
     int64_t history = kDefaultHistory;
@@ -742,7 +750,14 @@ struct owrx_engine {
     // (slot_tail >= the block index at its release); new buffers are zeroed and initial states
     // and taps uploaded on stream A, ordered before the first block that uses them.
     std::unordered_map<size_t, std::vector<void*>> pool_free;
-    std::unordered_map<void*, size_t> pool_size;  // every pool allocation (freed at destroy)
+    std::unordered_map<void*, size_t> pool_size;  // every pool buffer and its size class
+    // small pool buffers are carved from slabs (palloc): a fresh engine creating 98 304 chains
+    // made ~2 M hipMalloc calls, one per chain buffer; slabs and direct allocations are what
+    // destroy frees (carved buffers live inside a slab)
+    std::vector<void*> slabs;
+    std::unordered_set<void*> pool_carved;
+    char* slab_cur = nullptr;
+    size_t slab_left = 0;
     struct Retired {
         int64_t block;
         void* p;
@@ -762,6 +777,10 @@ struct owrx_engine {
     uint8_t* h_up = nullptr;  // pinned staging of those uploads (a ring; wraps after stream A)
     size_t up_cap = 0, up_head = 0;
     std::vector<ZeroJob> zero_pending;  // pool buffers taken but not yet zeroed (flush_zero)
+    // uploads not yet enqueued (upload()): their bytes, 16-B aligned, and (dst, offset, size)
+    // records; flush_uploads() copies them into the pinned ring and launches one copy_jobs
+    std::vector<uint8_t> up_data;
+    std::vector<CopyJob> up_jobs;  // src = offset into up_data until the flush
     // post staging needs of the current chains (kept as chains come and go)
     int64_t need_out = 256, need_sm = 4, need_dbg = 64;
 };
@@ -837,7 +856,10 @@ static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
     return nk;
 }
 
-// pool allocation (see owrx_engine): zeroed on stream A
+// pool allocation (see owrx_engine): zeroed on stream A.  Buffers up to kCarveMax come from
+// kSlabBytes slabs (256-B aligned offsets), larger ones from hipMalloc.
+constexpr size_t kCarveMax = 256u << 10;
+constexpr size_t kSlabBytes = 64u << 20;
 template <typename T>
 static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
     *p = nullptr;
@@ -847,6 +869,24 @@ static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
     if (it != e->pool_free.end() && !it->second.empty()) {
         q = it->second.back();
         it->second.pop_back();
+    } else if (bytes <= kCarveMax) {
+        if (e->slab_left < bytes) {
+            void* sl = nullptr;
+            const hipError_t r = hipMalloc(&sl, kSlabBytes);
+            if (r != hipSuccess) {
+                (void)hipGetLastError();
+                return r;
+            }
+            e->slabs.push_back(sl);
+            e->slab_cur = static_cast<char*>(sl);
+            e->slab_left = kSlabBytes;
+            e->stats.pool_allocs++;
+        }
+        q = e->slab_cur;
+        e->slab_cur += bytes;
+        e->slab_left -= bytes;
+        e->pool_size[q] = bytes;
+        e->pool_carved.insert(q);
     } else {
         const hipError_t r = hipMalloc(&q, bytes);
         if (r != hipSuccess) {
@@ -861,9 +901,14 @@ static hipError_t palloc(owrx_engine* e, T** p, size_t count) {
     return hipSuccess;
 }
 
-// release to the pool once the blocks enqueued so far have drained
+static int flush_uploads(owrx_engine* e);
+
+// release to the pool once the blocks enqueued so far have drained.  Pending uploads are
+// enqueued first: one may target this buffer, and its next owner's zeroing and upload must run
+// after it (copy_jobs does not order jobs to the same destination within a launch).
 template <typename T>
 static void prel(owrx_engine* e, T*& p) {
+    if (p && !e->up_jobs.empty()) (void)flush_uploads(e);
     if (p) e->pool_retired.push_back({e->block_index, (void*)p});
     p = nullptr;
 }
@@ -898,6 +943,7 @@ static void hprel_now(owrx_engine* e, T*& p) {
 }
 template <typename T>
 static void prel_now(owrx_engine* e, T*& p) {
+    if (p && !e->up_jobs.empty()) (void)flush_uploads(e);  // (see prel)
     if (p) e->pool_free[e->pool_size[(void*)p]].push_back((void*)p);
     p = nullptr;
 }
@@ -1003,13 +1049,71 @@ static int flush_zero(owrx_engine* e) {
     return OWRX_OK;
 }
 
+// The filter-spectra builds of the chains that joined since the last flush, one launch per
+// group (W is zeroed by fc_reserve before any build writes it).  Before anything that copies or
+// moves W rows (fc_reserve's regrowth, a leave's swap-remove) and with every upload flush.
+static int flush_wbuilds(owrx_engine* e) {
+    for (auto& gp : e->groups) {
+        ChainGroup* g = gp.get();
+        size_t j0 = 0;
+        while (j0 < g->w_pending.size()) {
+            const size_t nj = std::min<size_t>(g->w_pending.size() - j0, 65535);
+            uint8_t* h = nullptr;
+            RCCHK(ring_take(e, sizeof(FcWJob) * nj, &h));
+            memcpy(h, g->w_pending.data() + j0, sizeof(FcWJob) * nj);
+            HIPCHK(launch_fc_make_w_jobs(g->fc_M, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P,
+                                         reinterpret_cast<const FcWJob*>(h), (int)nj, g->d_fc_w,
+                                         g->fc_w_ks(), e->sA));
+            j0 += nj;
+        }
+        g->w_pending.clear();
+    }
+    return OWRX_OK;
+}
+
+// Enqueue every pending upload on stream A: the pool buffers' zeroing first (a buffer's initial
+// state is uploaded after it was zeroed), then one copy_jobs launch for all the uploads, their
+// bytes and job table in one take of the pinned ring.  Called before any stream-A work that may
+// read an uploaded buffer (each block, owrx_sync), and by upload() past kUpFlushBytes.
+constexpr size_t kUpFlushBytes = 4u << 20;
+static int flush_uploads(owrx_engine* e) {
+    RCCHK(flush_zero(e));
+    size_t j0 = 0;
+    while (j0 < e->up_jobs.size()) {
+        const size_t nj = std::min<size_t>(e->up_jobs.size() - j0, 65535);
+        const size_t tab = (sizeof(CopyJob) * nj + 255) & ~(size_t)255;
+        const size_t lo = (size_t)(intptr_t)e->up_jobs[j0].src;
+        const CopyJob& last = e->up_jobs[j0 + nj - 1];
+        const size_t hi = (size_t)(intptr_t)last.src + (size_t)last.bytes;
+        uint8_t* h = nullptr;
+        RCCHK(ring_take(e, tab + (hi - lo), &h));
+        memcpy(h + tab, e->up_data.data() + lo, hi - lo);
+        CopyJob* t = reinterpret_cast<CopyJob*>(h);
+        int64_t most = 0;
+        for (size_t i = 0; i < nj; ++i) {
+            const CopyJob& u = e->up_jobs[j0 + i];
+            t[i] = CopyJob{u.dst, h + tab + ((size_t)(intptr_t)u.src - lo), u.bytes};
+            most = std::max(most, u.bytes);
+        }
+        hipLaunchKernelGGL(copy_jobs, dim3((unsigned)std::min<int64_t>(64, (most + 4095) / 4096), (unsigned)nj),
+                           dim3(256), 0, e->sA, t);
+        HIPCHK(hipGetLastError());
+        j0 += nj;
+    }
+    e->up_jobs.clear();
+    e->up_data.clear();
+    return flush_wbuilds(e);
+}
+
+// Host bytes -> device buffer on stream A, ordered before the next block (or flush_uploads).
+// Chain joins upload their initial states this way: batched, ~no HIP calls per join.
 static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
     if (n == 0) return OWRX_OK;
-    RCCHK(flush_zero(e));
-    uint8_t* h = nullptr;
-    RCCHK(ring_take(e, n, &h));
-    memcpy(h, src, n);
-    HIPCHK(kcopy(dst, h, n, e->sA));
+    const size_t off = (e->up_data.size() + 15) & ~(size_t)15;
+    e->up_data.resize(off + n);
+    memcpy(e->up_data.data() + off, src, n);
+    e->up_jobs.push_back(CopyJob{dst, (const void*)(intptr_t)off, (int64_t)n});
+    if (e->up_data.size() >= kUpFlushBytes) RCCHK(flush_uploads(e));
     return OWRX_OK;
 }
 
@@ -1449,7 +1553,7 @@ static int fc_choose_m(int D, int P, int64_t nk_max) {
 static int fc_build_w(owrx_engine* e, Chain* c, int slot) {
     ChainGroup* g = c->group;
     if (!g->fc_M) return OWRX_OK;
-    RCCHK(flush_zero(e));
+    // (W is zeroed by fc_reserve before any build writes it; nothing else pending is read here)
     HIPCHK(launch_fc_make_w(g->fc_M, g->d_h, g->T, g->D, g->fc_Dp, g->fc_P, c->rate_fx,
                             g->d_fc_w + fc_w_chain_offset(slot, g->fc_Dp), g->fc_w_ks(), e->sA));
     return OWRX_OK;
@@ -1467,6 +1571,7 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
     // on stream A behind the blocks that read the old spectra (those release it when drained)
     HIPCHK(palloc(e, &nw, (size_t)M * cap * g->fc_Dp));
     RCCHK(flush_zero(e));  // zeroed before the rows are copied in
+    RCCHK(flush_wbuilds(e));  // the old rows complete before they move
     if (g->d_fc_w && g->fc_w_cap > 0) {
         const size_t row = sizeof(float2) * (size_t)g->fc_w_cap * g->fc_Dp;
         HIPCHK(hipMemcpy2DAsync(nw, sizeof(float2) * (size_t)cap * g->fc_Dp, g->d_fc_w, row, row,
@@ -1945,7 +2050,7 @@ static int wait_input_block(owrx_engine* e, int64_t j) {
 // every stage runs once over both, the fast DDC with each block's own frame placement
 static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t split = 0) {
     const double t_enter = now_ms();
-    RCCHK(flush_zero(e));  // pool buffers of chains / waterfalls created since the last block
+    RCCHK(flush_uploads(e));  // pool buffers and uploads of chains / waterfalls created since the last block
     // Block k's pinned descriptors are staged per slot (reused by block k + kSlots, after the
     // slot drained and block k's stream-A work is known done).  The caller's input: blocks
     // k - retention + 1 .. k may still be read on stream A when this call returns, block
@@ -2497,6 +2602,10 @@ int owrx_engine_destroy(owrx_engine* e) {
         for (float v : e->wf_ms_log) fprintf(stderr, " %.3f", v);
         fprintf(stderr, "\n");
     }
+    if (getenv("OWRX_HOST_LOG") && e->next_handle > 0)
+        fprintf(stderr, "owrx chain create (ms over all creates): setup %.1f, buffers %.1f, bandpass %.1f, "
+                "W %.1f, group %.1f, staging %.1f\n", e->cc_ms[0], e->cc_ms[1], e->cc_ms[2], e->cc_ms[3],
+                e->cc_ms[4], e->cc_ms[5]);
     if (getenv("OWRX_HOST_LOG"))
         for (int k = 0; k < 2; ++k)
             fprintf(stderr, "owrx %s slot drains: %lld, wait %.3f ms, pushes %.3f ms (per drain %.4f / %.4f)\n",
@@ -2527,7 +2636,9 @@ int owrx_engine_destroy(owrx_engine* e) {
         for (int i = 0; i < kSlots; ++i) dfree(g->d_partial[i]);
         for (auto& h : g->h_chains) hfree(h);
     }
-    for (auto& kv : e->pool_size) hipFree(kv.first);  // the pool's buffers, in use or not
+    for (auto& kv : e->pool_size)  // the pool's buffers, in use or not (carved: in a slab)
+        if (!e->pool_carved.count(kv.first)) hipFree(kv.first);
+    for (void* sl : e->slabs) hipFree(sl);
     for (auto& kv : e->hpool_size) hipHostFree(kv.first);
     hfree(e->h_up);
     dfree(e->d_ring);
@@ -2775,6 +2886,7 @@ int owrx_sync(owrx_engine* e) {
     // owrx_process_device's contract, or the ring).  The flush stages its descriptors in the
     // next block's slot, so only that slot's previous block must have drained; the rest of the
     // pipeline (B's and C's last blocks) drains behind the flush instead of before it.
+    RC_FAIL(e, flush_uploads(e));
     if (e->last_blk) {
         RC_FAIL(e, drain_slots(e, true, e->nslots - 1));
         RC_FAIL(e, run_waterfalls(e, e->last_blk, e->last_start, e->last_end, true, false, nullptr, true));
@@ -3012,6 +3124,12 @@ static int chain_set_bandpass_taps(owrx_engine* e, Chain* c) {
 
 int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     ENGINE_GUARD(e);
+    double tcc = now_ms();
+    auto lap = [&](int k) {
+        const double t = now_ms();
+        e->cc_ms[k] += t - tcc;
+        tcc = t;
+    };
     e->chain_epoch++;  // the slots rebuild their post descriptors
     if (!handle || chain_validate(p)) {
         set_last_error("owrx_chain_create: invalid chain parameters");
@@ -3108,9 +3226,16 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     c->rate_fx = rate_to_fx(p->shift_rate);
     c->cap = chain_stage_cap(e, D, p->frac_rate);
     const int64_t scap = c->cap + p->sq_length + 16;
+    // output staging per block by output type: the encoder input holds up to scap + 160 + kNrN
+    // samples (d_s16: a NoiseFilter emits up to a frame more than its input); ADPCM writes half a
+    // byte per sample plus an 8-B sync frame per 1001 bytes (sizing every output at 4 B per
+    // sample made 98 304 ADPCM chains allocate ~6x the pinned staging they use)
+    const int64_t an = scap + 160 + kNrN;
     c->out_cap = p->output == OWRX_OUT_IQ    ? 8 * c->cap + 64
                  : p->output == OWRX_OUT_SEL ? 8 * scap + 64
-                                             : 4 * scap + 8 * (scap / 2 / kAdpcmSyncPeriod + 2) + 64;
+                 : p->output == OWRX_OUT_ADPCM ? an / 2 + 1 + 8 * (an / 2 / kAdpcmSyncPeriod + 2) + 64
+                 : p->output == OWRX_OUT_S16 ? 2 * an + 64
+                                             : 4 * an + 64;
     c->sm_cap = p->output == OWRX_OUT_IQ ? 4 : (int)(scap / p->sq_length + 4);
     if (p->output != OWRX_OUT_IQ && scap / p->sq_length + 2 > 1024) {  // kMaxSqBlocks
         set_last_error("owrx_chain_create: squelch length %d too short for the block size",
@@ -3127,6 +3252,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
         }
         if (c->bp_design_taps - 1 > kBpHist) c->bp_hist = (c->bp_design_taps - 1 + 255) & ~255;
     }
+    lap(0);
     ChainStateP ps;
     memset(&ps, 0, sizeof(ps));
     ChainStateS ss;
@@ -3158,20 +3284,24 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     for (int i = 0; i < e->nslots; ++i) HIPCHK(palloc(e, &c->d_dem[i], dem_n));
     // + kNrN: a NoiseFilter emits up to one frame more than its input per step
     for (int i = 0; i < e->nslots; ++i) HIPCHK(palloc(e, &c->d_s16[i], (size_t)scap + 160 + kNrN));
+    lap(1);
     int rc = chain_set_bandpass_taps(e, c.get());
     if (!rc && p->nr_enabled && p->output != OWRX_OUT_IQ) rc = chain_nr_alloc(e, c.get());
     if (rc) {
         free_chain(e, c.get());
         return rc;
     }
+    lap(2);
     if (g->fc_M) {
         int wrc = fc_reserve(e, g, (int)g->members.size() + 1);
-        if (!wrc) wrc = fc_build_w(e, c.get(), (int)g->members.size());
+        if (!wrc)  // built with the next flush, batched with the other joins (flush_wbuilds)
+            g->w_pending.push_back(FcWJob{c->rate_fx, fc_w_chain_offset((int)g->members.size(), g->fc_Dp)});
         if (wrc) {
             free_chain(e, c.get());
             return wrc;
         }
     }
+    lap(3);
     const int h = e->next_handle++;
     g->members.push_back(h);
     g->chains_stale = true;
@@ -3181,7 +3311,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     e->need_dbg = std::max<int64_t>(e->need_dbg, (c->cap + c->prm.sq_length + 16) * 8 + 64);
     e->chains[h] = std::move(c);
     RC_FAIL(e, group_refresh_device(e, g));
+    lap(4);
     RC_FAIL(e, ensure_post_capacity(e));
+    lap(5);
     *handle = h;
     return OWRX_OK;
 }
@@ -3199,7 +3331,7 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
     const int last = (int)g->members.size() - 1;
     if (slot != last && g->fc_M) {
-        RC_FAIL(e, flush_zero(e));
+        RC_FAIL(e, flush_uploads(e));  // pending builds land before the last member's rows move
         HIPCHK(launch_fc_move_w(g->fc_M, g->d_fc_w, g->fc_w_ks(), g->fc_Dp, last, slot, e->sA));
     }
     g->members[slot] = g->members[last];

@@ -22,6 +22,7 @@
 // at immediate offsets + packed FMAs.  Measured on MI355X (tools/micro/ddc_bench.cpp, D = 833,
 // P = 27): 67-74 TFLOP/s at 32 chains and 80-87 at 256, against 50-56 / 60-66 for the
 // register-direct ddc_polyphase (OWRX_DDC_KERNEL=flat, kept for A/B at P = 27).
+#include <atomic>
 #include <stdlib.h>
 #include <string.h>
 
@@ -56,16 +57,28 @@ OWRX_DDC_DEPTHS(OWRX_DDC_INSTANTIATE, extern)
 int ddc_blocks_per_cu(int P, int nchains) {
     const bool flat = ddc_uses_flat(P, nchains);
     const int tpw = ddc_tiles_per_wave(nchains);
+    // memoised per (depth, form, tiles per wave): the occupancy query cost ~10 us per chain
+    // create (group_refresh_device runs on every join)
+    static std::atomic<int> memo[7][2][7];
+    const int pi = P == 8 ? 0 : P == 16 ? 1 : P == 27 ? 2 : P == 28 ? 3 : P == 32 ? 4 : P == 48 ? 5 : 6;
+    int ti = 0;
+    while (ti < 6 && (1 << ti) < tpw) ++ti;
+    std::atomic<int>& m = memo[pi][flat ? 1 : 0][ti];
+    const int known = m.load(std::memory_order_relaxed);
+    if (known > 0) return known;
+    int nb = 2;
     switch (P) {
-        case 8: return ddc_occ<8>(flat, tpw);
-        case 16: return ddc_occ<16>(flat, tpw);
-        case 27: return ddc_occ<27>(flat, tpw);
-        case 28: return ddc_occ<28>(flat, tpw);
-        case 32: return ddc_occ<32>(flat, tpw);
-        case 48: return ddc_occ<48>(flat, tpw);
-        case 64: return ddc_occ<64>(flat, tpw);
+        case 8: nb = ddc_occ<8>(flat, tpw); break;
+        case 16: nb = ddc_occ<16>(flat, tpw); break;
+        case 27: nb = ddc_occ<27>(flat, tpw); break;
+        case 28: nb = ddc_occ<28>(flat, tpw); break;
+        case 32: nb = ddc_occ<32>(flat, tpw); break;
+        case 48: nb = ddc_occ<48>(flat, tpw); break;
+        case 64: nb = ddc_occ<64>(flat, tpw); break;
         default: return 2;
     }
+    m.store(nb, std::memory_order_relaxed);
+    return nb;
 }
 
 // Supported polyphase depths; taps are zero padded up to the instantiated P.

@@ -111,13 +111,14 @@ OWRX_DEV void fc_fft_rows(float2* sm, const float2* __restrict__ tw) {
     }
 }
 
-// ---- W_c[kappa][r], fp64, one chain per launch --------------------------------------------
-// grid: Dp / kFcRT workgroups; block 256.  h: the group's linear taps (T floats); the chain's
-// row kappa is written at W + kappa * w_ks.
+// ---- W_c[kappa][r], fp64 ----------------------------------------------------------------------
+// One workgroup: kFcRT branches of one chain.  h: the group's linear taps (T floats); the chain's
+// row kappa is written at W + kappa * w_ks.  fc_make_w: one chain per launch (grid Dp / kFcRT;
+// retunes); fc_make_w_jobs: every chain that joined since the last flush (grid (Dp / kFcRT,
+// jobs)), so a burst of joins fills the chip instead of 54 workgroups per launch.
 template <int M>
-__global__ void __launch_bounds__(256)
-fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rate_fx,
-          float2* __restrict__ W, int64_t w_ks) {
+__device__ void fc_make_w_rows(const float* __restrict__ h, int T, int D, int P, uint64_t rate_fx,
+                               float2* __restrict__ W, int64_t w_ks) {
     __shared__ double2 g[kFcRT][64];   // P <= 64
     __shared__ double2 tw[M];          // e^{+j 2 pi m / M}
     const int tid = threadIdx.x;
@@ -156,6 +157,21 @@ fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rat
         const int r = r0 + j;  // tiled: the chain's K-block of 8 branches every 64 entries
         W[(int64_t)kap * w_ks + (r >> 3) * kFcTile * 8 + (r & 7)] = make_float2((float)re, (float)im);  // zero for r >= D
     }
+}
+
+template <int M>
+__global__ void __launch_bounds__(256)
+fc_make_w(const float* __restrict__ h, int T, int D, int Dp, int P, uint64_t rate_fx,
+          float2* __restrict__ W, int64_t w_ks) {
+    fc_make_w_rows<M>(h, T, D, P, rate_fx, W, w_ks);
+}
+
+template <int M>
+__global__ void __launch_bounds__(256)
+fc_make_w_jobs(const float* __restrict__ h, int T, int D, int P, const FcWJob* __restrict__ jobs,
+               float2* __restrict__ W, int64_t w_ks) {
+    const FcWJob j = jobs[blockIdx.y];
+    fc_make_w_rows<M>(h, T, D, P, j.rate_fx, W + j.off, w_ks);
 }
 
 // ---- U[kappa][f][r]: M-point DFT of every branch frame --------------------------------------
@@ -654,6 +670,18 @@ int fc_kslices_max(int M, int nchains, int Dp, int ncu) {
     }
 
 int fc_frame_supported(int m) { return m == 64 || m == 128 || m == 192 || m == 256 || m == 384; }
+
+hipError_t launch_fc_make_w_jobs(int m, const float* h, int T, int D, int Dp, int P,
+                                 const FcWJob* jobs, int njobs, float2* W, int64_t w_ks,
+                                 hipStream_t st) {
+    if (njobs <= 0) return hipSuccess;
+    if (njobs > 65535) return hipErrorInvalidValue;
+    const dim3 grid(Dp / kFcRT, njobs);
+#define OWRX_FC_WJ(MM) hipLaunchKernelGGL(fc_make_w_jobs<MM>, grid, dim3(256), 0, st, h, T, D, P, jobs, W, w_ks)
+    OWRX_FC_SWITCH(m, OWRX_FC_WJ)
+#undef OWRX_FC_WJ
+    return hipGetLastError();
+}
 
 hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
                             uint64_t rate_fx, float2* W, int64_t w_ks, hipStream_t st) {

@@ -24,6 +24,13 @@ struct WfRow {
 };
 
 // ---- DDC (Shift + FirDecimate, fused, all chains of one (D, taps) group) ----------------
+// One chain's filter-spectra build in a batched fc_make_w_jobs launch: its shift rate and the
+// offset of its slot in the group's W.
+struct FcWJob {
+    uint64_t rate_fx;
+    int64_t off;
+};
+
 struct DdcChain {
     uint64_t rate_fx;    // shift rate in 2^-64 turns per sample
     float2 wD;           // exp(j 2 pi D rate): rotator step between consecutive outputs

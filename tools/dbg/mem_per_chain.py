@@ -35,5 +35,5 @@ try:
             last = f
 except Exception as exc:
     print("  stopped at %d chains: %s" % (n, str(exc)[:160]), flush=True)
-print("%d created in %.1f s" % (n, time.time() - t0), flush=True)
+print("%d created in %.1f s (%.1f us per chain)" % (n, time.time() - t0, 1e6 * (time.time() - t0) / max(1, n)), flush=True)
 eng.close()
