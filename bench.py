@@ -233,6 +233,7 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     gc_was = gc.isenabled()
     gc.collect()
     gc.disable()
+    parts = []  # per block: (push, reads) seconds
     t0 = time.perf_counter()
     for i in range(nblocks):
         deadline = t0 + i * period
@@ -275,6 +276,7 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
         tr += e - d
         # pipelined: how late the block's push (and this iteration) ran against its deadline
         lat.append(e - a if not pipelined else e - deadline)
+        parts.append((b - a, e - d))
     st_loop = eng.stats()
     if gc_was:
         gc.enable()
@@ -310,6 +312,10 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             "blocks": nblocks, "block_period_ms": round(1e3 * period, 2),
             "max_block_latency_ms": round(1e3 * max(lat), 3),
             "mean_block_latency_ms": round(1e3 * sum(lat) / len(lat), 3),
+            # the five latest blocks: [block index, latency, push, reads] in ms
+            "worst_blocks": [[i, round(1e3 * lat[i], 1), round(1e3 * parts[i][0], 1),
+                              round(1e3 * parts[i][1], 1)]
+                             for i in sorted(range(len(lat)), key=lambda i: -lat[i])[:5]],
             "latency_definition": ("push start to outputs in the host rings (sync per block)"
                                    if not pipelined else
                                    "deadline to the end of the block's push + churn + reads "
