@@ -3330,8 +3330,11 @@ int owrx_chain_destroy(owrx_engine* e, int handle) {
     // swap-remove: the last member takes the slot (and its filter spectra move with it)
     const int slot = (int)(std::find(g->members.begin(), g->members.end(), handle) - g->members.begin());
     const int last = (int)g->members.size() - 1;
+    // pending spectra builds run first: before the last member's rows move, and before a later
+    // join's build can target this slot (one fc_make_w_jobs launch does not order two jobs on
+    // the same slot)
+    if (!g->w_pending.empty()) RC_FAIL(e, flush_uploads(e));
     if (slot != last && g->fc_M) {
-        RC_FAIL(e, flush_uploads(e));  // pending builds land before the last member's rows move
         HIPCHK(launch_fc_move_w(g->fc_M, g->d_fc_w, g->fc_w_ks(), g->fc_Dp, last, slot, e->sA));
     }
     g->members[slot] = g->members[last];

@@ -569,6 +569,39 @@ def test_block_pairing_same_outputs(amd, fs, modes, B):
     assert a[2] == b[2]
 
 
+def test_join_leave_join_before_first_block(amd):
+    """A chain that joins and leaves before any block, then another chain that joins: the second
+    one takes the first one's W slot and (from the pool) its buffers while both joins' spectra
+    builds and initial-state uploads are still batched.  Its audio and s-meter equal an engine
+    where only it ever existed, byte for byte."""
+    import torch
+    from openwebrx_amd import synth
+    fs, B = 2400000, 1 << 17
+    modes = ["nfm", "usb"]
+    iq, offs = synth.make_iq(fs, 6 * B, modes)
+    pa = amd.params.chain_params(fs, offs[0], "nfm")
+    pb = amd.params.chain_params(fs, offs[1], "usb")
+
+    def run(first):
+        eng = amd.Engine(fs, max_block=B)
+        if first:
+            eng.chain(pa).close()
+        c = eng.chain(pb)
+        h = eng.history
+        buf = torch.zeros(h + iq.size, dtype=torch.complex64, device="cuda")
+        buf[h:] = torch.from_numpy(iq).to("cuda")
+        torch.cuda.synchronize()
+        for k in range(6):
+            eng.process_device(buf.data_ptr() + 8 * (h + k * B), B)
+        eng.sync()
+        out = (c.read_audio(), c.read_smeter().tobytes())
+        eng.close()
+        return out
+
+    a, b = run(False), run(True)
+    assert len(a[0]) > 0 and a == b
+
+
 def test_block_pairing_rejects_bad_state(amd):
     """Pairing needs input retention >= 4 and an engine with no chain, waterfall or block yet."""
     eng = amd.Engine(2400000, max_block=1 << 16)
