@@ -781,6 +781,7 @@ struct owrx_engine {
     // records; flush_uploads() copies them into the pinned ring and launches one copy_jobs
     std::vector<uint8_t> up_data;
     std::vector<CopyJob> up_jobs;  // src = offset into up_data until the flush
+    std::unordered_map<void*, size_t> up_index;  // dst -> its pending job (latest bytes win)
     // post staging needs of the current chains (kept as chains come and go)
     int64_t need_out = 256, need_sm = 4, need_dbg = 64;
 };
@@ -1102,6 +1103,7 @@ static int flush_uploads(owrx_engine* e) {
     }
     e->up_jobs.clear();
     e->up_data.clear();
+    e->up_index.clear();
     return flush_wbuilds(e);
 }
 
@@ -1109,9 +1111,21 @@ static int flush_uploads(owrx_engine* e) {
 // Chain joins upload their initial states this way: batched, ~no HIP calls per join.
 static int upload(owrx_engine* e, void* dst, const void* src, size_t n) {
     if (n == 0) return OWRX_OK;
+    // a second upload to a pending destination (setBandpass twice between blocks) replaces the
+    // first one's bytes: one copy_jobs launch does not order two jobs on the same destination
+    const auto hit = e->up_index.find(dst);
+    if (hit != e->up_index.end()) {
+        const CopyJob& j = e->up_jobs[hit->second];
+        if ((size_t)j.bytes == n) {
+            memcpy(e->up_data.data() + (size_t)(intptr_t)j.src, src, n);
+            return OWRX_OK;
+        }
+        RCCHK(flush_uploads(e));
+    }
     const size_t off = (e->up_data.size() + 15) & ~(size_t)15;
     e->up_data.resize(off + n);
     memcpy(e->up_data.data() + off, src, n);
+    e->up_index[dst] = e->up_jobs.size();
     e->up_jobs.push_back(CopyJob{dst, (const void*)(intptr_t)off, (int64_t)n});
     if (e->up_data.size() >= kUpFlushBytes) RCCHK(flush_uploads(e));
     return OWRX_OK;

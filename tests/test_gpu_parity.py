@@ -602,6 +602,37 @@ def test_join_leave_join_before_first_block(amd):
     assert len(a[0]) > 0 and a == b
 
 
+def test_two_setbandpass_between_blocks_last_wins(amd):
+    """Two setBandpass calls between blocks (a dragged passband) queue two uploads of the same
+    taps buffer before the next block: the output equals an engine that got only the second."""
+    import torch
+    from openwebrx_amd import synth
+    fs, B = 2400000, 1 << 17
+    iq, offs = synth.make_iq(fs, 6 * B, ["usb"])
+    p = amd.params.chain_params(fs, offs[0], "usb")
+
+    def run(both):
+        eng = amd.Engine(fs, max_block=B)
+        c = eng.chain(p)
+        h = eng.history
+        buf = torch.zeros(h + iq.size, dtype=torch.complex64, device="cuda")
+        buf[h:] = torch.from_numpy(iq).to("cuda")
+        torch.cuda.synchronize()
+        for k in range(6):
+            if k == 3:
+                if both:
+                    c.set_bandpass(amd.params.f32(-0.15), amd.params.f32(0.05))
+                c.set_bandpass(amd.params.f32(0.0), amd.params.f32(0.12))
+            eng.process_device(buf.data_ptr() + 8 * (h + k * B), B)
+        eng.sync()
+        out = c.read_audio()
+        eng.close()
+        return out
+
+    a, b = run(False), run(True)
+    assert len(a) > 0 and a == b
+
+
 def test_block_pairing_rejects_bad_state(amd):
     """Pairing needs input retention >= 4 and an engine with no chain, waterfall or block yet."""
     eng = amd.Engine(2400000, max_block=1 << 16)
