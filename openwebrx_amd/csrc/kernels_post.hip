@@ -991,8 +991,9 @@ hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const i
 //   wave 1  stages the int16 input (16-B loads, lane = chain) into an LDS ring one chunk of
 //           kAdChunk samples ahead, so the encoder never waits on memory;
 //   wave 0  encodes groups of 8 samples out of LDS (one ds_read_b128 per group) with the
-//           table step (adpcm_encode_tab: successor index / step in one LDS read) and emits the
-//           group's 4 completed bytes as one store.
+//           remainder form (adpcm_encode_rem: no lane masks, the successor record in one LDS
+//           read; the encoder is issue-bound, so its instruction count is its speed) and emits
+//           the group's 4 completed bytes as one store.
 // Byte stream: low nibble first; a byte started by the last sample of a block completes with
 // the next block's first sample (has_left).  Frames: "SYNC" + (index, predictor) before every
 // byte whose index in the chain's byte stream is a multiple of 1001 (AudioEngine.js:449-491),
@@ -1005,16 +1006,14 @@ constexpr int kAdGroups = kAdChunk / 8;
 
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 
-template <bool T2>  // T2: the byte-addressed successor table (adpcm_encode_tab2; A/B)
 __global__ void __launch_bounds__(128)
 chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
             const int* __restrict__ sel, int nsel) {
-    __shared__ __align__(16) uint32_t NS[T2 ? kAdpcmTab2Entries : kAdpcmTabEntries];
+    __shared__ __align__(16) uint2 NS[kAdpcmRemEntries];
     __shared__ uint4 ring[2][kAdGroups][64];  // [slot][group][lane]: 8 int16 samples
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    if constexpr (T2) adpcm_tab2_fill(NS, threadIdx.x, 128);
-    else adpcm_tab_fill(NS, threadIdx.x, 128);  // (array references: the extent is checked)
+    adpcm_rem_fill(NS, threadIdx.x, 128);  // (array reference: the extent is checked)
     const SerLane sl = ser_lane(sel, nsel);
     const int c = sl.c;
     const ChainPost* Pp = posts + c;
@@ -1051,14 +1050,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     // ---- wave 0: the encoder
     ChainStateS* sp = Pp->sstate;
     const ChainStateS st0 = *sp;
-    auto ad = [&] {
-        if constexpr (T2) return adpcm_tab2_state(st0.adpcm);
-        else return adpcm_tab_state(st0.adpcm);
-    }();
-    auto encode = [&](int x) {
-        if constexpr (T2) return adpcm_encode_tab2(ad, x, NS);
-        else return adpcm_encode_tab(ad, x, NS);
-    };
+    AdpcmRem ad = adpcm_rem_state(st0.adpcm);
     const int pend = st0.has_left;  // 1: bytes start at odd samples of this block
     int left = st0.left_code;       // the started byte's low nibble (pend == 1)
     int64_t K = st0.adpcm_bytes + pend;  // index of the next byte to start
@@ -1091,12 +1083,13 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
             const bool frame_here = kmod == 0 || kmod > kAdpcmSyncPeriod - 4;
             const bool slow = sl.active && (frame_here || i0 + 8 > n);
             if (!__any(slow) && i0 + 8 <= nmin) {
-                uint32_t w = 0;
+                uint32_t w = 0;  // the codes ^ 7 (adpcm_encode_rem), fixed below
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
-                    w |= (uint32_t)encode(x) << (4 * t);
+                    w |= (adpcm_encode_rem(ad, x, NS) & 15u) << (4 * t);
                 }
+                w ^= 0x77777777u;
                 const uint32_t bytes4 = pend ? ((w << 4) | (uint32_t)left) : w;
                 if (pend) left = (int)(w >> 28);
                 if (sl.active) *reinterpret_cast<__attribute__((address_space(1))) u32_unaligned*>(
@@ -1117,7 +1110,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
                     if (kmod == 0) frame();
                     if (++kmod == kAdpcmSyncPeriod) kmod = 0;
                 }
-                const int code = encode(x);
+                const int code = (int)((adpcm_encode_rem(ad, x, NS) & 15u) ^ 7u);
                 if (start) {
                     nib = code;
                 } else {
@@ -1195,18 +1188,8 @@ hipError_t launch_post_serial(const ChainPost* posts, ChainCounts* counts, const
 hipError_t launch_chain_adpcm(const ChainPost* posts, ChainCounts* counts, const int* sel,
                               int nsel, hipStream_t st) {
     if (nsel <= 0) return hipSuccess;
-    // the byte-addressed successor table (default: 564-567 vs 573-574 us per C3 block, same box,
-    // profiles/r02ab_ab_adpcm_tab2_c3.txt); OWRX_AD_TAB=1: the index-row table (A/B)
-    static const bool t2 = [] {
-        const char* v = getenv("OWRX_AD_TAB");
-        return !(v && strcmp(v, "1") == 0);
-    }();
-    if (t2)
-        hipLaunchKernelGGL(chain_adpcm<true>, dim3((nsel + 63) / 64), dim3(128), 0, st, posts, counts,
-                           sel, nsel);
-    else
-        hipLaunchKernelGGL(chain_adpcm<false>, dim3((nsel + 63) / 64), dim3(128), 0, st, posts,
-                           counts, sel, nsel);
+    hipLaunchKernelGGL(chain_adpcm, dim3((nsel + 63) / 64), dim3(128), 0, st, posts, counts, sel,
+                       nsel);
     return hipGetLastError();
 }
 

@@ -320,63 +320,69 @@ OWRX_DEV int adpcm_encode_tab(AdpcmTab& s, int sample, const uint32_t* __restric
     return mag | (sgn & 8);
 }
 
-// Byte-addressed variant (chain_adpcm default; OWRX_AD_TAB=1 selects adpcm_encode_tab):
-// NS2[index * 16 + sign * 8 + magnitude] = next step | (next index * 64) << 16 (the entry does
-// not depend on the sign: each row is stored twice), so the next record's LDS byte address is
-// the current record's high half + 32 * sign + 4 * magnitude -- one select after the last
-// magnitude compare -- and the 4-bit code is that address's bits 2..5.  Each magnitude bit's
-// remainder is selected from a subtraction done beside the compare.  Bit-identical to
+// Remainder form (chain_adpcm): no lane masks on the recurrence.  One wave issues about one
+// instruction per 4.5-5 cycles and the serial encoder is issue-bound
+// (profiles/r05_issue_latency_micro.txt), so this form minimises instructions, not depth:
+//   - 8-B successor records {step | (2 index) << 16, h | q << 16} (h = step >> 1, q = step >> 2)
+//     whose 16-bit fields the subtractions read in place (SDWA): nothing is unpacked per sample;
+//   - per magnitude bit t in (step, h, q): u = a - t; the sign of u is the INVERTED bit (a < t), an
+//     alignbit shifts it into the record index; a = min_u32(a, u) is the remainder (u wraps above
+//     a when a < t);
+//   - rows of 8 records in reverse magnitude order, one row per (index, sign):
+//     NSR[(2 index + sign) * 8 + (7 - mag)], so the index built from (2 index + sign) and the
+//     three inverted bits addresses the successor directly and its low nibble is the code ^ 7;
+//   - dq = (step >> 3) + a0 - a3 (the subtracted thresholds; step >> 3 = h >> 2).
+// 136 vs 199 cycles per sample for the masked byte-addressed table it replaced
+// (tools/micro/adpcm_r05.cpp, profiles/r05_adpcm_encoder_variants.txt); bit-identical to
 // adpcm_encode.
-constexpr int kAdpcmTab2Entries = 89 * 16;
+constexpr int kAdpcmRemEntries = 89 * 16;
 
 template <int EXT>
-OWRX_DEV void adpcm_tab2_fill(uint32_t (&NS2)[EXT], int tid, int nthreads) {
-    static_assert(EXT >= kAdpcmTab2Entries, "byte-addressed successor table too small");
-    for (int e = tid; e < kAdpcmTab2Entries; e += nthreads) {
-        const int i = e >> 4, m = e & 7;
+OWRX_DEV void adpcm_rem_fill(uint2 (&NSR)[EXT], int tid, int nthreads) {
+    static_assert(EXT >= kAdpcmRemEntries, "remainder-form successor table too small");
+    for (int e = tid; e < kAdpcmRemEntries; e += nthreads) {
+        const int i = e >> 4, m = 7 - (e & 7);
         int ni = i + kAdpcmIndex[m];
         ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
-        NS2[e] = (uint32_t)kAdpcmStep[ni] | ((uint32_t)(ni * 64) << 16);
+        const uint32_t st = (uint32_t)kAdpcmStep[ni];
+        NSR[e] = make_uint2(st | ((uint32_t)(ni * 2) << 16), (st >> 1) | ((st >> 2) << 16));
     }
 }
 
-struct AdpcmTab2 {
-    uint32_t rec;  // step | (index * 64) << 16
+struct AdpcmRem {
+    uint32_t w0, w1;  // step | (2 index) << 16, h | q << 16
     int pred;
-    OWRX_DEV int index() const { return (int)(rec >> 22); }
+    OWRX_DEV int index() const { return (int)(w0 >> 17); }
 };
 
-OWRX_DEV AdpcmTab2 adpcm_tab2_state(AdpcmState s) {
-    return AdpcmTab2{(uint32_t)kAdpcmStep[s.index] | ((uint32_t)(s.index * 64) << 16), s.pred};
+OWRX_DEV AdpcmRem adpcm_rem_state(AdpcmState s) {
+    const uint32_t st = (uint32_t)kAdpcmStep[s.index];
+    return AdpcmRem{st | ((uint32_t)(s.index * 2) << 16), (st >> 1) | ((st >> 2) << 16), s.pred};
 }
 
-OWRX_DEV int adpcm_encode_tab2(AdpcmTab2& s, int sample, const uint32_t* __restrict__ NS2) {
-    // everything that needs only the predictor first, then a scheduling fence, so that it is
-    // issued while this sample's record is still on its way from LDS (the record's first use
-    // carries the wait)
+// Returns the successor's record index; its low nibble is the 4-bit code ^ 7.
+OWRX_DEV uint32_t adpcm_encode_rem(AdpcmRem& s, int sample, const uint2* __restrict__ NSR) {
     const int d = sample - s.pred;
     const int sgn = d >> 31;
-    const int sg32 = sgn & 32;
-    const int a0 = max(d, -d);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t rec = s.rec;
-    const int step = (int)(rec & 0xffffu);
-    const int h = step >> 1, q = step >> 2, s3 = step >> 3;
-    const int rb = (int)(rec >> 16) + sg32;
-    const bool m4 = a0 >= step;
-    const int a1 = m4 ? a0 - step : a0;
-    const bool m2 = a1 >= h;
-    const int a2 = m2 ? a1 - h : a1;
-    const bool m1 = a2 >= q;
-    const int base = rb + (m4 ? 16 : 0) + (m2 ? 8 : 0);
-    const int addr = m1 ? base + 4 : base;
-    s.rec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(NS2) + addr);
-    // the predictor update after the lookup is issued (it fills the lookup's latency)
-    __builtin_amdgcn_sched_barrier(0);
-    const int dq = s3 + (m4 ? step : 0) + (m2 ? h : 0) + (m1 ? q : 0);
+    const uint32_t a0 = (uint32_t)max(d, -d);
+    const uint32_t w0 = s.w0, w1 = s.w1;
+    uint32_t acc = ((uint32_t)d >> 31) + (w0 >> 16);
+    const uint32_t u4 = a0 - (w0 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u4, 31);
+    const uint32_t a1 = min(a0, u4);
+    const uint32_t u2 = a1 - (w1 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u2, 31);
+    const uint32_t a2 = min(a1, u2);
+    const uint32_t u1 = a2 - (w1 >> 16);
+    acc = __builtin_amdgcn_alignbit(acc, u1, 31);
+    const uint32_t a3 = min(a2, u1);
+    const uint2 r = NSR[acc];
+    const int dq = (int)(((w1 & 0xffffu) >> 2) + (a0 - a3));
+    s.w0 = r.x;
+    s.w1 = r.y;
     const int p = s.pred + ((dq ^ sgn) - sgn);
     s.pred = min(max(p, -32768), 32767);
-    return (addr >> 2) & 15;  // magnitude bits and the sign (32 bytes = code bit 3)
+    return acc;
 }
 
 }  // namespace owrx

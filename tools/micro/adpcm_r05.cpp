@@ -1,9 +1,11 @@
 // IMA-ADPCM serial encoder microbenchmark, round 5 (diagnostic; not part of the product):
-// cycles per sample of the production byte-addressed successor table (adpcm_encode_tab2)
-// against a successor table whose 64-B records carry the successor step's compare thresholds
-// (step, h, step + h, q, h + q, step + q, step + h + q) and dq terms, so that after a record
-// arrives the magnitude needs three compares and two selects and no subtractions.  One lane per
-// stream, 64 streams x 5000 samples; the codes of both encoders are compared.
+// cycles per sample of one 64-lane wave (one lane per stream, 64 streams x 5000 samples) for the
+// round 2-4 production encoder (byte-addressed masked successor table, tab2, defined below as the
+// baseline) and its variants: 64-B threshold records, a ds_bpermute step, the successor row read
+// beside the compares, reversed rows with accumulated compare bits (tab3), 8-B records with SDWA
+// compares and a v_addc index in asm (tab4), the mask-free sub / alignbit / min form (tab6), and
+// that form as shipped (adpcm_encode_rem, owrx_dev.h).  Every variant's codes are compared with
+// tab2's.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 adpcm_r05.cpp -o adpcm_r05
 #include "../../openwebrx_amd/csrc/owrx_dev.h"
 
@@ -14,6 +16,66 @@
 #include <vector>
 
 using namespace owrx;
+
+// The round 2-4 production encoder (byte-addressed masked table), kept here as the baseline:
+// NS2[index * 16 + sign * 8 + magnitude] = next step | (next index * 64) << 16 (the entry does
+// not depend on the sign: each row is stored twice), so the next record's LDS byte address is
+// the current record's high half + 32 * sign + 4 * magnitude -- one select after the last
+// magnitude compare -- and the 4-bit code is that address's bits 2..5.  Each magnitude bit's
+// remainder is selected from a subtraction done beside the compare.  Bit-identical to
+// adpcm_encode.
+constexpr int kAdpcmTab2Entries = 89 * 16;
+
+template <int EXT>
+OWRX_DEV void adpcm_tab2_fill(uint32_t (&NS2)[EXT], int tid, int nthreads) {
+    static_assert(EXT >= kAdpcmTab2Entries, "byte-addressed successor table too small");
+    for (int e = tid; e < kAdpcmTab2Entries; e += nthreads) {
+        const int i = e >> 4, m = e & 7;
+        int ni = i + kAdpcmIndex[m];
+        ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
+        NS2[e] = (uint32_t)kAdpcmStep[ni] | ((uint32_t)(ni * 64) << 16);
+    }
+}
+
+struct AdpcmTab2 {
+    uint32_t rec;  // step | (index * 64) << 16
+    int pred;
+    OWRX_DEV int index() const { return (int)(rec >> 22); }
+};
+
+OWRX_DEV AdpcmTab2 adpcm_tab2_state(AdpcmState s) {
+    return AdpcmTab2{(uint32_t)kAdpcmStep[s.index] | ((uint32_t)(s.index * 64) << 16), s.pred};
+}
+
+OWRX_DEV int adpcm_encode_tab2(AdpcmTab2& s, int sample, const uint32_t* __restrict__ NS2) {
+    // everything that needs only the predictor first, then a scheduling fence, so that it is
+    // issued while this sample's record is still on its way from LDS (the record's first use
+    // carries the wait)
+    const int d = sample - s.pred;
+    const int sgn = d >> 31;
+    const int sg32 = sgn & 32;
+    const int a0 = max(d, -d);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t rec = s.rec;
+    const int step = (int)(rec & 0xffffu);
+    const int h = step >> 1, q = step >> 2, s3 = step >> 3;
+    const int rb = (int)(rec >> 16) + sg32;
+    const bool m4 = a0 >= step;
+    const int a1 = m4 ? a0 - step : a0;
+    const bool m2 = a1 >= h;
+    const int a2 = m2 ? a1 - h : a1;
+    const bool m1 = a2 >= q;
+    const int base = rb + (m4 ? 16 : 0) + (m2 ? 8 : 0);
+    const int addr = m1 ? base + 4 : base;
+    s.rec = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(NS2) + addr);
+    // the predictor update after the lookup is issued (it fills the lookup's latency)
+    __builtin_amdgcn_sched_barrier(0);
+    const int dq = s3 + (m4 ? step : 0) + (m2 ? h : 0) + (m1 ? q : 0);
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    return (addr >> 2) & 15;  // magnitude bits and the sign (32 bytes = code bit 3)
+}
+
 
 constexpr int kThRec = 64;                 // bytes per record
 constexpr int kThEntries = 89 * 8;         // (index, magnitude) -> the successor's record
@@ -130,11 +192,138 @@ __device__ __forceinline__ int row_encode(AdpcmTab2& s, int x, const uint32_t* N
     return (m4 ? 4 : 0) | (m2 ? 2 : 0) | (m1 ? 1 : 0) | (sgn & 8);
 }
 
+// V == 4: rows of 8 successor records in reverse magnitude order, indexed by (index * 2 + sign):
+// NS3[(2 index + sign) * 8 + (7 - mag)] = next step | (2 next index) << 16.  The word index is
+// built by doubling an accumulator and adding each inverted magnitude bit (a compare's result, a
+// v_addc carry-in), so the code is the index's low nibble ^ 7 and no select builds an address.
+constexpr int kAdpcmTab3Entries = 89 * 16;
+
+__device__ void tab3_fill(uint32_t* NS3, int tid, int nt) {
+    for (int e = tid; e < kAdpcmTab3Entries; e += nt) {
+        const int index = e >> 4, mag = 7 - (e & 7);
+        int ni = index + kAdpcmIndex[mag];
+        ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
+        NS3[e] = (uint32_t)kAdpcmStep[ni] | ((uint32_t)(ni * 2) << 16);
+    }
+}
+
+struct Tab3 {
+    uint32_t rec;  // step | (2 index) << 16
+    int pred;
+};
+
+__device__ __forceinline__ uint32_t tab3_encode(Tab3& s, int x, const uint32_t* __restrict__ NS3) {
+    const int d = x - s.pred;
+    const int sgn = d >> 31;
+    const uint32_t sb = (uint32_t)d >> 31;
+    const int a0 = max(d, -d);
+    const uint32_t rec = s.rec;
+    const int step = (int)(rec & 0xffffu), h = step >> 1, q = step >> 2, s3 = step >> 3;
+    uint32_t acc = (rec >> 16) + sb;
+    const bool n4 = a0 < step;
+    acc = 2 * acc + (uint32_t)n4;
+    const int a1 = n4 ? a0 : a0 - step;
+    const bool n2 = a1 < h;
+    acc = 2 * acc + (uint32_t)n2;
+    const int a2 = n2 ? a1 : a1 - h;
+    const bool n1 = a2 < q;
+    acc = 2 * acc + (uint32_t)n1;
+    s.rec = NS3[acc];
+    const int dq = s3 + (n4 ? 0 : step) + (n2 ? 0 : h) + (n1 ? 0 : q);
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    return acc;  // low nibble: code ^ 7
+}
+
+// V == 5: tab3's layout with 8-B records {step | (2 index) << 16, h | q << 16}, and the magnitude
+// search in one asm block: SDWA compares / selects read the 16-bit fields in place (no unpacking),
+// and each compare's VCC is the carry-in of a v_addc that doubles the word-index accumulator.
+struct Tab4 {
+    uint32_t w0, w1;  // step | (2 index) << 16, h | q << 16
+    int pred;
+};
+
+__device__ void tab4_fill(uint2* NS4, int tid, int nt) {
+    for (int e = tid; e < kAdpcmTab3Entries; e += nt) {
+        const int index = e >> 4, mag = 7 - (e & 7);
+        int ni = index + kAdpcmIndex[mag];
+        ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
+        const uint32_t st = (uint32_t)kAdpcmStep[ni];
+        NS4[e] = make_uint2(st | ((uint32_t)(ni * 2) << 16), (st >> 1) | ((st >> 2) << 16));
+    }
+}
+
+__device__ __forceinline__ uint32_t tab4_encode(Tab4& s, int x, const uint2* __restrict__ NS4, int zero) {
+    const int d = x - s.pred;
+    const int sgn = d >> 31;
+    const uint32_t sb = (uint32_t)d >> 31;
+    int a = max(d, -d);
+    uint32_t acc = sb + (s.w0 >> 16);
+    int t4, t2, tq;
+    uint64_t cy;
+    asm volatile(
+        "v_cmp_lt_u32_sdwa vcc, %[a], %[w0] src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_addc_co_u32_e64 %[acc], %[cy], %[acc], %[acc], vcc\n\t"
+        "v_cndmask_b32_sdwa %[t4], %[w0], %[z], vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+        "v_sub_u32_e32 %[a], %[a], %[t4]\n\t"
+        "v_cmp_lt_u32_sdwa vcc, %[a], %[w1] src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_addc_co_u32_e64 %[acc], %[cy], %[acc], %[acc], vcc\n\t"
+        "v_cndmask_b32_sdwa %[t2], %[w1], %[z], vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD\n\t"
+        "v_sub_u32_e32 %[a], %[a], %[t2]\n\t"
+        "v_cmp_lt_u32_sdwa vcc, %[a], %[w1] src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "v_addc_co_u32_e64 %[acc], %[cy], %[acc], %[acc], vcc\n\t"
+        "v_cndmask_b32_sdwa %[tq], %[w1], %[z], vcc dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+        : [a] "+v"(a), [acc] "+v"(acc), [t4] "=&v"(t4), [t2] "=&v"(t2), [tq] "=&v"(tq), [cy] "=&s"(cy)
+        : [w0] "v"(s.w0), [w1] "v"(s.w1), [z] "v"(zero)
+        : "vcc");
+    const int s3 = (int)((s.w1 & 0xffffu) >> 2);
+    const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(NS4) + (acc << 3));
+    s.w0 = r.x;
+    s.w1 = r.y;
+    const int dq = s3 + t4 + t2 + tq;
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    return acc;  // low nibble: code ^ 7
+}
+
+// V == 6: tab4's records and rows, no lane masks at all: per magnitude bit u = a - t (t a 16-bit
+// field of the record, read in place by SDWA), acc = alignbit(acc, u, 31) shifts u's sign (the
+// inverted bit) into the word index, a = min_u32(a, u) keeps the remainder (u wraps above a when
+// a < t); dq = s3 + a0 - a3.  Plain C++: the compiler schedules and pads it.
+__device__ __forceinline__ uint32_t tab6_encode(Tab4& s, int x, const uint2* __restrict__ NS4) {
+    const int d = x - s.pred;
+    const int sgn = d >> 31;
+    const uint32_t sb = (uint32_t)d >> 31;
+    const uint32_t a0 = (uint32_t)max(d, -d);
+    const uint32_t w0 = s.w0, w1 = s.w1;
+    uint32_t acc = sb + (w0 >> 16);
+    const uint32_t u4 = a0 - (w0 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u4, 31);
+    const uint32_t a1 = min(a0, u4);
+    const uint32_t u2 = a1 - (w1 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u2, 31);
+    const uint32_t a2 = min(a1, u2);
+    const uint32_t u1 = a2 - (w1 >> 16);
+    acc = __builtin_amdgcn_alignbit(acc, u1, 31);
+    const uint32_t a3 = min(a2, u1);
+    const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(NS4) + (acc << 3));
+    const int dq = (int)(((w1 & 0xffffu) >> 2) + (a0 - a3));
+    s.w0 = r.x;
+    s.w1 = r.y;
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    return acc;  // low nibble: code ^ 7
+}
+
 template <int V>
 __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n, uint8_t* __restrict__ out,
                                            long long* cyc) {
-    __shared__ __align__(16) uint32_t NS[(V == 0 || V == 3) ? kAdpcmTab2Entries : kThEntries * (kThRec / 4)];
+    __shared__ __align__(16) uint2 NSR[V == 7 ? kAdpcmRemEntries : 1];
+    if constexpr (V == 7) adpcm_rem_fill(NSR, threadIdx.x, 64);
+    __shared__ __align__(16) uint32_t NS[(V == 5 || V == 6) ? 2 * kAdpcmTab3Entries : (V == 0 || V == 3 || V == 4) ? kAdpcmTab2Entries : kThEntries * (kThRec / 4)];
     if constexpr (V == 0 || V == 3) adpcm_tab2_fill(NS, threadIdx.x, 64);
+    else if constexpr (V == 4) tab3_fill(NS, threadIdx.x, 64);
+    else if constexpr (V == 5 || V == 6) tab4_fill(reinterpret_cast<uint2*>(NS), threadIdx.x, 64);
     else th_fill(NS, threadIdx.x, 64);
     __syncthreads();
     const int lane = threadIdx.x;
@@ -143,6 +332,10 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
     auto ad2 = adpcm_tab2_state(AdpcmState{0, 0});
     ThState th = th_state(0, 0);
     BpState bp{0, kAdpcmStep[0], 0};
+    Tab3 t3{(uint32_t)kAdpcmStep[0], 0};
+    Tab4 t4s{(uint32_t)kAdpcmStep[0], (uint32_t)(kAdpcmStep[0] >> 1) | ((uint32_t)(kAdpcmStep[0] >> 2) << 16), 0};
+    const int zero = __builtin_amdgcn_readfirstlane(n) * 0;
+    AdpcmRem rem = adpcm_rem_state(AdpcmState{0, 0});
     const int la = lane - 1, lb = lane + 63;
     const int tabA = kAdpcmStep[la < 0 ? 0 : la];
     const int tabB = kAdpcmStep[lb > 88 ? 88 : lb];
@@ -152,6 +345,25 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
     for (int j = 0; j < n; j += 8) {
         for (int q = 0; q < 8; ++q) nxt[q] = src[j + 8 + q];
         uint32_t w = 0;
+        if constexpr (V == 7) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w |= (adpcm_encode_rem(rem, cur[u], NSR) & 15u) << (4 * u);
+            w ^= 0x77777777u;
+        } else if constexpr (V == 6) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                w |= (tab6_encode(t4s, cur[u], reinterpret_cast<const uint2*>(NS)) & 15u) << (4 * u);
+            w ^= 0x77777777u;
+        } else if constexpr (V == 5) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                w |= (tab4_encode(t4s, cur[u], reinterpret_cast<const uint2*>(NS), zero) & 15u) << (4 * u);
+            w ^= 0x77777777u;
+        } else if constexpr (V == 4) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w |= (tab3_encode(t3, cur[u], NS) & 15u) << (4 * u);
+            w ^= 0x77777777u;
+        } else
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             int c;
@@ -224,5 +436,37 @@ int main() {
     for (int c = 0; c < S; ++c)
         for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
     printf("row-prefetch codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    uint8_t* d4;
+    hipMalloc(&d4, (size_t)S * n);
+    run("tab3: reversed rows, accumulated compare bits", kern<4>, d4);
+    hipMemcpy(b.data(), d4, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("tab3 codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    uint8_t* d5;
+    hipMalloc(&d5, (size_t)S * n);
+    run("tab4: 8-B records, SDWA compares + v_addc index", kern<5>, d5);
+    hipMemcpy(b.data(), d5, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("tab4 codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    uint8_t* d6;
+    hipMalloc(&d6, (size_t)S * n);
+    run("tab6: 8-B records, sub / alignbit / min (no masks)", kern<6>, d6);
+    hipMemcpy(b.data(), d6, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("tab6 codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    uint8_t* d7;
+    hipMalloc(&d7, (size_t)S * n);
+    run("adpcm_encode_rem (production, owrx_dev.h)", kern<7>, d7);
+    hipMemcpy(b.data(), d7, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("adpcm_encode_rem codes differing: %zu of %d bytes\n", diff, S * n / 2);
     return 0;
 }
