@@ -65,6 +65,8 @@ std::vector<float> fft_twiddles(int n) {
     return t;
 }
 
+// Every profile has attack > decay > 0: post_serial_front's envelope step takes
+// max(attack d, decay d) for (d > 0 ? attack : decay) d on that basis.
 AgcParams agc_profile(int profile) {
     AgcParams p;
     p.reference = 0.8f;

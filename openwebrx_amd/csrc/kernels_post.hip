@@ -730,16 +730,19 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
     constexpr int kQuads = kSerChunk / 4;
     const auto dem_in = gp(reinterpret_cast<const float4*>(Pp->dem));
     float4 pre[kQuads];
+    // unconditional loads (the quad index clamped to the lane's last quad), zeroed past n when
+    // stored to LDS (after wave 1's gain work, which the loads' latency hides behind): a per-lane
+    // `i < n ?` load is a branch the compiler may close with a full wait before the next one (it
+    // did for the first chunk: 16 memory latencies per launch)
+    const int last_q = n > 0 ? (n - 1) >> 2 : 0;
     auto stage_load = [&](int ch) {
 #pragma unroll
-        for (int q = 0; q < kQuads; ++q) {
-            const int i = ch * kSerChunk + 4 * q;
-            pre[q] = i < n ? dem_in[i >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int q = 0; q < kQuads; ++q) pre[q] = dem_in[min(ch * kQuads + q, last_q)];
     };
     auto stage_store = [&](int ch) {
 #pragma unroll
         for (int q = 0; q < kQuads; ++q) {
+            if (ch * kSerChunk + 4 * q >= n) pre[q] = make_float4(0.f, 0.f, 0.f, 0.f);
             in_[ch & 1][4 * q][lane] = pre[q].x;
             in_[ch & 1][4 * q + 1][lane] = pre[q].y;
             in_[ch & 1][4 * q + 2][lane] = pre[q].z;
@@ -779,8 +782,11 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
 #pragma clang fp contract(off)
                         const float a = fabsf(u);
                         const float d = a - agc.env;
-                        const float rate = (d > 0.0f) ? agcp.attack : agcp.decay;
-                        const float t = rate * d;
+                        // rate * d, rate = attack if d > 0 else decay: attack > decay > 0 in
+                        // every profile (design.cpp agc_params), so it is max(attack d, decay d)
+                        // exactly (rounding is monotonic; d = +-0 gives +-0 either way) -- no
+                        // compare / select and its lane-mask wait states on the recurrence
+                        const float t = fmaxf(agcp.attack * d, agcp.decay * d);
                         agc.env = agc.env + t;
                     }
                     // WFm has no Agc (csdr/chain/analog.py:66-71): envelope = reference makes
@@ -990,10 +996,12 @@ hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const i
 // segments; this kernel is the serial recurrence with everything else moved off its path:
 //   wave 1  stages the int16 input (16-B loads, lane = chain) into an LDS ring one chunk of
 //           kAdChunk samples ahead, so the encoder never waits on memory;
-//   wave 0  encodes groups of 8 samples out of LDS (one ds_read_b128 per group) with the
+//   wave 0  encodes groups of 32 samples out of LDS (four ds_read_b128 per group) with the
 //           remainder form (adpcm_encode_rem: no lane masks, the successor record in one LDS
 //           read; the encoder is issue-bound, so its instruction count is its speed) and emits
-//           the group's 4 completed bytes as one store.
+//           the group's 16 completed bytes as one store.  32-sample groups: the per-group
+//           conditions (a wave vote, exec-mask plumbing, the store) cost ~70 instructions, a
+//           third of an 8-sample group's encoding (profiles/r05_adpcm_group32.txt).
 // Byte stream: low nibble first; a byte started by the last sample of a block completes with
 // the next block's first sample (has_left).  Frames: "SYNC" + (index, predictor) before every
 // byte whose index in the chain's byte stream is a multiple of 1001 (AudioEngine.js:449-491),
@@ -1001,16 +1009,21 @@ hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const i
 // such a byte, or which runs past a lane's last sample, takes the checked per-sample path.
 // Runs on stream C behind post_serial_front, so block k's encoding overlaps block k+1's front
 // and block k+2's DDC.
-constexpr int kAdChunk = 128;                  // samples per staged chunk (16 groups of 8)
-constexpr int kAdGroups = kAdChunk / 8;
+constexpr int kAdChunk = 128;           // samples per staged chunk
+constexpr int kAdQ = kAdChunk / 8;      // 16-B quads (8 samples) per lane and chunk
+constexpr int kAdG = 32;                // samples per encoder group (16 byte starts)
+constexpr int kAdGroups = kAdChunk / kAdG;
 
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
+struct __attribute__((packed, aligned(1))) U128Unaligned {
+    uint32_t x, y, z, w;
+};
 
 __global__ void __launch_bounds__(128)
 chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts,
             const int* __restrict__ sel, int nsel) {
     __shared__ __align__(16) uint2 NS[kAdpcmRemEntries];
-    __shared__ uint4 ring[2][kAdGroups][64];  // [slot][group][lane]: 8 int16 samples
+    __shared__ uint4 ring[2][kAdQ][64];  // [slot][quad][lane]: 8 int16 samples
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     adpcm_rem_fill(NS, threadIdx.x, 128);  // (array reference: the extent is checked)
@@ -1026,15 +1039,15 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     const int nchunks = (nmax + kAdChunk - 1) / kAdChunk;
     const auto src = gp(reinterpret_cast<const uint4*>(Pp->s16));  // 16-B aligned slot
 
-    auto stage = [&](int ch) {  // wave 1: chunk ch -> ring slot ch & 1
-        uint4 v[kAdGroups];
+    // wave 1: chunk ch -> ring slot ch & 1.  The loads are unconditional (the quad index clamped
+    // to the lane's last quad; quads past n are never encoded), so all 16 are in flight at once
+    const int last_q = n > 0 ? (n - 1) >> 3 : 0;
+    auto stage = [&](int ch) {
+        uint4 v[kAdQ];
 #pragma unroll
-        for (int g = 0; g < kAdGroups; ++g) {
-            const int i = ch * kAdChunk + 8 * g;
-            v[g] = i < n ? src[i >> 3] : make_uint4(0, 0, 0, 0);
-        }
+        for (int q = 0; q < kAdQ; ++q) v[q] = src[min(ch * kAdQ + q, last_q)];
 #pragma unroll
-        for (int g = 0; g < kAdGroups; ++g) ring[ch & 1][g][lane] = v[g];
+        for (int q = 0; q < kAdQ; ++q) ring[ch & 1][q][lane] = v[q];
     };
     if (wave == 1 && nchunks > 0) stage(0);
     __syncthreads();
@@ -1071,40 +1084,64 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     };
     for (int ch = 0; ch < nchunks; ++ch) {
         const uint4(*rg)[64] = ring[ch & 1];
-        uint4 vnext = rg[0][lane];
-        for (int g = 0; g < kAdGroups; ++g) {
-            const int i0 = ch * kAdChunk + 8 * g;
-            if (i0 >= nmax) break;
-            const uint4 v = vnext;  // the next group's read is in flight while this one encodes
-            if (g + 1 < kAdGroups) vnext = rg[g + 1][lane];
-            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-            // four byte starts in the group: bytes K .. K + 3; a frame precedes byte k when
-            // k % 1001 == 0
-            const bool frame_here = kmod == 0 || kmod > kAdpcmSyncPeriod - 4;
-            const bool slow = sl.active && (frame_here || i0 + 8 > n);
-            if (!__any(slow) && i0 + 8 <= nmin) {
-                uint32_t w = 0;  // the codes ^ 7 (adpcm_encode_rem), fixed below
+        uint4 vn[4];
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
-                    w |= (adpcm_encode_rem(ad, x, NS) & 15u) << (4 * t);
+        for (int k = 0; k < 4; ++k) vn[k] = rg[k][lane];
+        for (int g = 0; g < kAdGroups; ++g) {
+            const int i0 = ch * kAdChunk + kAdG * g;
+            if (i0 >= nmax) break;
+            uint4 v[4];  // the next group's reads are in flight while this one encodes
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = vn[k];
+            if (g + 1 < kAdGroups) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) vn[k] = rg[4 * (g + 1) + k][lane];
+            }
+            // sixteen byte starts in the group: bytes K .. K + 15; a frame precedes byte k when
+            // k % 1001 == 0
+            const bool frame_here = kmod == 0 || kmod > kAdpcmSyncPeriod - kAdG / 2;
+            const bool slow = sl.active && (frame_here || i0 + kAdG > n);
+            if (!__any(slow) && i0 + kAdG <= nmin) {
+                uint32_t w[4];  // the codes ^ 7 (adpcm_encode_rem), fixed below
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t wv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    uint32_t acc = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
+                        acc |= (adpcm_encode_rem(ad, x, NS) & 15u) << (4 * t);
+                    }
+                    w[k] = acc ^ 0x77777777u;
                 }
-                w ^= 0x77777777u;
-                const uint32_t bytes4 = pend ? ((w << 4) | (uint32_t)left) : w;
-                if (pend) left = (int)(w >> 28);
-                if (sl.active) *reinterpret_cast<__attribute__((address_space(1))) u32_unaligned*>(
-                                   &out.p[ob]) = bytes4;
-                ob += 4;
-                kmod += 4;
+                uint4 b = make_uint4(w[0], w[1], w[2], w[3]);
+                if (pend) {  // bytes start at odd samples: shift the nibble stream by one
+                    b = make_uint4((w[0] << 4) | (uint32_t)left, (w[1] << 4) | (w[0] >> 28),
+                                   (w[2] << 4) | (w[1] >> 28), (w[3] << 4) | (w[2] >> 28));
+                    left = (int)(w[3] >> 28);
+                }
+                if (sl.active) {
+                    auto* d = reinterpret_cast<__attribute__((address_space(1))) U128Unaligned*>(&out.p[ob]);
+                    d->x = b.x;
+                    d->y = b.y;
+                    d->z = b.z;
+                    d->w = b.w;
+                }
+                ob += kAdG / 2;
+                kmod += kAdG / 2;
                 if (kmod >= kAdpcmSyncPeriod) kmod -= kAdpcmSyncPeriod;
                 continue;
             }
-            // checked path: per sample, lanes past their end keep their state
+            // checked path: per sample (read back from the ring), lanes past their end keep
+            // their state
+            const uint32_t* gw = reinterpret_cast<const uint32_t*>(&rg[4 * g][0]);
             int nib = left;
 #pragma unroll 1
-            for (int t = 0; t < 8; ++t) {
+            for (int t = 0; t < kAdG; ++t) {
                 if (!sl.active || i0 + t >= n) break;
-                const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
+                // quad t >> 3 of the group, word (t & 7) >> 1 of this lane's 16 B
+                const uint32_t word = gw[(t >> 3) * 256 + lane * 4 + ((t & 7) >> 1)];
+                const int x = (int)(int16_t)(word >> (16 * (t & 1)));
                 const bool start = (t & 1) == pend;
                 if (start) {
                     if (kmod == 0) frame();

@@ -1,4 +1,6 @@
-"""Per-pair serial-stage time and per-chain audio bytes at C3 (diagnostic): the rocprof trace of
+"""usage: serial_pairs.py [pairs] [chains] [modes, comma-separated]
+
+Per-pair serial-stage time and per-chain audio bytes at C3 (diagnostic): the rocprof trace of
 the C3 bench shows post_serial_front and chain_adpcm ~30 % slower on the same engine blocks
 (about every third pair); this runs the bench's C3 chains (no waterfall) pair by pair, synced,
 with the engine's HIP-event timing on, and prints each pair's serial GPU time next to the spread
@@ -13,9 +15,11 @@ from bench import gen_stream_torch  # noqa: E402
 from openwebrx_amd import Engine, params  # noqa: E402
 from openwebrx_amd.synth import carrier_offsets  # noqa: E402
 
-fs, C, block = 10000000, 256, 1 << 20
+fs, block = 10000000, 1 << 20
 pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-modes = [("nfm", "usb", "cw")[c % 3] for c in range(C)]
+C = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+mset = tuple(sys.argv[3].split(",")) if len(sys.argv) > 3 else ("nfm", "usb", "cw")
+modes = [mset[c % len(mset)] for c in range(C)]
 offs = carrier_offsets(fs, C)
 plist = [params.chain_params(fs, o, m) for o, m in zip(offs, modes)]
 dev = torch.device("cuda", 0)
@@ -28,7 +32,7 @@ hist = eng.history
 stream = gen_stream_torch(torch, dev, fs, hist + 2 * pairs * block, modes, offs)
 base = stream.data_ptr() + 8 * hist
 torch.cuda.synchronize()
-mi = {m: np.array([i for i, x in enumerate(modes) if x == m]) for m in ("nfm", "usb", "cw")}
+mi = {m: np.array([i for i, x in enumerate(modes) if x == m]) for m in mset}
 last = eng.stats()
 for p in range(pairs):
     for j in (2 * p, 2 * p + 1):
