@@ -858,8 +858,12 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
         // gain samples of a chunk: j % 8 in {0, 1} (wave 1), {2, 3, 4} (wave 2), {5, 6, 7} (3);
         // fully unrolled per wave (no inner loop: a loop header would make the compiler wait
         // for wave 1's in-flight loads before the gain work instead of after it)
-        auto gain = [&](auto lo_c, auto cnt_c, int ch) {
+        // the audioBuffer tap is rare: its per-sample store test only in the instantiation
+        // that has one (wave-uniform choice)
+        const bool any_tap = __any(tap_lim > 0);
+        auto gain = [&](auto lo_c, auto cnt_c, auto tap_c, int ch) {
             constexpr int LO = decltype(lo_c)::value, CNT = decltype(cnt_c)::value;
+            constexpr bool TAP = decltype(tap_c)::value;
             const int base = ch * kSerChunk;
             const float2(*srcu)[64] = ue[ch & 1];
             const bool full = ch < nfull;
@@ -872,12 +876,14 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
                     float a;
                     {
 #pragma clang fp contract(off)
-                        float g = (q.y > 0.0f) ? g_ref / q.y : g_max;
-                        if (g > g_max) g = g_max;
+                        // (q.y > 0 ? reference / q.y : max_gain) clamped to max_gain: the envelope
+                        // is never negative or -0, and reference / +0 = +inf clamps to max_gain,
+                        // so one min (no compare / select pairs and their wait states)
+                        const float g = fminf(g_ref / q.y, g_max);
                         a = g * q.x;
                     }
                     as_[ch & 1][j][lane] = a;
-                    {   // audioBuffer readers (a secondary demodulator on the audio)
+                    if (TAP) {  // audioBuffer readers (a secondary demodulator on the audio)
                         const int qi = base + j;
                         if ((full || qi < n) && qi < tap_lim) gp(tap)[qi] = a;
                     }
@@ -901,9 +907,15 @@ post_serial_front(const ChainPost* __restrict__ posts, ChainCounts* __restrict__
             if (ld) stage_load(it + 1);
             const int ch = it - 1;
             if (ch >= 0 && ch < nchunks) {
-                if (wave == 1) gain(I0{}, I2{}, ch);
-                else if (wave == 2) gain(I2{}, I3{}, ch);
-                else gain(I5{}, I3{}, ch);
+                if (any_tap) {
+                    if (wave == 1) gain(I0{}, I2{}, std::true_type{}, ch);
+                    else if (wave == 2) gain(I2{}, I3{}, std::true_type{}, ch);
+                    else gain(I5{}, I3{}, std::true_type{}, ch);
+                } else {
+                    if (wave == 1) gain(I0{}, I2{}, std::false_type{}, ch);
+                    else if (wave == 2) gain(I2{}, I3{}, std::false_type{}, ch);
+                    else gain(I5{}, I3{}, std::false_type{}, ch);
+                }
             }
             const int w = it - 2;  // chunk written out this iteration (as_ complete since the
             if (w >= 0 && wave >= 2) {  // previous barrier); quads alternate waves 2, 3
