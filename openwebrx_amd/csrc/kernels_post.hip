@@ -1118,11 +1118,13 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t wv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                    // each code enters at the top nibble and the word shifts down by one
+                    // (alignbit: one instruction; the record index's high bits fall off)
                     uint32_t acc = 0;
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
                         const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
-                        acc |= (adpcm_encode_rem(ad, x, NS) & 15u) << (4 * t);
+                        acc = __builtin_amdgcn_alignbit(adpcm_encode_rem(ad, x, NS), acc, 4);
                     }
                     w[k] = acc ^ 0x77777777u;
                 }
