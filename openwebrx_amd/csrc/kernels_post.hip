@@ -215,7 +215,25 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
         if (tid < kFdHist) ddc_l[tid] = ddc_g[tid];
         sh_x[tid] = fd_buf[tid];  // kBpHist == NT
     }
-    {   // segment partials: 8 independent loads in flight per thread, summed in segment order
+    if (P.nseg == 1 && P.output != OWRX_OUT_IQ) {
+        // one segment (the fast-convolution DDC): eight outputs' loads in flight per thread (the
+        // index clamped, not branched on, so the compiler issues them together) -- a load per
+        // loop iteration left ~10 full L2 / HBM round trips per thread back to back
+        const auto src = partial + (int64_t)P.chain_in_group * P.nk + col0;
+        for (int i0 = 0; i0 < n_new; i0 += 8 * NT) {
+            float2 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = src[min(i0 + u * NT + tid, n_new - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * NT + tid;
+                if (i >= n_new) break;
+                const float2 y = make_float2(0.0f + v[u].x, 0.0f + v[u].y);  // as the sum below
+                if (P.debug && i < P.dbg_cap) P.dbg_ddc[i] = y;
+                ddc_buf[kFdHist + i] = y;
+            }
+        }
+    } else {   // segment partials: 8 independent loads in flight per thread, summed in segment order
         const int64_t sstride = (int64_t)P.group_chains * P.nk;
         const int nseg = P.nseg;
         for (int i = tid; i < n_new; i += NT) {
@@ -366,7 +384,15 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     }();
     if constexpr (FUSED) {
         __syncthreads();  // every read of the DDC outputs (interpolator history) is done
-        for (int j = tid; j < pend; j += NT) sq_l[j] = sq_g[j];
+        // the pending squelch samples: four loads in flight per thread (clamped index)
+        for (int j0 = 0; j0 < pend; j0 += 4 * NT) {
+            float2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = sq_g[min(j0 + u * NT + tid, pend - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j0 + u * NT + tid < pend) sq_l[j0 + u * NT + tid] = v[u];
+        }
         for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
         __syncthreads();
     } else if (lds_bp) {
@@ -382,31 +408,30 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
         const auto x = fd_win + kBpHist + j;
         float2 y;
         if (lds_bp) {
+            // packed FP32 (v_pk_fma_f32): each complex MAC is two packed FMAs -- (re, im) +=
+            // (g.x, g.x) (v.x, v.y), then += (-g.y, g.y) (v.y, v.x) -- the same FMA sequence per
+            // accumulator as four scalar FMAs (bit-identical) at half the instructions; even taps
+            // in a, odd in b
+            typedef float bp_f2 __attribute__((ext_vector_type(2)));
             const float2* xs = sh_x + kBpHist + j;
-            float ar = 0.0f, ai = 0.0f, br = 0.0f, bi = 0.0f;
+            bp_f2 a = bp_f2{0.0f, 0.0f}, b = bp_f2{0.0f, 0.0f};
             int t = 0;
 #pragma unroll 4
             for (; t + 1 < nbt; t += 2) {
                 const float2 g0 = sh_taps[t], g1 = sh_taps[t + 1];
                 const float2 v0 = xs[-t], v1 = xs[-t - 1];
-                ar = fmaf(g0.x, v0.x, ar);
-                ar = fmaf(-g0.y, v0.y, ar);
-                ai = fmaf(g0.x, v0.y, ai);
-                ai = fmaf(g0.y, v0.x, ai);
-                br = fmaf(g1.x, v1.x, br);
-                br = fmaf(-g1.y, v1.y, br);
-                bi = fmaf(g1.x, v1.y, bi);
-                bi = fmaf(g1.y, v1.x, bi);
+                a = __builtin_elementwise_fma(bp_f2{g0.x, g0.x}, bp_f2{v0.x, v0.y}, a);
+                a = __builtin_elementwise_fma(bp_f2{-g0.y, g0.y}, bp_f2{v0.y, v0.x}, a);
+                b = __builtin_elementwise_fma(bp_f2{g1.x, g1.x}, bp_f2{v1.x, v1.y}, b);
+                b = __builtin_elementwise_fma(bp_f2{-g1.y, g1.y}, bp_f2{v1.y, v1.x}, b);
             }
             if (t < nbt) {
                 const float2 g0 = sh_taps[t];
                 const float2 v0 = xs[-t];
-                ar = fmaf(g0.x, v0.x, ar);
-                ar = fmaf(-g0.y, v0.y, ar);
-                ai = fmaf(g0.x, v0.y, ai);
-                ai = fmaf(g0.y, v0.x, ai);
+                a = __builtin_elementwise_fma(bp_f2{g0.x, g0.x}, bp_f2{v0.x, v0.y}, a);
+                a = __builtin_elementwise_fma(bp_f2{-g0.y, g0.y}, bp_f2{v0.y, v0.x}, a);
             }
-            y = make_float2(ar + br, ai + bi);
+            y = make_float2(a.x + b.x, a.y + b.y);
         } else if (nbt > 0) {
             float ar = 0.0f, ai = 0.0f;
             for (int t = 0; t < nbt; ++t) {
