@@ -342,6 +342,7 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
     int cur[8], nxt[8];
     for (int q = 0; q < 8; ++q) cur[q] = src[q];
     const long long t0 = clock64();
+    const long long r0 = wall_clock64();
     for (int j = 0; j < n; j += 8) {
         for (int q = 0; q < 8; ++q) nxt[q] = src[j + 8 + q];
         uint32_t w = 0;
@@ -377,7 +378,11 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
         for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
     }
     const long long t1 = clock64();
-    if (lane == 0) *cyc = t1 - t0;
+    const long long r1 = wall_clock64();
+    if (lane == 0) {
+        cyc[0] = t1 - t0;
+        cyc[1] = r1 - r0;
+    }
 }
 
 int main() {
@@ -401,15 +406,19 @@ int main() {
     hipMemcpy(dx, h.data(), h.size() * 2, hipMemcpyHostToDevice);
     hipMalloc(&d0, (size_t)S * n);
     hipMalloc(&d1, (size_t)S * n);
-    hipMalloc(&dc, 8);
+    hipMalloc(&dc, 16);
     auto run = [&](const char* name, void (*k)(const int16_t*, int, uint8_t*, long long*), uint8_t* o) {
-        long long cyc = 0;
+        long long cyc[2] = {0, 0};
         for (int rep = 0; rep < 5; ++rep) {
             hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, dx, n, o, dc);
             hipDeviceSynchronize();
         }
-        hipMemcpy(&cyc, dc, 8, hipMemcpyDeviceToHost);
-        printf("%-44s %7.1f cycles/sample (%s)\n", name, cyc / (double)n, hipGetErrorString(hipGetLastError()));
+        hipMemcpy(cyc, dc, 16, hipMemcpyDeviceToHost);
+        int wrate = 0;
+        hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, 0);  // kHz
+        const double ns = cyc[1] * 1e6 / (double)wrate / n;
+        printf("%-44s %7.1f cycles/sample, %6.1f ns/sample (%.2f GHz) (%s)\n", name, cyc[0] / (double)n, ns,
+               cyc[0] / (double)n / ns, hipGetErrorString(hipGetLastError()));
     };
     run("tab2 (production chain_adpcm encoder)", kern<0>, d0);
     run("threshold records (64 B successor records)", kern<1>, d1);
