@@ -404,7 +404,55 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
         if constexpr (FUSED) return sh_x;
         else return fd_buf;
     }();
-    for (int j = tid; j < (P.bp_long ? 0 : n_fd); j += NT) {
+    typedef float bp_f2 __attribute__((ext_vector_type(2)));
+    int j = tid;
+    if (lds_bp) {
+        // four outputs per thread in flight (j, j + NT, j + 2 NT, j + 3 NT): each output is two
+        // dependent FMA chains of ~nbt steps, so one output at a time left the loop latency-bound
+        // (~55 cycles per tap and output; phase stamps: 30-40 of post_parallel's ~50 us per C3
+        // pair).  Per output the FMA order is unchanged (bit-identical); the block's x reads sit
+        // at constant offsets (r NT) from one address.  Whole blocks only; the rest below.
+        constexpr int kBpR = 4;
+        for (; j + (kBpR - 1) * NT < n_fd; j += kBpR * NT) {
+            const float2* xs = sh_x + kBpHist + j;
+            bp_f2 a[kBpR], b[kBpR];
+#pragma unroll
+            for (int r = 0; r < kBpR; ++r) a[r] = b[r] = bp_f2{0.0f, 0.0f};
+            int t = 0;
+#pragma unroll 2
+            for (; t + 1 < nbt; t += 2) {
+                const float2 g0 = sh_taps[t], g1 = sh_taps[t + 1];
+#pragma unroll
+                for (int r = 0; r < kBpR; ++r) {
+                    const float2 v0 = xs[r * NT - t], v1 = xs[r * NT - t - 1];
+                    a[r] = __builtin_elementwise_fma(bp_f2{g0.x, g0.x}, bp_f2{v0.x, v0.y}, a[r]);
+                    a[r] = __builtin_elementwise_fma(bp_f2{-g0.y, g0.y}, bp_f2{v0.y, v0.x}, a[r]);
+                    b[r] = __builtin_elementwise_fma(bp_f2{g1.x, g1.x}, bp_f2{v1.x, v1.y}, b[r]);
+                    b[r] = __builtin_elementwise_fma(bp_f2{-g1.y, g1.y}, bp_f2{v1.y, v1.x}, b[r]);
+                }
+            }
+            if (t < nbt) {
+                const float2 g0 = sh_taps[t];
+#pragma unroll
+                for (int r = 0; r < kBpR; ++r) {
+                    const float2 v0 = xs[r * NT - t];
+                    a[r] = __builtin_elementwise_fma(bp_f2{g0.x, g0.x}, bp_f2{v0.x, v0.y}, a[r]);
+                    a[r] = __builtin_elementwise_fma(bp_f2{-g0.y, g0.y}, bp_f2{v0.y, v0.x}, a[r]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < kBpR; ++r) {
+                const int jr = j + r * NT;
+                const float2 y = make_float2(a[r].x + b[r].x, a[r].y + b[r].y);
+                sq_buf[pend + jr] = y;
+                if (P.debug && jr < P.dbg_cap) {
+                    P.dbg_fd[jr] = xs[r * NT];
+                    P.dbg_bp[jr] = y;
+                }
+            }
+        }
+    }
+    for (; j < (P.bp_long ? 0 : n_fd); j += NT) {
         const auto x = fd_win + kBpHist + j;
         float2 y;
         if (lds_bp) {
@@ -412,7 +460,6 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
             // (g.x, g.x) (v.x, v.y), then += (-g.y, g.y) (v.y, v.x) -- the same FMA sequence per
             // accumulator as four scalar FMAs (bit-identical) at half the instructions; even taps
             // in a, odd in b
-            typedef float bp_f2 __attribute__((ext_vector_type(2)));
             const float2* xs = sh_x + kBpHist + j;
             bp_f2 a = bp_f2{0.0f, 0.0f}, b = bp_f2{0.0f, 0.0f};
             int t = 0;
