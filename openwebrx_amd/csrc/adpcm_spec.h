@@ -19,11 +19,15 @@ namespace owrx {
 // encoder (oracle orc_adpcm_encode / orc_fft_adpcm_row).
 constexpr int kSpecThreads = 256;
 
-OWRX_DEV uint32_t pack_state(const AdpcmTab& s) {
+OWRX_DEV uint32_t pack_state(const AdpcmRem& s) {
     return ((uint32_t)s.index() << 16) | ((uint32_t)s.pred & 0xffffu);
 }
-OWRX_DEV AdpcmTab unpack_state(uint32_t v) {
-    return AdpcmTab{adpcm_tab_rec((int)(v >> 16)), (int)(int16_t)(v & 0xffffu)};
+OWRX_DEV AdpcmRem unpack_state(uint32_t v) {
+    return adpcm_rem_state(AdpcmState{(int)(v >> 16), (int)(int16_t)(v & 0xffffu)});
+}
+// one sample with the remainder-form encoder (owrx_dev.h): its 4-bit code
+OWRX_DEV uint8_t spec_encode(AdpcmRem& s, int x, const uint2* __restrict__ NSR) {
+    return (uint8_t)((adpcm_encode_rem(s, x, NSR) & 15u) ^ 7u);
 }
 
 // Segment-transposed LDS layout: sample t of the window lives at (t % seg) * S + t / seg, so
@@ -45,7 +49,8 @@ OWRX_DEV int spec_at(const SpecGeom& g, int t) { return (t % g.seg) * g.S + t / 
 template <int WIN>
 struct SpecLds {
     static constexpr int kCap = WIN + 2 * ((WIN / kSpecThreads + 2) > 64 ? (WIN / kSpecThreads + 2) : 64) + 2;
-    uint32_t NS[kAdpcmTabEntries];  // adpcm_encode_tab successor table (16-B aligned rows)
+    uint2 NSR[kAdpcmRemEntries];  // adpcm_encode_rem successor records (round 5: ~25 % fewer
+                                  // cycles per sample than the table step it replaced)
     int16_t x[kCap];
     uint8_t code[kCap];
     uint32_t traj[kCap];
@@ -68,14 +73,14 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, const SpecGeom& g, uint3
     const int16_t* T = L.T;
     // pass 1
     if (tid < nseg) {
-        AdpcmTab st;
+        AdpcmRem st;
         if (tid == 0) {
             st = unpack_state(start);
         } else {
             // the previous segment's last samples: x[b0 - 1], x[b0 - 2] at the tail of lane tid-1
             const int prev1 = (int)L.x[(seg - 1) * S + tid - 1];
             if (guess_index >= 0) {
-                st = AdpcmTab{adpcm_tab_rec(guess_index), prev1};
+                st = adpcm_rem_state(AdpcmState{guess_index, prev1});
             } else {
                 // predictor = previous sample, step index from the local slope
                 const int d = abs(prev1 - (int)L.x[(seg - 2) * S + tid - 1]);
@@ -84,12 +89,12 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, const SpecGeom& g, uint3
                     const int mid = (lo + hi) >> 1;
                     if (T[mid] < d) lo = mid + 1; else hi = mid;
                 }
-                st = AdpcmTab{adpcm_tab_rec(lo), prev1};
+                st = adpcm_rem_state(AdpcmState{lo, prev1});
             }
         }
         L.seg_start[tid] = pack_state(st);
         for (int j = 0, a = tid; j < len; ++j, a += S) {
-            L.code[a] = (uint8_t)adpcm_encode_tab(st, L.x[a], L.NS);
+            L.code[a] = spec_encode(st, L.x[a], L.NSR);
             L.traj[a] = pack_state(st);
         }
         L.seg_final[tid] = pack_state(st);
@@ -107,10 +112,10 @@ OWRX_DEV void adpcm_spec_window(SpecLds<WIN>& L, int n, const SpecGeom& g, uint3
         }
         __syncthreads();  // every start was read before any final changes
         if (rerun) {
-            AdpcmTab r = unpack_state(want);
+            AdpcmRem r = unpack_state(want);
             bool merged = false;
             for (int j = 0, a = tid; j < len; ++j, a += S) {
-                L.code[a] = (uint8_t)adpcm_encode_tab(r, L.x[a], L.NS);
+                L.code[a] = spec_encode(r, L.x[a], L.NSR);
                 const uint32_t ps = pack_state(r);
                 if (ps == L.traj[a]) {
                     merged = true;

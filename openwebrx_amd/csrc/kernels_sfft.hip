@@ -50,7 +50,7 @@ chain_sfft(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ counts
     int rf = ps->sf_row_frame;
     if (adpcm) {
         for (int i = tid; i < 89; i += kSfThreads) S.enc.T[i] = kAdpcmStep[i];
-        adpcm_tab_fill(S.enc.NS, tid, kSfThreads);
+        adpcm_rem_fill(S.enc.NSR, tid, kSfThreads);
     }
     float acc[PPT];
 #pragma unroll

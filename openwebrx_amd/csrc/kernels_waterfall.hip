@@ -1414,7 +1414,7 @@ wf_adpcm_rows_spec(const int16_t* __restrict__ s16, int N, int nrows, uint8_t* _
     SpecLds<kRowWin>& L = *reinterpret_cast<SpecLds<kRowWin>*>(smem);
     const int tid = threadIdx.x;
     for (int i = tid; i < 89; i += kSpecThreads) L.T[i] = kAdpcmStep[i];
-    adpcm_tab_fill(L.NS, tid, kSpecThreads);
+    adpcm_rem_fill(L.NSR, tid, kSpecThreads);
     const int M = N + 10;
     // rows dealt round-robin over a grid that fits its CUs at once (launch_wf_adpcm)
     for (int row = blockIdx.x; row < nrows; row += gridDim.x) {
