@@ -380,9 +380,11 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
     passed = [l["chains"] for l in levels if l.get("keeps_up")]
     if best and hold_s > 0:
         # the top passing level once more, held for hold_s of stream (60 s); if
-        # it does not keep up that long, the level below it once
+        # it does not keep up that long, the passing levels below it in turn, at most three
+        # holds in all (one slow block of 572 fails a hold: round 5's driver-form run failed it
+        # at 196 608 and 131 072 chains, each on one 140-440 ms block)
         import gc
-        for C in passed[::-1][:2]:
+        for C in passed[::-1][:3]:
             gc.collect()  # the failed level's Python objects (its engine is closed already)
             _log("capacity hold: %d chains for %.0f s" % (C, hold_s))
             ms = [modes[c % len(modes)] for c in range(C)]
