@@ -2478,7 +2478,21 @@ static hipError_t create_streams(owrx_engine* e) {
     const std::vector<uint32_t> mB = mask_range(a_end, a_end + nb);
     const std::vector<uint32_t> mC = mask_range(a_end + nb, a_end + nb + nc);
     const std::vector<uint32_t> mR = mask_range(a_end + nb + nc, a_end + nb + nc + nr);
-    const std::vector<uint32_t> mW = nw > 0 ? mask_range(a_end + nb + nc + nr, ncu) : mR;
+    std::vector<uint32_t> mW = nw > 0 ? mask_range(a_end + nb + nc + nr, ncu) : mR;
+    // The row encoders may also use stream A's CUs, one workgroup per row, so a batch's rows (one
+    // ~129 KiB-LDS workgroup each, near-serial per row) run side by side instead of eight at a
+    // time on the row queue's own 4 CUs: a 35-row batch took ~2.4 ms there, and the last one
+    // ended the 20-step C3 bench ~1.5 ms after the chain work (7 934-8 622 -> 9 373-9 555 Msps,
+    // profiles/r05_rows_wide_ab.txt).  OWRX_ROWS_WIDE=0: the row queue's own CUs only (A/B).
+    static const bool rows_wide = [] {
+        const char* v = getenv("OWRX_ROWS_WIDE");
+        return !(v && strcmp(v, "0") == 0);
+    }();
+    if (rows_wide) {
+        const std::vector<uint32_t> mAw = mask_range(0, a_end);
+        for (size_t i = 0; i < mW.size(); ++i) mW[i] |= mAw[i];
+        e->rows_grid = 0;
+    }
     // Hardware queues and the command processor's pipes.  Every CU-masked stream is an HSA
     // queue of its own, and a process's queues are spread over the CP's four compute pipes in
     // creation order (measured: the 1st, 5th and 9th masked queue share one).  A queue holding a
