@@ -2491,7 +2491,7 @@ static hipError_t create_streams(owrx_engine* e) {
     if (rows_wide) {
         const std::vector<uint32_t> mAw = mask_range(0, a_end);
         for (size_t i = 0; i < mW.size(); ++i) mW[i] |= mAw[i];
-        e->rows_grid = 0;
+        if (!getenv("OWRX_ROWS_GRID")) e->rows_grid = 0;  // (an explicit grid still wins)
     }
     // Hardware queues and the command processor's pipes.  Every CU-masked stream is an HSA
     // queue of its own, and a process's queues are spread over the CP's four compute pipes in
