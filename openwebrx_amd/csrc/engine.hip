@@ -1050,6 +1050,24 @@ static int flush_zero(owrx_engine* e) {
     return OWRX_OK;
 }
 
+// Device buffer zeroed on stream A with the other pending zeroing (one zero_jobs launch) instead
+// of dalloc's synchronous hipMemset (a fillBufferAligned dispatch per buffer): for the slot and
+// group buffers that capacity growth reallocates between blocks, after a drain.  The caller
+// flushes the zeroing before anything can free the buffer again (flush_zero).
+template <typename T>
+static hipError_t dalloc_z(owrx_engine* e, T** p, size_t count) {
+    *p = nullptr;
+    const size_t bytes = (sizeof(T) * std::max<size_t>(count, 1) + 255) & ~(size_t)255;
+    const hipError_t r = hipMalloc((void**)p, bytes);
+    if (r != hipSuccess) {
+        (void)hipGetLastError();  // not sticky for the next launch (see dalloc)
+        *p = nullptr;
+        return r;
+    }
+    e->zero_pending.push_back({(void*)*p, (int64_t)bytes});
+    return hipSuccess;
+}
+
 // The filter-spectra builds of the chains that joined since the last flush, one launch per
 // group (W is zeroed by fc_reserve before any build writes it).  Before anything that copies or
 // moves W rows (fc_reserve's regrowth, a leave's swap-remove) and with every upload flush.
@@ -1454,26 +1472,27 @@ static int ensure_post_capacity(owrx_engine* e) {
     for (int si = 0; si < e->nslots; ++si) {
         Slot& s = e->slots[si];
         free_slot_staging(s);
-        HIPCHK(dalloc(&s.d_posts, cap));
+        HIPCHK(dalloc_z(e, &s.d_posts, cap));
         HIPCHK(halloc(&s.h_posts, cap));
         // serial lane lists (+ demodulator-run padding), then the long-bandpass post list and
         // chain_afc's list (a RawSAm chain at 48 kHz is on both: up to cap entries each)
-        HIPCHK(dalloc(&s.d_sel, (size_t)3 * cap + kSelPad));
+        HIPCHK(dalloc_z(e, &s.d_sel, (size_t)3 * cap + kSelPad));
         HIPCHK(halloc(&s.h_sel, (size_t)3 * cap + kSelPad));
-        HIPCHK(dalloc(&s.d_counts, cap));
-        HIPCHK(dalloc(&s.d_out, (size_t)e->out_total));
-        HIPCHK(dalloc(&s.d_sm, (size_t)cap * e->sm_stride));
+        HIPCHK(dalloc_z(e, &s.d_counts, cap));
+        HIPCHK(dalloc_z(e, &s.d_out, (size_t)e->out_total));
+        HIPCHK(dalloc_z(e, &s.d_sm, (size_t)cap * e->sm_stride));
         HIPCHK(halloc(&s.h_counts, (size_t)cap));
         HIPCHK(halloc(&s.h_out, (size_t)e->out_total));
         HIPCHK(halloc(&s.h_sm, (size_t)cap * e->sm_stride));
         if (!s.h_jobs) HIPCHK(halloc(&s.h_jobs, (size_t)kMaxCopyJobs));
         s.post_dirty = true;
         if (e->debug) {
-            HIPCHK(dalloc(&s.d_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
+            HIPCHK(dalloc_z(e, &s.d_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
             HIPCHK(halloc(&s.h_dbg, (size_t)cap * kDebugStages * e->dbg_stride));
         }
     }
     e->post_cap = cap;
+    RCCHK(flush_zero(e));  // the new buffers' zeroing, one launch (see dalloc_z)
     return OWRX_OK;
 }
 
@@ -1485,8 +1504,9 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         dfree(g->d_chains);
         for (auto& h : g->h_chains) hfree(h);
         g->chains_cap = std::max(n, 2 * g->chains_cap);
-        HIPCHK(dalloc(&g->d_chains, (size_t)g->chains_cap));
+        HIPCHK(dalloc_z(e, &g->d_chains, (size_t)g->chains_cap));
         for (auto& h : g->h_chains) HIPCHK(halloc(&h, (size_t)g->chains_cap));
+        RCCHK(flush_zero(e));
     }
     const int64_t nk_max = proc_block(e) / g->D + 4;
     // Launch shape: each tile group's D phases are split into nseg segments, one 4-wave
@@ -1517,8 +1537,9 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         const size_t alloc = need + need / 2;
         for (int i = 0; i < e->nslots; ++i) {  // the depth is fixed before the first chain
             dfree(g->d_partial[i]);
-            HIPCHK(dalloc(&g->d_partial[i], alloc));
+            HIPCHK(dalloc_z(e, &g->d_partial[i], alloc));
         }
+        RCCHK(flush_zero(e));
         g->partial_elems = alloc;
     }
     g->nseg = nseg;
@@ -1529,7 +1550,8 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
         if (ny > g->fc_y_elems) {
             RCCHK(drain_all(e));
             dfree(g->d_fc_y);
-            HIPCHK(dalloc(&g->d_fc_y, ny + ny / 2));
+            HIPCHK(dalloc_z(e, &g->d_fc_y, ny + ny / 2));
+            RCCHK(flush_zero(e));
             g->fc_y_elems = ny + ny / 2;
         }
     }
