@@ -377,7 +377,9 @@ OWRX_DEV uint32_t adpcm_encode_rem(AdpcmRem& s, int sample, const uint2* __restr
     acc = __builtin_amdgcn_alignbit(acc, u1, 31);
     const uint32_t a3 = min(a2, u1);
     const uint2 r = NSR[acc];
-    const int dq = (int)(((w1 & 0xffffu) >> 2) + (a0 - a3));
+    // dq = (step >> 3) + a0 - a3 with a0 >= a3: the |a0 - a3| + s3 form is one v_sad_u32
+    const uint32_t s3 = (w1 & 0xffffu) >> 2;
+    const int dq = (int)((a0 > a3 ? a0 - a3 : a3 - a0) + s3);
     s.w0 = r.x;
     s.w1 = r.y;
     const int p = s.pred + ((dq ^ sgn) - sgn);
