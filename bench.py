@@ -850,11 +850,13 @@ def main():
     # the capacity ladder's engines keep the default 8 (their staging grows with the chains)
     depth = int(os.environ.get("OWRX_BENCH_DEPTH", "16"))
     eng.set_pipeline_depth(depth)
-    # block pairing (owrx_set_block_pairing) where consecutive blocks are contiguous in memory
-    # (rank 0's recording; the broadcast windows of ranks > 0 are not): two 2^20-sample blocks per
-    # engine launch sequence, the DDC GEMM reading the filter spectra once for both, outputs
-    # byte-identical (test_block_pairing_same_outputs)
-    pairing = rank == 0 and not args.no_pairing and retention >= 4
+    # block pairing (owrx_set_block_pairing) on every rank: two 2^20-sample blocks per engine
+    # launch sequence, the DDC GEMM reading the filter spectra once for both, outputs
+    # byte-identical (test_block_pairing_same_outputs).  A pair must be contiguous in memory:
+    # rank 0's recording is, and ranks > 0 receive each pair in one broadcast into one
+    # [history | 2 blocks] window (IqBroadcast(pair=True), round 6), so every rank runs the N = 1
+    # engine
+    pairing = not args.no_pairing and retention >= 4
     if pairing:
         eng.set_block_pairing(True)
     hist = eng.history
@@ -895,7 +897,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         hist_b = int(t.item())
         src_view = stream[hist - hist_b:] if rank == 0 else None
-        bcast = IqBroadcast(torch, dist, dev, hist_b, block, stream=src_view, retention=retention)
+        bcast = IqBroadcast(torch, dist, dev, hist_b, block, stream=src_view, retention=retention,
+                            pair=pairing)
     torch.cuda.synchronize(dev)
 
     def drain():

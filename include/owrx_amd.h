@@ -106,7 +106,8 @@ int owrx_wait_stream(owrx_engine* e, void* stream);
  * blocks = r the block handed to owrx_process_device (with its history) must stay unmodified
  * until r further owrx_process_device / owrx_commit calls (or owrx_sync) have returned, and the
  * engine waits only for block k - r + 1's stream-A work before returning from block k, so the
- * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 31. */
+ * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 31, and
+ * r >= 4 while block pairing is on (OWRX_EINVAL otherwise). */
 int owrx_set_input_retention(owrx_engine* e, int blocks);
 /* Block pairing (enable = 1; input retention >= 4, before the first chain, waterfall and block):
  * owrx_process_device holds a block until the next call; when the next block follows it in

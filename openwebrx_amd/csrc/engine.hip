@@ -907,9 +907,24 @@ static int flush_uploads(owrx_engine* e);
 // release to the pool once the blocks enqueued so far have drained.  Pending uploads are
 // enqueued first: one may target this buffer, and its next owner's zeroing and upload must run
 // after it (copy_jobs does not order jobs to the same destination within a launch).
+// A failed flush (a timed-out staging wait, no pinned memory) leaves its uploads and zeroing
+// queued; one of them may target the buffer being released, which the pool then hands to another
+// chain, so the later flush would write stale bytes over that chain's fresh state.  The queued
+// work is dropped instead and the engine fails (every later call returns the error).
+static void flush_before_release(owrx_engine* e) {
+    if (e->up_jobs.empty()) return;
+    if (flush_uploads(e) != OWRX_OK) {
+        e->up_jobs.clear();
+        e->up_data.clear();
+        e->up_index.clear();
+        e->zero_pending.clear();
+        e->failed = true;
+    }
+}
+
 template <typename T>
 static void prel(owrx_engine* e, T*& p) {
-    if (p && !e->up_jobs.empty()) (void)flush_uploads(e);
+    if (p) flush_before_release(e);
     if (p) e->pool_retired.push_back({e->block_index, (void*)p});
     p = nullptr;
 }
@@ -944,7 +959,7 @@ static void hprel_now(owrx_engine* e, T*& p) {
 }
 template <typename T>
 static void prel_now(owrx_engine* e, T*& p) {
-    if (p && !e->up_jobs.empty()) (void)flush_uploads(e);  // (see prel)
+    if (p) flush_before_release(e);  // (see prel)
     if (p) e->pool_free[e->pool_size[(void*)p]].push_back((void*)p);
     p = nullptr;
 }
@@ -1627,8 +1642,11 @@ static int fc_reserve(owrx_engine* e, ChainGroup* g, int slots) {
 // configuration (engine geometry and hop -- not the launch batching) and groups start at fixed
 // frame offsets of a row, so the summation order -- hence every row, bit for bit -- depends
 // neither on how the stream is cut into blocks nor on how frames are batched into launches:
-//  - N = 16384 and the DIF split (N = 16384 Q): 4 (micro-benchmark, C3 geometry, 960 frames
-//    from HBM: F = 4 49 us vs F = 2 55 us, profiles/r04*_wf_micro.txt);
+//  - N = 16384 on wf_fft_q16 (the default): 8 (wf_default_fpg; its group-end transpose and
+//    partial row amortise over twice the frames, 0.291 vs 0.275 of HBM at 3840 C3 frames,
+//    profiles/r05_wf_micro.txt); on wf_fft_l32 (OWRX_WF_KERNEL=l32) and after the DIF split
+//    (N = 16384 Q): 4 (C3 geometry, 960 frames from HBM: F = 4 49 us vs F = 2 55 us,
+//    profiles/r04*_wf_micro.txt);
 //  - wf_fft_r16: enough that a block's frames occupy stream A's CUs about once;
 //  - the four-step FFT (OWRX_WF_KERNEL=fourstep): one frame per group;
 // always clamped so that a group still open at a block's end fits the next block's history.
@@ -2734,6 +2752,12 @@ int owrx_set_input_retention(owrx_engine* e, int blocks) {
     ENGINE_GUARD(e);
     if (blocks < 1 || blocks >= kInEv) {
         set_last_error("owrx_set_input_retention: blocks must be in [1, %d]", kInEv - 1);
+        return OWRX_EINVAL;
+    }
+    // a paired engine holds a caller block until the next one arrives: pairing needs >= 4
+    // (owrx_set_block_pairing), so it may not be lowered below that afterwards
+    if (e->pair && blocks < 4) {
+        set_last_error("owrx_set_input_retention: block pairing is on, blocks must be >= 4");
         return OWRX_EINVAL;
     }
     e->retention = blocks;

@@ -639,11 +639,13 @@ int fc_kslices(int tiles, int Dp, int ncu) {
     const int per_wave = (Dp >> 3) / kFcKSplit;  // K-blocks per wave, unsliced
     auto ok = [&](int k) { return k >= 1 && k <= kFcMaxKSlices && per_wave % k == 0; };
     if (forced > 0) return ok(forced) ? forced : 1;
-    // a grid that already covers the CUs twice keeps whole K: C3's 384 tiles on 228 CUs ran 0.53
-    // of HBM unsliced vs 0.51 with 3 slices (profiles/r04_fc_kslices_c3.txt); C4's 128 and C5's
-    // 64 tiles gain 0.32 -> 0.48 and 0.25 -> 0.36 from slicing, and a paired C5 GEMM's 256 tiles
-    // (1.1 per CU) 0.26 -> 0.33 with 3 slices (profiles/r05_c5_kslices.txt)
-    if (tiles >= 2 * ncu) return 1;
+    // a grid of 1.5 or more workgroups per CU keeps whole K: C3's unpaired 384 tiles on 228 CUs
+    // (1.7 per CU; the push path, ranks run with --no-pairing) ran 0.53 of HBM unsliced vs 0.51
+    // with 3 slices (profiles/r04_fc_kslices_c3.txt, profiles/r05_c5_kslices.txt), and paired C3
+    // grids are twice that; C4's 128 and C5's 64 tiles gain 0.32 -> 0.48 and 0.25 -> 0.36 from
+    // slicing, and a paired C5 GEMM's 256 tiles (1.1 per CU) 0.26 -> 0.33 with 3 slices
+    // (round 5 moved the bound to 2 per CU, which sliced unpaired C3 too: ADVICE r05)
+    if (2 * tiles >= 3 * ncu) return 1;
     int best = 1;
     for (int k = 2; k <= kFcMaxKSlices; ++k) {
         if (!ok(k)) continue;

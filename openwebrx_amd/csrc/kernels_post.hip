@@ -29,6 +29,13 @@ constexpr int kPostThreads = 256;
 constexpr int kMaxSqBlocks = 1024;
 constexpr int kMaxSqLen = 3072;  // longest squelch block kept in registers while compacting
 constexpr int kBpLds = 6144;     // bandpass input window staged in LDS (48 KiB)
+// the staged bandpass on the f32 MFMA (bp_mfma_tiles, round 6); false keeps round 5's packed-FMA
+// direct form (A/B builds: -DOWRX_BP_FMA)
+#ifdef OWRX_BP_FMA
+constexpr bool kBpMfma = false;
+#else
+constexpr bool kBpMfma = true;
+#endif
 
 // 1 / prod_{j != i} (i - j) for the 12 Lagrange nodes
 OWRX_DEV float lagrange_den(int i) {
@@ -139,14 +146,66 @@ OWRX_DEV int wfm_audio(const ChainPost& P, ChainStateP& S, int nsq) {
 // 3125-tap complex FIR at 250 kHz) stops after section 1; bp_long then filters it across many
 // workgroups and PHASE 2 (post_tail) runs sections 3-4.
 // The workgroup's LDS, declared by each kernel (post_body has two instantiations in post_parallel)
+constexpr int kBpPad = kBpHist + 48;  // the bandpass taps zero-padded for the MFMA tiles (>= Kp + 16)
 struct PostLds {
     ChainStateP S;
     int n_fd;
     float2 taps[kBpHist + 1];
+    float2 hp[kBpPad];  // hp[k] = taps[k - p], zero outside [0, nbt) (bp_mfma_tiles)
     float2 x[kBpLds];  // the bandpass window; with FUSED the chain-block's whole working set
     float power[kMaxSqBlocks];
     uint8_t pass[kMaxSqBlocks];
 };
+
+// Bandpass (complex FIR, nbt taps) on the f32 MFMA: y[j] = sum_t h[t] x[j - t] for the n_fd
+// outputs of the window x[j] = win[kBpHist + j] (history below), written to out[j].  Tiles of 256
+// outputs j = j0 + 16 c + a are one 16 x 16 product D[c][a] = sum_s X[c][s] H[s][a] over
+// s < Kp = nbt + 15 (rounded up to 4): X[c][s] = x[j0 + 16 c + p - s], H[s][a] = h[a - p + s]
+// (p = Kp - nbt), so s runs over the taps t = a - p + s in ascending order and the zero taps
+// outside [0, nbt) are exact no-ops; complex as four real products per k-step (re: h.x x.x then
+// -h.y x.y; im: h.x x.y then h.y x.x).  v_mfma_f32_16x16x4_f32 is a k-ordered f32 fmaf chain
+// (cdna_hip_programming.md, FP32-input MFMA), and each output's row a is its absolute index mod
+// 16 (abs0 = that of j = 0), so every output's arithmetic is the same whatever the block cut:
+// paired / unpaired and sharded runs stay byte-identical.  One tile is 4 x Kp / 4 MFMAs of 32
+// cycles on one wave; the FMA form it replaces issued ~600 dependent VALU ops per output at one
+// wave per SIMD (30-40 of post_parallel's ~50 us per C3 pair, profiles/r05_post_parallel_phases.txt).
+// The window reads are clamped into [0, kBpHist + n_fd): only zero-tap products and outputs past
+// n_fd (not stored) see a clamped value, and it is a finite sample of the window.
+template <typename OUT, typename DBG>
+OWRX_DEV void bp_mfma_tiles(const float2* __restrict__ win, const float2* __restrict__ hp, int nbt,
+                            int n_fd, int64_t abs0, OUT out, DBG dbg) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int Kp = (nbt + 18) & ~3;
+    const int p = Kp - nbt;
+    const int a0 = (int)(abs0 & 15);
+    const int ntile = (n_fd + a0 + 255) >> 8;
+    const int xmax = kBpHist + n_fd - 1;
+    const float2* hq = hp + (lane & 15) + (lane >> 4);
+    for (int tl = wv; tl < ntile; tl += kPostThreads / 64) {
+        const int j0 = 256 * tl - a0;
+        const int xb = kBpHist + j0 + 16 * (lane & 15) + p - (lane >> 4);
+        f4 ar = {0.0f, 0.0f, 0.0f, 0.0f}, ai = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 6
+        for (int kc = 0; kc < Kp; kc += 4) {
+            const float2 xv = win[min(max(xb - kc, 0), xmax)];
+            const float2 hv = hq[kc];
+            ar = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, hv.x, ar, 0, 0, 0);
+            ai = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, hv.x, ai, 0, 0, 0);
+            ar = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, -hv.y, ar, 0, 0, 0);
+            ai = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, hv.y, ai, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int j = j0 + 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            if (j >= 0 && j < n_fd) {
+                const float2 y = make_float2(ar[r], ai[r]);
+                out(j, y);
+                dbg(j, win[kBpHist + j], y);
+            }
+        }
+    }
+}
 
 // FUSED (PHASE 0): the block's DDC outputs, FractionalDecimator output (the bandpass window) and
 // bandpass output stay in LDS -- stages 0-4 read and write the chain's global buffers only for
@@ -393,11 +452,27 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
             for (int u = 0; u < 4; ++u)
                 if (j0 + u * NT + tid < pend) sq_l[j0 + u * NT + tid] = v[u];
         }
-        for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
+        if (lds_bp && kBpMfma) {
+            const int Kp = (nbt + 18) & ~3;
+            for (int k = tid; k < Kp + 16; k += NT) {
+                const int t = k - (Kp - nbt);
+                Ls.hp[k] = (t >= 0 && t < nbt) ? bp_taps[t] : make_float2(0.0f, 0.0f);
+            }
+        } else {
+            for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
+        }
         __syncthreads();
     } else if (lds_bp) {
         for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[j] = fd_buf[j];
-        for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
+        if (kBpMfma) {
+            const int Kp = (nbt + 18) & ~3;
+            for (int k = tid; k < Kp + 16; k += NT) {
+                const int t = k - (Kp - nbt);
+                Ls.hp[k] = (t >= 0 && t < nbt) ? bp_taps[t] : make_float2(0.0f, 0.0f);
+            }
+        } else {
+            for (int t = tid; t < nbt; t += NT) sh_taps[t] = bp_taps[t];
+        }
         __syncthreads();
     }
     const auto fd_win = [&]() {
@@ -406,7 +481,17 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     }();
     typedef float bp_f2 __attribute__((ext_vector_type(2)));
     int j = tid;
-    if (lds_bp) {
+    if (lds_bp && kBpMfma) {
+        bp_mfma_tiles(
+            sh_x, Ls.hp, nbt, n_fd, S.fd_count, [&](int jj, float2 y) { sq_buf[pend + jj] = y; },
+            [&](int jj, float2 x0, float2 y) {
+                if (P.debug && jj < P.dbg_cap) {
+                    P.dbg_fd[jj] = x0;
+                    P.dbg_bp[jj] = y;
+                }
+            });
+        j = n_fd;
+    } else if (lds_bp) {
         // four outputs per thread in flight (j, j + NT, j + 2 NT, j + 3 NT): each output is two
         // dependent FMA chains of ~nbt steps, so one output at a time left the loop latency-bound
         // (~55 cycles per tap and output; phase stamps: 30-40 of post_parallel's ~50 us per C3

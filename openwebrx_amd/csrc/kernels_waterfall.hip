@@ -884,6 +884,29 @@ __host__ __device__ constexpr inline int q16_bin(int p) {
 // 4-6 and 12-13 (the lanes of one store differ in those), a bijection
 OWRX_DEV int wf_q16_lswz(int b) { return b ^ (((b >> 4) & 7) | (((b >> 12) & 3) << 3)); }
 
+// wf_fft_q16's butterflies and twiddle products: scalar FP32 (f2dft / f2mul) or packed (dft_r /
+// pk_mul: half the instructions, each issuing over twice the cycles; ABL 256, tools/micro A/B)
+template <bool PK>
+OWRX_DEV void q16_dft16(float2* a) {
+    if constexpr (PK) {
+        c2 t[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i] = c2_of(a[i]);
+        dft_r<16>(t);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a[i] = f2_of(t[i]);
+    } else {
+        f2dft<16>(a);
+    }
+}
+template <bool PK>
+OWRX_DEV float2 q16_mul(float2 a, float2 w) {
+    if constexpr (PK)
+        return f2_of(pk_mul(c2_of(a), c2_of(w)));
+    else
+        return f2mul(a, w);
+}
+
 template <int CTRL>
 OWRX_DEV float dppq(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
@@ -907,6 +930,8 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     constexpr int N = K::N, NT = K::NT;
     constexpr bool kSpread = (ABL & 8) != 0, kW16 = (ABL & 32) != 0, kLate = (ABL & 64) != 0;
     constexpr bool kSwapRev = (ABL & 128) != 0;
+    constexpr bool kPk = (ABL & 256) != 0;   // packed FP32 butterflies and twiddle products
+    constexpr bool kTbS = (ABL & 512) != 0;  // P1's W_256^(n1b k2) factor wave-uniform (SGPRs), not LDS
     constexpr int kUnits = kW16 ? 8 : 16;  // load instructions per thread per frame
     extern __shared__ __attribute__((aligned(16))) float2 sm[];
     __shared__ int s_next;
@@ -957,6 +982,13 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     const float2 t3v = tw[((t0 & 3) * ((t0 >> 2) & 15) * 256) & (N - 1)];   // [c][q], t0 < 64
     const float2 tav = tw[((t0 & 63) * (t0 >> 6)) & (N - 1)];               // [k2][n1a]
     const float2 tbv = tw[((t0 & 15) * ((t0 >> 4) & 15) * 64) & (N - 1)];   // [k2][n1b], t0 < 256
+    // kTbS: n1b = t >> 6 is the wave's index, so W_256^(n1b k2) is uniform over the wave
+    float2 tbs[16];
+    if constexpr (kTbS && !kW16) {
+        const int wv6 = __builtin_amdgcn_readfirstlane(t0 >> 6);
+#pragma unroll
+        for (int r = 1; r < 16; ++r) tbs[r] = tw[(64 * r * wv6) & (N - 1)];
+    }
     auto finish = [&]() {
         __syncthreads();
         if (t0 == 0 && atomicAdd(work + 1, 1) == (int)gridDim.x - 1) {
@@ -1054,15 +1086,20 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
             WF_WS(2);
             if (f == 1) WF_STAMP(1);
             // P1
-            f2dft<16>(a);
+            q16_dft16<kPk>(a);
             {
                 int tn = threadIdx.x;
                 asm volatile("" : "+v"(tn));
                 const int m1 = kW16 ? (tn & ~63) + 2 * (tn & 31) + ((tn >> 5) & 1) : tn;
                 const float2* TA = sm + K::TA + (m1 & 63);
                 const float2* TB = sm + K::TB + (m1 >> 6);
+                if constexpr (kTbS && !kW16) {
 #pragma unroll
-                for (int r = 1; r < 16; ++r) a[r] = f2mul(a[r], f2mul(TA[64 * r], TB[16 * r]));
+                    for (int r = 1; r < 16; ++r) a[r] = q16_mul<kPk>(a[r], q16_mul<kPk>(TA[64 * r], tbs[r]));
+                } else {
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) a[r] = q16_mul<kPk>(a[r], q16_mul<kPk>(TA[64 * r], TB[16 * r]));
+                }
             }
             if (f == 1) WF_STAMP(2);
             WF_PIN(a);
@@ -1089,9 +1126,9 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 #pragma unroll
                     for (int r = 0; r < 16; ++r) a[r] = img[p + 64 * r];
                 }
-                f2dft<16>(a);
+                q16_dft16<kPk>(a);
 #pragma unroll
-                for (int r = 1; r < 16; ++r) a[r] = f2mul(a[r], sm[K::TW2 + r * 64 + n1a]);
+                for (int r = 1; r < 16; ++r) a[r] = q16_mul<kPk>(a[r], sm[K::TW2 + r * 64 + n1a]);
                 if (f == 1) WF_STAMP(4);
                 WF_PIN(a);
                 WF_WS(9);
@@ -1115,9 +1152,9 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 #pragma unroll
                     for (int m = 0; m < 16; ++m) a[m] = img[base + 4 * m];
                 }
-                f2dft<16>(a);
+                q16_dft16<kPk>(a);
 #pragma unroll
-                for (int c = 1; c < 16; ++c) a[c] = f2mul(a[c], sm[K::TW3 + c * 4 + q]);
+                for (int c = 1; c < 16; ++c) a[c] = q16_mul<kPk>(a[c], sm[K::TW3 + c * 4 + q]);
                 const float s1 = q < 2 ? 1.0f : -1.0f;
                 const float s2 = (q == 0 || q == 3) ? 1.0f : -1.0f;
                 const bool q3 = q == 3;
@@ -1192,8 +1229,12 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 }
 
 // the product's variant: the next frame's loads after the first exchange's stores, spread
-// over the phases (tools/micro/wf_r05.hip: 0.29 vs 0.25 of HBM for wf_fft_l32 at 3840 C3 frames)
-constexpr int kWfQ16 = 72;
+// over the phases (tools/micro/wf_r05.hip: 0.29 vs 0.25 of HBM for wf_fft_l32 at 3840 C3 frames),
+// and P1's W_256^(n1b k2) factor from SGPRs (round 6, +512: half of P1's LDS table reads gone,
+// the same products, bit-identical rows; tools/micro/wf_r06.hip 0.258 vs 0.256 at 3480 frames,
+// 0.249 vs 0.244 at 1740).  The packed-FP32 butterflies (+256) measured no faster: 0.260 / 0.248,
+// and slower as VALU alone (0.405 vs 0.427; profiles/r06_wf_micro_a.txt, profiles/r06_fma_rate.txt)
+constexpr int kWfQ16 = 584;
 
 // ---- FFT sizes above one CU's LDS (32768, 65536): decimation-in-frequency split ------------
 // N = Q * 16384 (Q = 2, 4): X[Q k + j] = sum_n y_j[n] W_16384^(n k) with

@@ -6,9 +6,10 @@ wideband IQ broadcast from rank 0 as the only exchange step.
   chain per group.
 * IqBroadcast -- rank 0 owns the stream (host ingest or an HBM-resident recording); each
   block goes to every rank with one torch.distributed broadcast (RCCL over xGMI with the
-  "nccl" backend, gloo in the CPU tests).  Ranks > 0 assemble [history | block] windows,
-  rotating three, because the engine still reads block k (asynchronously) while k+1 arrives
-  and k+2's broadcast is already enqueued (owrx_process_device contract, include/owrx_amd.h).
+  "nccl" backend, gloo in the CPU tests).  Ranks > 0 assemble [history | block] windows (or
+  [history | 2 blocks] with pair=True, so their engines pair blocks as rank 0's does), rotating
+  enough of them for the engine's input retention (owrx_process_device contract,
+  include/owrx_amd.h).
 * Placement -- the same balance for the in-process drop-in (pycsdr shim, one engine per GPU
   in one OpenWebRX process), where chains come and go one at a time.
 No reduction: every rank returns its own chains' outputs to the host.
@@ -62,65 +63,81 @@ class IqBroadcast:
     broadcast of the next block overlaps this block's host and GPU work.  Ranks > 0 therefore
     rotate retention + 2 windows (three at retention 1): issue(i + 1) rewrites block
     i + 1 - nwin's window, which the engine has finished once owrx_process_device(i) returned
-    (owrx_set_input_retention's contract: blocks before k - retention + 1 are released)."""
+    (owrx_set_input_retention's contract: blocks before k - retention + 1 are released).
+
+    pair=True (ranks that run owrx_set_block_pairing, round 6): blocks 2u and 2u + 1 travel in
+    one broadcast into one window [history | block 2u | block 2u + 1], so on every rank the two
+    blocks of a pair are contiguous in memory and the engine runs them as one engine block,
+    exactly as rank 0 does on its resident recording.  A window then covers two blocks and the
+    ring holds retention // 2 + 3 of them."""
 
     NWIN = 3
 
-    def __init__(self, torch, dist, device, history, block, src=0, stream=None, retention=1):
+    def __init__(self, torch, dist, device, history, block, src=0, stream=None, retention=1,
+                 pair=False):
         self.torch, self.dist = torch, dist
         self.history, self.block, self.src = history, block, src
         self.rank = dist.get_rank()
         self.stream = stream  # rank src: complex64 tensor [history | blocks...]
-        self.pending = {}     # block -> async broadcast handle
-        self.next_issue = 0   # broadcasts are enqueued in block order on every rank
+        self.per = 2 if pair else 1  # blocks per broadcast (and per window)
+        self.pending = {}     # unit -> async broadcast handle
+        self.next_issue = 0   # broadcasts are enqueued in unit order on every rank
         # an engine with input retention r still reads blocks k - r + 1 .. k after
         # owrx_process_device(k) returned, and block k + 1's broadcast is issued before block k is
-        # processed: r + 2 windows (3 for r = 1)
-        self.nwin = max(self.NWIN, int(retention) + 2)
+        # processed: the units of blocks k - r .. k + 1 stay intact, r + 2 windows unpaired (3 for
+        # r = 1), r // 2 + 3 paired
+        if pair:
+            self.nwin = max(self.NWIN, int(retention) // 2 + 3)
+        else:
+            self.nwin = max(self.NWIN, int(retention) + 2)
         if self.rank != src:
-            self.windows = [torch.zeros(history + block, dtype=torch.complex64, device=device)
-                            for _ in range(self.nwin)]
+            self.windows = [torch.zeros(history + self.per * block, dtype=torch.complex64,
+                                        device=device) for _ in range(self.nwin)]
 
-    def _view(self, i):
-        h, b = self.history, self.block
-        lo = 0 if i == 0 else h  # the first broadcast also carries the initial history
+    def _view(self, u):
+        """Broadcast unit u: (the part that travels, the tensor holding it, offset of its first
+        block)."""
+        h, b = self.history, self.per * self.block
+        lo = 0 if u == 0 else h  # the first broadcast also carries the initial history
         if self.rank == self.src:
-            return self.stream[lo + i * b if i else 0: h + (i + 1) * b], self.stream, h + i * b
-        w = self.windows[i % self.nwin]
+            return self.stream[lo + u * b if u else 0: h + (u + 1) * b], self.stream, h + u * b
+        w = self.windows[u % self.nwin]
         return w[lo:h + b], w, h
 
     def issue(self, i):
         """Enqueue the broadcasts up to block i's (not waiting for them), in block order: the
         ranks' collectives must match one for one."""
-        while self.next_issue <= i:
+        u = i // self.per
+        while self.next_issue <= u:
             self._issue(self.next_issue)
             self.next_issue += 1
 
-    def _issue(self, i):
-        h, b = self.history, self.block
-        if self.rank != self.src and i > 0:
-            # the window starts with the previous block's last `history` samples: that block's
+    def _issue(self, u):
+        h, b = self.history, self.per * self.block
+        if self.rank != self.src and u > 0:
+            # the window starts with the previous unit's last `history` samples: that unit's
             # broadcast must land first (a stream-level wait with RCCL)
-            prev = self.pending.get(i - 1)
+            prev = self.pending.get(u - 1)
             if prev is not None:
                 prev.wait()
-            w, pw = self.windows[i % self.nwin], self.windows[(i - 1) % self.nwin]
+            w, pw = self.windows[u % self.nwin], self.windows[(u - 1) % self.nwin]
             w[:h].copy_(pw[b:b + h])
-        part, _, _ = self._view(i)
-        self.pending[i] = self.dist.broadcast(self.torch.view_as_real(part), src=self.src,
+        part, _, _ = self._view(u)
+        self.pending[u] = self.dist.broadcast(self.torch.view_as_real(part), src=self.src,
                                               async_op=True)
 
     def wait(self, i):
         """Block i's (tensor, offset) once its broadcast has landed (issued if it was not)."""
         self.issue(i)
-        w = self.pending.pop(i, None)
+        u = i // self.per
+        w = self.pending.pop(u, None)
         if w is not None:
             w.wait()
         # older handles whose windows issue(i) already waited for
-        for k in [k for k in self.pending if k < i]:
+        for k in [k for k in self.pending if k < u]:
             self.pending.pop(k)
-        _, t, off = self._view(i)
-        return t, off
+        _, t, off = self._view(u)
+        return t, off + (i % self.per) * self.block
 
     def step(self, i):
         """Unpipelined: broadcast block i and return it."""

@@ -569,6 +569,18 @@ def test_block_pairing_same_outputs(amd, fs, modes, B):
     assert a[2] == b[2]
 
 
+def test_retention_floor_while_paired(amd):
+    """Block pairing needs input retention >= 4 (owrx_set_block_pairing); lowering the retention
+    below that afterwards is refused, and the paired engine keeps its retention."""
+    eng = amd.Engine(2400000, max_block=1 << 16)
+    eng.set_input_retention(4)
+    eng.set_block_pairing(True)
+    with pytest.raises(Exception):
+        eng.set_input_retention(3)
+    eng.set_input_retention(6)  # >= 4 stays allowed
+    eng.close()
+
+
 def test_join_leave_join_before_first_block(amd):
     """A chain that joins and leaves before any block, then another chain that joins: the second
     one takes the first one's W slot and (from the pool) its buffers while both joins' spectra

@@ -37,7 +37,8 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retention=1):
+def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retention=1,
+            pair=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -45,13 +46,19 @@ def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retenti
     full = torch.complex(torch.randn(hist + nblocks * block, generator=g),
                          torch.randn(hist + nblocks * block, generator=g))
     bc = IqBroadcast(torch, dist, "cpu", hist, block, stream=full if rank == 0 else None,
-                     retention=retention)
+                     retention=retention, pair=pair)
     ok = True
     live = []  # the windows an engine with this input retention may still read
+    prev = None
     for i in range(nblocks):
         if pipelined and i + 1 < nblocks:
             bc.issue(i + 1)  # the next block's broadcast is in flight while block i is used
         t, off = bc.wait(i) if pipelined else bc.step(i)
+        if pair and i % 2 == 1:
+            # the pair's second block sits right behind its first one in memory, so a paired
+            # engine (owrx_set_block_pairing) runs the two as one engine block on every rank
+            ok &= prev is not None and t.data_ptr() + 8 * off == prev[0].data_ptr() + 8 * (prev[1] + block)
+        prev = (t, off)
         live = (live + [(i, t, off)])[-retention:]
         for k, tk, ok_off in live:  # none of them rewritten yet
             got = tk[ok_off - hist: ok_off + block]
@@ -63,16 +70,20 @@ def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retenti
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined,retention", [(False, 1), (True, 1), (True, 8)])
-def test_iq_broadcast_world2_gloo(pipelined, retention):
+@pytest.mark.parametrize("pipelined,retention,pair", [(False, 1, False), (True, 1, False),
+                                                       (True, 8, False), (False, 4, True),
+                                                       (True, 4, True), (True, 8, True)])
+def test_iq_broadcast_world2_gloo(pipelined, retention, pair):
     """Every rank reconstructs [history | block] windows equal to rank 0's stream, with the
     broadcasts one at a time or pipelined one block ahead (bench.py's N > 1 loop); with input
     retention r (bench.py sets 8 at every N) the last r blocks' windows stay intact while the
-    next broadcasts land."""
+    next broadcasts land.  pair=True: blocks travel two per broadcast into [history | 2 blocks]
+    windows and each pair is contiguous in memory on every rank, so ranks > 0 pair blocks
+    (owrx_set_block_pairing) as rank 0 does on its recording."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 14, q, pipelined, retention))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 14, q, pipelined, retention, pair))
              for r in range(2)]
     for p in procs:
         p.start()
