@@ -757,6 +757,9 @@ def main():
     ap.add_argument("--no-waterfall", action="store_true")
     ap.add_argument("--no-pairing", action="store_true",
                     help="one engine block per 2^20-sample block (owrx_set_block_pairing off)")
+    ap.add_argument("--block-group", type=int, default=int(os.environ.get("OWRX_BENCH_GROUP", "2")),
+                    help="contiguous 2^20-sample blocks per engine block (owrx_set_block_group: "
+                         "2 = pairs, 4 = quads; input retention raised to 4 x this when lower)")
     ap.add_argument("--realtime-seconds", type=float, default=3.0,
                     help="paced real-time check at 10 Msps through the host push path (0: skip)")
     ap.add_argument("--no-timing", action="store_true",
@@ -844,7 +847,10 @@ def main():
     # ranks (IqBroadcast sizes its ring to the retention): every block stays valid for
     # `retention` further blocks, so the host may run that far ahead of stream A
     # (owrx_set_input_retention), at every N
+    group = 1 if args.no_pairing else max(1, min(4, args.block_group))
     retention = int(os.environ.get("OWRX_BENCH_RETENTION", "8"))
+    if group > 2:
+        retention = max(retention, 4 * group)  # the host stays 3 engine blocks ahead (in_keep)
     eng.set_input_retention(retention)
     # 16 blocks in flight for the headline engine (256 chains: a few MB of staging per block);
     # the capacity ladder's engines keep the default 8 (their staging grows with the chains)
@@ -856,9 +862,9 @@ def main():
     # rank 0's recording is, and ranks > 0 receive each pair in one broadcast into one
     # [history | 2 blocks] window (IqBroadcast(pair=True), round 6), so every rank runs the N = 1
     # engine
-    pairing = not args.no_pairing and retention >= 4
+    pairing = group > 1 and retention >= 2 * group
     if pairing:
-        eng.set_block_pairing(True)
+        eng.set_block_group(group)
     hist = eng.history
     wf = None
     if rank == 0 and not args.no_waterfall:
@@ -898,7 +904,7 @@ def main():
         hist_b = int(t.item())
         src_view = stream[hist - hist_b:] if rank == 0 else None
         bcast = IqBroadcast(torch, dist, dev, hist_b, block, stream=src_view, retention=retention,
-                            pair=pairing)
+                            group=group if pairing else 1)
     torch.cuda.synchronize(dev)
 
     def drain():
@@ -1126,6 +1132,8 @@ def main():
                 "pipeline_depth_blocks": depth,
                 "waterfall_batch_frames_rank0": wf_batch,
                 "block_pairing_rank0": bool(pairing),
+                "block_pairing_all_ranks": bool(pairing),
+                "block_group": group if pairing else 1,
             },
             "value_definition": ("Msamples/s of the ONE wideband IQ stream ingested, at any N: "
                                  "each GPU runs the whole stream (broadcast from rank 0; waterfall "

@@ -107,7 +107,7 @@ int owrx_wait_stream(owrx_engine* e, void* stream);
  * until r further owrx_process_device / owrx_commit calls (or owrx_sync) have returned, and the
  * engine waits only for block k - r + 1's stream-A work before returning from block k, so the
  * host runs up to r blocks ahead of stream A.  Default 1 (the contract above); 1 <= r <= 31, and
- * r >= 4 while block pairing is on (OWRX_EINVAL otherwise). */
+ * r >= 2 x the block group while grouping / pairing is on (OWRX_EINVAL otherwise). */
 int owrx_set_input_retention(owrx_engine* e, int blocks);
 /* Block pairing (enable = 1; input retention >= 4, before the first chain, waterfall and block):
  * owrx_process_device holds a block until the next call; when the next block follows it in
@@ -119,6 +119,13 @@ int owrx_set_input_retention(owrx_engine* e, int blocks);
  * successor, so it adds one block of latency: for callers that are blocks ahead of the stream
  * (a recording), not for a live source.  Staging is sized for 2 x max_block. */
 int owrx_set_block_pairing(owrx_engine* e, int enable);
+/* Block grouping, the general form of pairing (round 6): blocks = 1 (off), 2 (= pairing), 3 or 4
+ * contiguous caller blocks run as one engine block, with input retention >= 2 x blocks; same
+ * preconditions, contract and byte-identical outputs as owrx_set_block_pairing.  Each engine block
+ * reads the DDC's filter spectra once for all its blocks' frames (quads: the per-bin GEMM at about
+ * twice a pair's arithmetic intensity) and launches every stage once; it adds blocks - 1 blocks of
+ * latency.  Staging is sized for blocks x max_block. */
+int owrx_set_block_group(owrx_engine* e, int blocks);
 /* Blocks of chain work in flight (streams A -> B -> C -> host rings), 1..16, default 8; only
  * before the first chain and block.  Each one holds pinned and device staging for every chain
  * (at 98 304 chains ~0.5 GB pinned per block), so deeper pipelines are for few-chain, high-rate

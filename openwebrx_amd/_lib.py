@@ -149,6 +149,7 @@ PROTOTYPES = {
     "owrx_waterfall_set_latency": (_i32, [_vp, _i32, _f64]),
     "owrx_set_input_retention": (_i32, [_vp, _i32]),
     "owrx_set_block_pairing": (_i32, [_vp, _i32]),
+    "owrx_set_block_group": (_i32, [_vp, _i32]),
     "owrx_set_pipeline_depth": (_i32, [_vp, _i32]),
     "owrx_set_stall_timeout": (_i32, [_vp, _i64]),
     "owrx_debug_stall": (_i32, [_vp, _i32, _i64]),

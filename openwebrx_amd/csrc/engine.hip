@@ -112,8 +112,9 @@ hipError_t launch_fc_make_w_jobs(int m, const float* h, int T, int D, int Dp, in
 int64_t fc_w_chain_offset(int c, int Dp);  // chain c's first entry in a bin's row of the tiled W
 int fc_w_tile();                           // chains per W tile: capacities are multiples of it
 int fc_w_layout_check(int Dp, int cap);    // host self-test of the tiled W layout
-hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
-                         int64_t blk_end1, int nk1, const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
+int fc_frames(const FcSubs& sb, int V);  // frames of a (grouped) engine block
+hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, const FcSubs& sb,
+                         const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
                          int ncu, hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form);
@@ -653,7 +654,7 @@ struct GroupWork {
     int64_t k_end;
     int nk;
     bool fast;
-    int nk1;  // outputs of the first caller block of a pair (= nk unpaired)
+    FcSubs sub;  // the caller blocks' outputs and input ends (one block: n = 1)
 };
 
 struct owrx_engine {
@@ -718,11 +719,14 @@ struct owrx_engine {
     hipEvent_t evIn[kInEv] = {};
     int64_t in_done = -1;
     int retention = 1;
-    // block pairing (owrx_set_block_pairing): a caller block held until the next one arrives,
-    // then both run as one engine block (pend_n: the held block's samples, 0 = none)
-    bool pair = false;
+    // block grouping (owrx_set_block_group; pairs: owrx_set_block_pairing): caller blocks held
+    // until `group` contiguous ones arrived, then run as one engine block (pend_k held blocks from
+    // pend_blk, pend_n[] samples each, pend_total in all; 0 = none)
+    int group = 1;
     const float2* pend_blk = nullptr;
-    int64_t pend_n = 0;
+    int pend_k = 0;
+    int64_t pend_n[kMaxSubBlocks] = {};
+    int64_t pend_total = 0;
     // blocks of chain work in flight (owrx_set_pipeline_depth, <= kSlots): every slot holds
     // pinned and device staging for all chains, so the depth is the caller's memory trade
     int nslots = kDefaultSlots;
@@ -849,7 +853,7 @@ static int sync_stream(owrx_engine* e, hipStream_t st) {
 }
 
 // the largest engine block: two caller blocks when pairing
-static int64_t proc_block(const owrx_engine* e) { return e->pair ? 2 * e->max_block : e->max_block; }
+static int64_t proc_block(const owrx_engine* e) { return (int64_t)e->group * e->max_block; }
 
 static int64_t chain_stage_cap(const owrx_engine* e, int D, double frac) {
     int64_t nk = proc_block(e) / D + 4;
@@ -2091,7 +2095,7 @@ static int build_posts(owrx_engine* e, Slot& S, int si) {
 // Wait until block j's stream-A work (which read its input and its staged descriptors) is done.
 // engine blocks after which the caller's oldest retained input is read: `retention` caller
 // blocks, each engine block of a paired engine holding up to two of them
-static int in_keep(const owrx_engine* e) { return e->pair ? (e->retention - 1) / 2 : e->retention; }
+static int in_keep(const owrx_engine* e) { return e->group > 1 ? (e->retention - 1) / e->group : e->retention; }
 
 static int wait_input_block(owrx_engine* e, int64_t j) {
     if (j <= e->in_done || j < 0) return OWRX_OK;
@@ -2100,9 +2104,10 @@ static int wait_input_block(owrx_engine* e, int64_t j) {
     return OWRX_OK;
 }
 
-// `split` > 0: a pair of caller blocks, the first `split` samples long (owrx_set_block_pairing);
-// every stage runs once over both, the fast DDC with each block's own frame placement
-static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t split = 0) {
+// `nsub` > 1: that many caller blocks of sub_n[] samples each (owrx_set_block_group); every stage
+// runs once over all of them, the fast DDC with each block's own frame placement
+static int process_block(owrx_engine* e, const float2* blk, int64_t n, int nsub = 1,
+                         const int64_t* sub_n = nullptr) {
     const double t_enter = now_ms();
     RCCHK(flush_uploads(e));  // pool buffers and uploads of chains / waterfalls created since the last block
     // Block k's pinned descriptors are staged per slot (reused by block k + kSlots, after the
@@ -2191,15 +2196,19 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t s
             }
         }
         g->chains_stale = stale;  // consumed by this block's upload below
-        // a pair's first block: the outputs its own call would have produced
-        int64_t nk1 = nk64;
-        if (split > 0) {
-            const int64_t e1 = blk_start + split;
-            const int64_t k1 = e1 < g->T ? g->k_next : (e1 - g->T) / g->D + 1;
-            nk1 = std::min(nk64, std::max<int64_t>(0, k1 - g->k_next));
+        // each caller block's outputs: those its own call would have produced
+        FcSubs sb{};
+        sb.n = std::max(1, std::min(nsub, kMaxSubBlocks));
+        int64_t e_s = blk_start;
+        for (int si = 0; si < sb.n; ++si) {
+            e_s = si + 1 < sb.n ? e_s + sub_n[si] : blk_end;
+            const int64_t ks = e_s < g->T ? g->k_next : (e_s - g->T) / g->D + 1;
+            sb.nk[si] = (int)std::min(nk64, std::max<int64_t>(si ? sb.nk[si - 1] : 0, ks - g->k_next));
+            sb.end[si] = e_s;
         }
+        sb.nk[sb.n - 1] = (int)nk64;
         work.push_back(GroupWork{g, k_end, (int)nk64,
-                                 g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST, (int)nk1});
+                                 g->fc_M != 0 && e->ddc_mode == OWRX_DDC_FAST, sb});
     }
     // the slot's post descriptors and lane lists: as built for its last block unless a chain
     // changed since (or the groups with outputs differ); then this block's nk / k_begin
@@ -2277,7 +2286,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t s
             // the first fast group's GEMM is timed (one group in the benchmark configurations)
             const bool tm = timed && !S.timed_mac;
             int form = 0;
-            HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, blk_end, split > 0 ? blk_start + split : blk_end, gw.nk1,
+            HIPCHK(launch_fc_ddc(g->fc_M, blk, blk_start, gw.sub,
                                  g->d_chains, g->d_fc_w,
                                  g->fc_Dp, g->fc_w_ks(), (int)g->members.size(), g->D, g->fc_Dp,
                                  g->fc_V, g->fc_Fs, g->k_next, nk, g->d_fc_tw, g->d_fc_u,
@@ -2291,8 +2300,7 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t s
                 // algorithmic work of that GEMM: 8 flop per complex MAC over the frames that
                 // carry outputs; bytes = W (every member's spectra) + U + Y, each moved once
                 const double M = (double)g->fc_M;
-                const double F = (double)((gw.nk1 + g->fc_V - 1) / g->fc_V +
-                                          (nk - gw.nk1 + g->fc_V - 1) / g->fc_V);
+                const double F = (double)fc_frames(gw.sub, g->fc_V);
                 const double C = (double)g->members.size();
                 e->stats.ddc_mac_flop += 8.0 * M * g->fc_Dp * C * F;
                 e->stats.ddc_mac_bytes += 8.0 * M * g->fc_Dp * (C + F) + 8.0 * C * F * M;
@@ -2401,13 +2409,17 @@ static int process_block(owrx_engine* e, const float2* blk, int64_t n, int64_t s
     return OWRX_OK;
 }
 
-// the held caller block alone (owrx_set_block_pairing)
+// the held caller blocks (owrx_set_block_group), contiguous, as one engine block
 static int pair_flush(owrx_engine* e) {
     const float2* b = e->pend_blk;
-    const int64_t n = e->pend_n;
-    e->pend_n = 0;
+    const int k = e->pend_k;
+    const int64_t n = e->pend_total;
+    int64_t sub[kMaxSubBlocks];
+    for (int i = 0; i < k; ++i) sub[i] = e->pend_n[i];
+    e->pend_k = 0;
+    e->pend_total = 0;
     e->pend_blk = nullptr;
-    return process_block(e, b, n);
+    return k > 0 ? process_block(e, b, n, k, sub) : OWRX_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2427,11 +2439,11 @@ static int pair_flush(owrx_engine* e) {
     }                                                                \
     hipSetDevice((e)->device);
 
-// every entry point except owrx_process_device, the reads and the stats: a held caller block
-// (owrx_set_block_pairing) runs first, so the call sees the engine as after that block alone
+// every entry point except owrx_process_device, the reads and the stats: held caller blocks
+// (owrx_set_block_group) run first, so the call sees the engine as after those blocks alone
 #define ENGINE_GUARD(e)                                              \
     ENGINE_GUARD_HELD(e)                                             \
-    if ((e)->pend_n > 0) {                                           \
+    if ((e)->pend_k > 0) {                                           \
         const int _prc = pair_flush(e);                              \
         if (_prc < 0) {                                              \
             if (_prc == OWRX_EIO || _prc == OWRX_ETIMEDOUT) (e)->failed = true; \
@@ -2754,10 +2766,11 @@ int owrx_set_input_retention(owrx_engine* e, int blocks) {
         set_last_error("owrx_set_input_retention: blocks must be in [1, %d]", kInEv - 1);
         return OWRX_EINVAL;
     }
-    // a paired engine holds a caller block until the next one arrives: pairing needs >= 4
-    // (owrx_set_block_pairing), so it may not be lowered below that afterwards
-    if (e->pair && blocks < 4) {
-        set_last_error("owrx_set_input_retention: block pairing is on, blocks must be >= 4");
+    // a grouping engine holds caller blocks until the group is complete: groups of g need
+    // retention >= 2 g (owrx_set_block_group), so it may not be lowered below that afterwards
+    if (e->group > 1 && blocks < 2 * e->group) {
+        set_last_error("owrx_set_input_retention: block grouping of %d is on, blocks must be >= %d",
+                       e->group, 2 * e->group);
         return OWRX_EINVAL;
     }
     e->retention = blocks;
@@ -2814,44 +2827,50 @@ int owrx_process_device(owrx_engine* e, const float* iq_dev, int64_t n) {
     }
     if (n == 0) return OWRX_OK;
     const float2* blk = (const float2*)iq_dev;
-    if (!e->pair) {
+    if (e->group <= 1) {
         RC_FAIL(e, process_block(e, blk, n));
         return OWRX_OK;
     }
-    // pairing: the held block and this one, contiguous, run as one engine block; otherwise the
-    // held one alone, and this one is held
-    if (e->pend_n > 0) {
-        if (blk == e->pend_blk + e->pend_n) {
-            const float2* b = e->pend_blk;
-            const int64_t n1 = e->pend_n;
-            e->pend_n = 0;
-            e->pend_blk = nullptr;
-            RC_FAIL(e, process_block(e, b, n1 + n, n1));
-            return OWRX_OK;
-        }
+    // grouping: held blocks and this one, contiguous, run as one engine block once `group` of
+    // them arrived; a block that does not follow the held ones runs them first, alone
+    if (e->pend_k > 0 && blk != e->pend_blk + e->pend_total) RC_FAIL(e, pair_flush(e));
+    if (e->pend_k == 0) e->pend_blk = blk;
+    e->pend_n[e->pend_k++] = n;
+    e->pend_total += n;
+    if (e->pend_k >= e->group) {
         RC_FAIL(e, pair_flush(e));
+        return OWRX_OK;
     }
-    e->pend_blk = blk;
-    e->pend_n = n;
-    // input retention while held: the caller's block k - retention has been read (each engine
-    // block holds at most two caller blocks, so engine block b - (retention - 1) / 2 covers it)
+    // input retention while held: the caller's block k - retention has been read.  The engine
+    // blocks after the one holding it hold at least retention - pend_k - (group - 1) caller
+    // blocks, at most `group` each, so engine block b - floor((retention - pend_k) / group)
+    // covers it
     const double t = now_ms();
-    RC_FAIL(e, wait_input_block(e, e->block_index - 1 - (e->retention - 1) / 2));
+    RC_FAIL(e, wait_input_block(e, e->block_index - 1 - std::max(0, (e->retention - e->pend_k) / e->group)));
     e->stats.host_ms_wait_input += now_ms() - t;
     return OWRX_OK;
 }
 
-int owrx_set_block_pairing(owrx_engine* e, int enable) {
+int owrx_set_block_group(owrx_engine* e, int blocks) {
     ENGINE_GUARD(e);
-    // a paired engine sizes its staging for two caller blocks: before the first chain and block
-    if (enable < 0 || enable > 1 || e->block_index != 0 || !e->chains.empty() || !e->wfs.empty() ||
-        e->post_cap > 0 || (enable && e->retention < 4)) {
-        set_last_error("owrx_set_block_pairing: 0 or 1, before the first chain, waterfall and "
-                       "block, with input retention >= 4");
+    // a grouping engine sizes its staging for `blocks` caller blocks: before the first chain and
+    // block
+    if (blocks < 1 || blocks > kMaxSubBlocks || e->block_index != 0 || !e->chains.empty() ||
+        !e->wfs.empty() || e->post_cap > 0 || (blocks > 1 && e->retention < 2 * blocks)) {
+        set_last_error("owrx_set_block_group: 1..%d, before the first chain, waterfall and "
+                       "block, with input retention >= 2 x blocks", kMaxSubBlocks);
         return OWRX_EINVAL;
     }
-    e->pair = enable != 0;
+    e->group = blocks;
     return OWRX_OK;
+}
+
+int owrx_set_block_pairing(owrx_engine* e, int enable) {
+    if (e && (enable < 0 || enable > 1)) {
+        set_last_error("owrx_set_block_pairing: 0 or 1");
+        return OWRX_EINVAL;
+    }
+    return owrx_set_block_group(e, enable ? 2 : 1);
 }
 
 // Room for a block of n at the ring's write position: when it does not fit, the last `history`
@@ -3272,7 +3291,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
             // frames of the largest engine block; a pair cuts its frames at the caller blocks'
             // boundary, one frame more
             const int64_t nk_proc = proc_block(e) / D + 4;
-            ng->fc_Fs = (int)((nk_proc + ng->fc_V - 1) / ng->fc_V + (e->pair ? 1 : 0) + 15) & ~15;
+            ng->fc_Fs = (int)((nk_proc + ng->fc_V - 1) / ng->fc_V + (e->group - 1) + 15) & ~15;
             HIPCHK(dalloc(&ng->d_h, (size_t)T));
             HIPCHK(hipMemcpy(ng->d_h, h.data(), sizeof(float) * T, hipMemcpyHostToDevice));
             std::vector<float> tw = fft_twiddles(M);

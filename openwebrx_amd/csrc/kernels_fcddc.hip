@@ -174,26 +174,41 @@ fc_make_w_jobs(const float* __restrict__ h, int T, int D, int P, const FcWJob* _
     fc_make_w_rows<M>(h, T, D, P, j.rate_fx, W + j.off, w_ks);
 }
 
+// Frame f of an engine block of caller blocks (FcSubs): its sub-block s, the sub-block's first
+// output nk0 and first frame f0.
+struct FcFrame {
+    int s, nk0, f0;
+};
+OWRX_DEV FcFrame fc_frame_sub(const FcSubs& sb, int f, int V) {
+    FcFrame r{0, 0, 0};
+    for (int s = 0; s + 1 < sb.n; ++s) {
+        const int fe = r.f0 + (sb.nk[s] - r.nk0 + V - 1) / V;
+        if (f < fe) break;
+        r.s = s + 1;
+        r.nk0 = sb.nk[s];
+        r.f0 = fe;
+    }
+    return r;
+}
+
 // ---- U[kappa][f][r]: M-point DFT of every branch frame --------------------------------------
 // grid: (Dp / kFcRT, F); block 256.  tw: M-point table e^{-j 2 pi m / M}.
-// A pair of caller blocks (owrx_set_block_pairing): frames f < F1 are the first block's, from
-// k_begin and zero past blk_end1, the rest the second block's from k_begin + nk1 -- the frames
-// and zero padding each block's own launch would have had, so U is bit-identical to two
-// launches.  Unpaired: F1 = F, blk_end1 = blk_end.
+// Caller blocks grouped into one engine block (owrx_set_block_group): each sub-block's frames
+// start at its first output and are zero past its own input end (FcSubs) -- the frames and zero
+// padding each block's own launch would have had, so U is bit-identical to separate launches.
 template <int M>
 __global__ void __launch_bounds__(256)
-fc_fwd(const float2* __restrict__ blk, int64_t blk_start, int64_t blk_end, int64_t blk_end1,
-       int64_t k_begin, int nk1, int F1, int V, int D, int Dp, int Fs,
-       const float2* __restrict__ tw, float2* __restrict__ U) {
+fc_fwd(const float2* __restrict__ blk, int64_t blk_start, FcSubs sb, int64_t k_begin, int V, int D,
+       int Dp, int Fs, const float2* __restrict__ tw, float2* __restrict__ U) {
     using FM = FcM<M>;
     constexpr int RS = FM::RS;         // LDS row stride (float2): column writes hit distinct banks
     __shared__ float2 sm[kFcRT * RS];
     const int tid = threadIdx.x;
     const int r0 = blockIdx.x * kFcRT;
     const int f = blockIdx.y;
-    const bool second = f >= F1;
-    const int64_t k0 = second ? k_begin + nk1 + (int64_t)(f - F1) * V : k_begin + (int64_t)f * V;
-    if (!second) blk_end = blk_end1;
+    const FcFrame fr = fc_frame_sub(sb, f, V);
+    const int64_t k0 = k_begin + fr.nk0 + (int64_t)(f - fr.f0) * V;
+    const int64_t blk_end = sb.end[fr.s];
     const int j = tid % kFcRT;
     const int r = r0 + j;
     // rows i of the frame: 16 consecutive branches = one 128-B run per row
@@ -240,7 +255,16 @@ fc_mac(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w_cs,
     const int q = w >> 3;
     const int mper = M >> 3;
     int kap, cg, fg;
-    if (chain_fastest) {
+    const int nfg = (F + 16 * FTT - 1) / (16 * FTT);
+    if (chain_fastest && nfg > 1) {
+        // several frame tiles (grouped blocks, F > 16 FTT): a (kappa, chain group)'s frame tiles
+        // come back to back on one XCD, so the second reads its W tile from L2 and W streams
+        // from HBM once per launch (frame tiles outermost re-read all of W per tile)
+        fg = q % nfg;
+        const int r1 = q / nfg;
+        cg = r1 % ncg;
+        kap = xcd * mper + r1 / ncg;
+    } else if (chain_fastest) {
         cg = q % ncg;
         const int r1 = q / ncg;
         kap = xcd * mper + r1 % mper;
@@ -406,7 +430,16 @@ fc_mac_lds(const float2* __restrict__ U, const float2* __restrict__ W, int64_t w
     const int q = w >> 3;
     const int mper = M >> 3;
     int kap, cg, fg;
-    if (chain_fastest) {
+    const int nfg = (F + 16 * FTT - 1) / (16 * FTT);
+    if (chain_fastest && nfg > 1) {
+        // several frame tiles (grouped blocks, F > 16 FTT): a (kappa, chain group)'s frame tiles
+        // come back to back on one XCD, so the second reads its W tile from L2 and W streams
+        // from HBM once per launch (frame tiles outermost re-read all of W per tile)
+        fg = q % nfg;
+        const int r1 = q / nfg;
+        cg = r1 % ncg;
+        kap = xcd * mper + r1 / ncg;
+    } else if (chain_fastest) {
         cg = q % ncg;
         const int r1 = q / ncg;
         kap = xcd * mper + r1 % mper;
@@ -582,7 +615,7 @@ OWRX_DEV float2 fc_rotator(const DdcChain& ch, int64_t n) {
 template <int M>
 __global__ void __launch_bounds__(256)
 fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nchains, int Fs,
-       int F, int V, int D, int64_t k_begin, int nk, int nk1, int F1,
+       int F, int V, int D, int64_t k_begin, int nk, FcSubs sb,
        const float2* __restrict__ tw, float2* __restrict__ out, int ks, int64_t y_slice) {
     using FM = FcM<M>;
     constexpr int RW = FM::R3 ? 3072 / M : 1024 / M;
@@ -615,9 +648,10 @@ fc_out(const float2* __restrict__ Y, const DdcChain* __restrict__ chains, int nc
         const int row = row0 + rr;
         if (row >= nrows || m >= V) continue;
         const int c = row / F, f = row % F;
-        // the frame's block (fc_fwd): outputs [0, nk1) from frames < F1, then [nk1, nk)
-        const int kk = f < F1 ? f * V + m : nk1 + (f - F1) * V + m;
-        if (kk >= (f < F1 ? nk1 : nk)) continue;
+        // the frame's sub-block (fc_fwd): its outputs [nk[s - 1], nk[s])
+        const FcFrame fr = fc_frame_sub(sb, f, V);
+        const int kk = fr.nk0 + (f - fr.f0) * V + m;
+        if (kk >= sb.nk[fr.s]) continue;
         const float2 z = sm[rr * RS + FM::kpos(m)];
         const float2 y = make_float2(z.x * inv, -z.y * inv);
         const float2 rot = fc_rotator(chains[c], (k_begin + kk) * (int64_t)D);
@@ -695,19 +729,30 @@ hipError_t launch_fc_make_w(int m, const float* h, int T, int D, int Dp, int P,
 }
 
 // frames per block F = ceil(nk / V); U: [M][Fs][Dp], Y: [nchains][Fs][M], out: [nchains][nk].
-// A pair of caller blocks: the first's nk1 outputs (input up to blk_end1) in ceil(nk1 / V)
-// frames, the second's in their own; one GEMM over both (W read once for the two blocks).
-hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t blk_end,
-                         int64_t blk_end1, int nk1, const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
+// Grouped caller blocks (FcSubs): each sub-block's outputs in frames of their own; one GEMM over
+// all of them (W read once for the group's blocks).
+int fc_frames(const FcSubs& sb, int V) {
+    int F = 0, k0 = 0;
+    for (int s = 0; s < sb.n; ++s) {
+        F += (sb.nk[s] - k0 + V - 1) / V;
+        k0 = sb.nk[s];
+    }
+    return F;
+}
+
+hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, const FcSubs& sb,
+                         const DdcChain* chains, const float2* W, int64_t w_cs, int64_t w_ks,
                          int nchains, int D, int Dp, int V, int Fs, int64_t k_begin, int nk,
                          const float2* tw, float2* U, float2* Y, int64_t y_cap, float2* out,
                          int ncu, hipStream_t st, hipEvent_t mac0, hipEvent_t mac1, int* form) {
-    if (nk1 < 0 || nk1 > nk) return hipErrorInvalidValue;
-    const int F1 = (nk1 + V - 1) / V;
-    const int F = F1 + (nk - nk1 + V - 1) / V;
+    if (sb.n < 1 || sb.n > kMaxSubBlocks || sb.nk[sb.n - 1] != nk) return hipErrorInvalidValue;
+    for (int s = 0; s < sb.n; ++s)
+        if (sb.nk[s] < (s ? sb.nk[s - 1] : 0) || sb.end[s] < (s ? sb.end[s - 1] : blk_start))
+            return hipErrorInvalidValue;
+    const int F = fc_frames(sb, V);
     if (F > Fs || nk <= 0 || nchains <= 0) return hipErrorInvalidValue;
     const dim3 gf(Dp / kFcRT, F);
-#define OWRX_FC_F(MM) hipLaunchKernelGGL(fc_fwd<MM>, gf, dim3(256), 0, st, blk, blk_start, blk_end, blk_end1, k_begin, nk1, F1, V, D, Dp, Fs, tw, U)
+#define OWRX_FC_F(MM) hipLaunchKernelGGL(fc_fwd<MM>, gf, dim3(256), 0, st, blk, blk_start, sb, k_begin, V, D, Dp, Fs, tw, U)
     OWRX_FC_SWITCH(M, OWRX_FC_F)
 #undef OWRX_FC_F
     HIPCHK_RET(hipGetLastError());
@@ -757,7 +802,7 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, int64_t bl
     if (mac1) HIPCHK_RET(hipEventRecord(mac1, st));
     const int rw = (M % 3 == 0) ? 3072 / M : 1024 / M;
     const dim3 go((nchains * F + rw - 1) / rw);
-#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, nk1, F1, tw, out, ring ? ks : 1, y_slice)
+#define OWRX_FC_O(MM) hipLaunchKernelGGL(fc_out<MM>, go, dim3(256), 0, st, Y, chains, nchains, Fs, F, V, D, k_begin, nk, sb, tw, out, ring ? ks : 1, y_slice)
     OWRX_FC_SWITCH(M, OWRX_FC_O)
 #undef OWRX_FC_O
     return hipGetLastError();

@@ -387,4 +387,53 @@ OWRX_DEV uint32_t adpcm_encode_rem(AdpcmRem& s, int sample, const uint2* __restr
     return acc;
 }
 
+// The remainder form with a shorter predictor recurrence (round 6).  The encoder is bound by its
+// two loop-carried chains as much as by issue: the predictor (pred -> d -> |d| -> three magnitude
+// bits -> dq -> pred') and the successor record (record -> magnitude bits -> index -> LDS read ->
+// record).  Here the predictor is kept offset by 32768 (predo = pred + 32768 in [0, 65535]) and the
+// sample comes offset too, so |d| is one v_sad_u32 (no negate / max pair), and the update
+//   pred' = pred + sgn (s3 + a0 - a3) = (predo + sgn (s3 + a0) + sgn) - (a3 ^ sgn)
+// (sgn (v) = (v ^ sgn) - sgn, sgn = 0 or -1) has its first part computed beside the magnitude
+// compares: after the last bit only the xor, the subtraction and the clamp (v_med3) remain.
+// Bit-identical to adpcm_encode_rem; same records and return value.
+struct AdpcmRemO {
+    uint32_t w0, w1;  // as AdpcmRem
+    int predo;        // pred + 32768
+    OWRX_DEV int index() const { return (int)(w0 >> 17); }
+    OWRX_DEV int pred() const { return predo - 32768; }
+};
+
+OWRX_DEV AdpcmRemO adpcm_rem_o_state(AdpcmState s) {
+    const AdpcmRem r = adpcm_rem_state(s);
+    return AdpcmRemO{r.w0, r.w1, s.pred + 32768};
+}
+
+// xo = sample + 32768
+OWRX_DEV uint32_t adpcm_encode_rem_o(AdpcmRemO& s, uint32_t xo, const uint2* __restrict__ NSR) {
+    const int d = (int)xo - s.predo;
+    const int sgn = d >> 31;
+    const uint32_t po = (uint32_t)s.predo;
+    const uint32_t a0 = xo > po ? xo - po : po - xo;  // one v_sad_u32 (as dq in adpcm_encode_rem)
+    const uint32_t w0 = s.w0, w1 = s.w1;
+    const uint32_t s3 = (w1 & 0xffffu) >> 2;
+    const int e = (int)(s3 + a0);
+    const int q = s.predo + ((e ^ sgn) - sgn) + sgn;  // beside the compares
+    uint32_t acc = ((uint32_t)d >> 31) + (w0 >> 16);
+    const uint32_t u4 = a0 - (w0 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u4, 31);
+    const uint32_t a1 = min(a0, u4);
+    const uint32_t u2 = a1 - (w1 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u2, 31);
+    const uint32_t a2 = min(a1, u2);
+    const uint32_t u1 = a2 - (w1 >> 16);
+    acc = __builtin_amdgcn_alignbit(acc, u1, 31);
+    const uint32_t a3 = min(a2, u1);
+    const uint2 r = NSR[acc];
+    s.w0 = r.x;
+    s.w1 = r.y;
+    const int p = q - (int)(a3 ^ (uint32_t)sgn);
+    s.predo = min(max(p, 0), 65535);
+    return acc;
+}
+
 }  // namespace owrx

@@ -80,6 +80,18 @@ struct NrState {
 
 // The per-block fields of a chain group's posts (post_parallel's argument): the slot's posts
 // stay on the device across blocks and only this table changes.
+// Caller blocks in one engine block (owrx_set_block_group: pairs, quads): sub-block s holds the
+// DDC outputs [nk[s - 1], nk[s]) (nk[-1] = 0) from input up to the absolute sample end[s], in
+// ceil((nk[s] - nk[s - 1]) / V) frames of its own with its own zero padding, so the fast DDC's
+// frames and outputs are those of separate launches.  n = 1: one block (nk[0] = nk, end[0] =
+// the block's end).
+constexpr int kMaxSubBlocks = 4;
+struct FcSubs {
+    int n;
+    int nk[kMaxSubBlocks];
+    int64_t end[kMaxSubBlocks];
+};
+
 struct GroupStep {
     int64_t k_begin;
     int32_t nk;

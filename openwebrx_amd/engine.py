@@ -129,6 +129,12 @@ class Engine:
         one block more latency."""
         check(lib.owrx_set_block_pairing(self._h, 1 if enable else 0), "owrx_set_block_pairing")
 
+    def set_block_group(self, blocks):
+        """Run `blocks` (1..4) contiguous process_device blocks as one engine block
+        (owrx_set_block_group; input retention >= 2 x blocks, before the first chain, waterfall
+        and block): outputs byte-identical, blocks - 1 blocks more latency."""
+        check(lib.owrx_set_block_group(self._h, int(blocks)), "owrx_set_block_group")
+
     def set_pipeline_depth(self, blocks):
         """Blocks of chain work in flight (1..16, default 8), before the first chain and block."""
         check(lib.owrx_set_pipeline_depth(self._h, int(blocks)), "owrx_set_pipeline_depth")

@@ -69,25 +69,28 @@ class IqBroadcast:
     one broadcast into one window [history | block 2u | block 2u + 1], so on every rank the two
     blocks of a pair are contiguous in memory and the engine runs them as one engine block,
     exactly as rank 0 does on its resident recording.  A window then covers two blocks and the
-    ring holds retention // 2 + 3 of them."""
+    ring holds retention // 2 + 3 of them.  group=g: g blocks per broadcast and window (the
+    engines' owrx_set_block_group), retention // g + 3 windows."""
 
     NWIN = 3
 
     def __init__(self, torch, dist, device, history, block, src=0, stream=None, retention=1,
-                 pair=False):
+                 pair=False, group=None):
         self.torch, self.dist = torch, dist
         self.history, self.block, self.src = history, block, src
         self.rank = dist.get_rank()
         self.stream = stream  # rank src: complex64 tensor [history | blocks...]
-        self.per = 2 if pair else 1  # blocks per broadcast (and per window)
+        # blocks per broadcast (and per window): the engines' block group (owrx_set_block_group;
+        # pair=True: 2)
+        self.per = max(1, int(group)) if group is not None else (2 if pair else 1)
         self.pending = {}     # unit -> async broadcast handle
         self.next_issue = 0   # broadcasts are enqueued in unit order on every rank
         # an engine with input retention r still reads blocks k - r + 1 .. k after
         # owrx_process_device(k) returned, and block k + 1's broadcast is issued before block k is
         # processed: the units of blocks k - r .. k + 1 stay intact, r + 2 windows unpaired (3 for
         # r = 1), r // 2 + 3 paired
-        if pair:
-            self.nwin = max(self.NWIN, int(retention) // 2 + 3)
+        if self.per > 1:
+            self.nwin = max(self.NWIN, int(retention) // self.per + 3)
         else:
             self.nwin = max(self.NWIN, int(retention) + 2)
         if self.rank != src:

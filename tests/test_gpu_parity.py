@@ -517,15 +517,17 @@ def test_input_retention_same_outputs(amd):
     assert all(len(x) > 0 for x in a[0]) and len(a[2]) > 0
 
 
+@pytest.mark.parametrize("group", [2, 3, 4])
 @pytest.mark.parametrize("fs,modes,B", [
     (2400000, ["nfm", "usb", "am", "cw"] * 3, 1 << 17),
     (10000000, ["nfm", "usb", "cw"] * 4, 1 << 18),  # C3's design: D = 833, fast convolution
 ])
-def test_block_pairing_same_outputs(amd, fs, modes, B):
-    """owrx_set_block_pairing: contiguous blocks run two at a time (one DDC GEMM over both
-    blocks' frames); audio, s-meter and waterfall rows byte-identical to unpaired processing.
-    An odd block count (owrx_sync runs the held block), a block from another buffer (the held one
-    runs alone) and a chain created mid-stream (the guard runs the held block first)."""
+def test_block_pairing_same_outputs(amd, fs, modes, B, group):
+    """owrx_set_block_pairing / owrx_set_block_group: contiguous blocks run two (three, four) at a
+    time (one DDC GEMM over all their frames); audio, s-meter and waterfall rows byte-identical to
+    unpaired processing.  A block count that leaves blocks held (owrx_sync runs them), a block
+    from another buffer (the held ones run alone) and a chain created mid-stream (the guard runs
+    the held blocks first)."""
     import torch
     from openwebrx_amd import synth
     # blocks: 0+1 and 2+3 paired, 4 alone (chain created after it), 5 alone (6 is from another
@@ -539,8 +541,10 @@ def test_block_pairing_same_outputs(amd, fs, modes, B):
     def run(pair):
         eng = amd.Engine(fs, max_block=B)
         eng.set_input_retention(8)
-        if pair:
+        if pair and group == 2:
             eng.set_block_pairing(True)
+        elif pair:
+            eng.set_block_group(group)
         wf = eng.waterfall(N, hop, avg, adpcm=True)
         chains = [eng.chain(p) for p in plist[:-1]]
         h = eng.history
@@ -562,7 +566,12 @@ def test_block_pairing_same_outputs(amd, fs, modes, B):
         return out, st
 
     (a, sa), (b, sb) = run(False), run(True)
-    assert sa["blocks"] == nb and sb["blocks"] == nb - 4  # four pairs
+    # engine blocks: the held blocks run when the group is complete, before the chain created at
+    # block 5, and before the other buffer's block 6 and the block after it
+    expect = {2: [(0, 1), (2, 3), (4,), (5,), (6,), (7, 8), (9, 10), (11,)],
+              3: [(0, 1, 2), (3, 4), (5,), (6,), (7, 8, 9), (10, 11)],
+              4: [(0, 1, 2, 3), (4,), (5,), (6,), (7, 8, 9, 10), (11,)]}[group]
+    assert sa["blocks"] == nb and sb["blocks"] == len(expect)
     assert all(len(x) > 0 for x in a[0]) and len(a[2]) > 0
     for i in range(len(a[0])):
         assert a[0][i] == b[0][i] and a[1][i] == b[1][i], i
@@ -578,6 +587,17 @@ def test_retention_floor_while_paired(amd):
     with pytest.raises(Exception):
         eng.set_input_retention(3)
     eng.set_input_retention(6)  # >= 4 stays allowed
+    eng.close()
+    eng = amd.Engine(2400000, max_block=1 << 16)
+    eng.set_input_retention(7)
+    with pytest.raises(Exception):
+        eng.set_block_group(4)  # quads need retention >= 8
+    eng.set_input_retention(8)
+    eng.set_block_group(4)
+    with pytest.raises(Exception):
+        eng.set_input_retention(7)
+    with pytest.raises(Exception):
+        eng.set_block_group(5)
     eng.close()
 
 

@@ -1,7 +1,7 @@
 """The N > 1 path with real engines: two ranks on the one GPU, gloo
 for the per-pair IQ broadcast (RCCL refuses two ranks on one device), each rank running its
-shard of the chains on its own engine with block pairing on (IqBroadcast(pair=True) makes every
-pair contiguous on every rank).  The union of the ranks' chain outputs must be byte-identical to
+shard of the chains on its own engine with block pairing (or quads) on (IqBroadcast(group=g)
+makes every group of blocks contiguous on every rank).  The union of the ranks' chain outputs must be byte-identical to
 one engine running every chain, and every rank must have paired its blocks (bench.py's N > 1
 loop: the same calls in the same order)."""
 import os
@@ -32,7 +32,7 @@ def _stream(torch, hist):
     return buf, offs
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, group):
     import torch  # before libowrx_amd.so (tests/conftest.py)
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -44,7 +44,7 @@ def _rank(rank, world, port, q):
         from openwebrx_amd.multi import IqBroadcast, shard_chains
         eng = Engine(FS, max_block=B)
         eng.set_input_retention(8)
-        eng.set_block_pairing(True)
+        eng.set_block_group(group)
         hist = eng.history
         t = torch.tensor([float(hist)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -59,7 +59,7 @@ def _rank(rank, world, port, q):
         mine = shard_chains(items, world, rank, key=lambda it: it[1][1])
         chains = [(i, eng.chain(params.chain_params(FS, o, m))) for i, (o, m) in mine]
         torch.cuda.synchronize()
-        bc = IqBroadcast(torch, dist, "cuda", hist_b, B, stream=buf, retention=8, pair=True)
+        bc = IqBroadcast(torch, dist, "cuda", hist_b, B, stream=buf, retention=8, group=group)
         for j in range(NB):
             if j + 1 < NB:
                 bc.issue(j + 1)
@@ -78,14 +78,15 @@ def _rank(rank, world, port, q):
         q.put((rank, {"error": repr(ex)}))
 
 
-def test_two_ranks_paired_equal_one_engine():
+@pytest.mark.parametrize("group", [2, 4])
+def test_two_ranks_paired_equal_one_engine(group):
     import torch
     import torch.multiprocessing as mp
     from openwebrx_amd import Engine, params, synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, group)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=100) for _ in procs)
@@ -93,8 +94,8 @@ def test_two_ranks_paired_equal_one_engine():
         p.join(30)
     for r in (0, 1):
         assert "error" not in res[r], res[r]
-        # eight blocks as four engine blocks on both ranks: every pair formed
-        assert res[r]["blocks"] == NB // 2, (r, res[r]["blocks"])
+        # eight blocks as 8 / group engine blocks on both ranks: every group formed
+        assert res[r]["blocks"] == NB // group, (r, res[r]["blocks"])
     got = {}
     for r in (0, 1):
         got.update(res[r]["out"])
@@ -104,7 +105,7 @@ def test_two_ranks_paired_equal_one_engine():
     # one engine, every chain, the same blocks paired from one buffer
     eng = Engine(FS, max_block=B)
     eng.set_input_retention(8)
-    eng.set_block_pairing(True)
+    eng.set_block_group(group)
     buf, offs = _stream(torch, eng.history)
     assert list(offs) == list(synth.carrier_offsets(FS, len(MODES)))
     chains = [eng.chain(params.chain_params(FS, o, m)) for o, m in zip(offs, MODES)]

@@ -38,7 +38,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retention=1,
-            pair=False):
+            group=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,7 +46,7 @@ def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retenti
     full = torch.complex(torch.randn(hist + nblocks * block, generator=g),
                          torch.randn(hist + nblocks * block, generator=g))
     bc = IqBroadcast(torch, dist, "cpu", hist, block, stream=full if rank == 0 else None,
-                     retention=retention, pair=pair)
+                     retention=retention, group=group)
     ok = True
     live = []  # the windows an engine with this input retention may still read
     prev = None
@@ -54,9 +54,9 @@ def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retenti
         if pipelined and i + 1 < nblocks:
             bc.issue(i + 1)  # the next block's broadcast is in flight while block i is used
         t, off = bc.wait(i) if pipelined else bc.step(i)
-        if pair and i % 2 == 1:
-            # the pair's second block sits right behind its first one in memory, so a paired
-            # engine (owrx_set_block_pairing) runs the two as one engine block on every rank
+        if group > 1 and i % group:
+            # a group's later blocks sit right behind its first one in memory, so a grouping
+            # engine (owrx_set_block_group) runs them as one engine block on every rank
             ok &= prev is not None and t.data_ptr() + 8 * off == prev[0].data_ptr() + 8 * (prev[1] + block)
         prev = (t, off)
         live = (live + [(i, t, off)])[-retention:]
@@ -70,20 +70,20 @@ def _worker(rank, world, port, hist, block, nblocks, q, pipelined=False, retenti
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined,retention,pair", [(False, 1, False), (True, 1, False),
-                                                       (True, 8, False), (False, 4, True),
-                                                       (True, 4, True), (True, 8, True)])
-def test_iq_broadcast_world2_gloo(pipelined, retention, pair):
+@pytest.mark.parametrize("pipelined,retention,group", [(False, 1, 1), (True, 1, 1), (True, 8, 1),
+                                                        (False, 4, 2), (True, 4, 2), (True, 8, 2),
+                                                        (True, 16, 4)])
+def test_iq_broadcast_world2_gloo(pipelined, retention, group):
     """Every rank reconstructs [history | block] windows equal to rank 0's stream, with the
     broadcasts one at a time or pipelined one block ahead (bench.py's N > 1 loop); with input
     retention r (bench.py sets 8 at every N) the last r blocks' windows stay intact while the
-    next broadcasts land.  pair=True: blocks travel two per broadcast into [history | 2 blocks]
-    windows and each pair is contiguous in memory on every rank, so ranks > 0 pair blocks
-    (owrx_set_block_pairing) as rank 0 does on its recording."""
+    next broadcasts land.  group = 2 (4): blocks travel two (four) per broadcast into
+    [history | group blocks] windows and each group is contiguous in memory on every rank, so
+    ranks > 0 group blocks (owrx_set_block_group) as rank 0 does on its recording."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 14, q, pipelined, retention, pair))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, 1000, 16, q, pipelined, retention, group))
              for r in range(2)]
     for p in procs:
         p.start()
