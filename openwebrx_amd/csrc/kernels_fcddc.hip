@@ -756,24 +756,43 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, const FcSu
     OWRX_FC_SWITCH(M, OWRX_FC_F)
 #undef OWRX_FC_F
     HIPCHK_RET(hipGetLastError());
-    // wave tiles: 32 frames x 32 chains, or 16 frames x 64 chains when a block has <= 16 frames
-    const bool wide = F > 16;
-    const int ctt = wide ? 4 : 8;
-    const int ftt = wide ? 2 : 1;
-    const int ncg = (nchains + 8 * ctt - 1) / (8 * ctt);
-    const int nfg = (F + 16 * ftt - 1) / (16 * ftt);
-    const dim3 gm(M * ncg * nfg);
-    if (Dp % kFcDpAlign) return hipErrorInvalidValue;
-    static const int chain_fastest = [] {  // OWRX_FC_ORDER=kappa: the previous order (A/B)
-        const char* v = getenv("OWRX_FC_ORDER");
-        return (v && strcmp(v, "kappa") == 0) ? 0 : 1;
-    }();
     // the LDS-DMA ring form by default: C3 fc_mac 0.469-0.495 of HBM vs 0.455-0.465 with register
     // operands, 5 815-5 899 vs 5 712-5 788 Msps, same box (profiles/r03al_ab_fc_mac_lds_c3.txt);
     // OWRX_FC_MAC=reg: the register form (A/B)
     static const bool lds_ring = [] {
         const char* v = getenv("OWRX_FC_MAC");
         return !(v && strcmp(v, "reg") == 0);
+    }();
+    // wave tiles: 32 frames x 32 chains, or 16 frames x 64 chains when a block has <= 16 frames.
+    // OWRX_FC_TALL=1 (A/B): 64 frames x 32 chains past 32 frames (grouped blocks: C3 quads,
+    // F = 52), one frame tile and twice the MFMAs per K-block's loads -- but 320 registers, one
+    // wave per SIMD: C3 quads 0.40 of the MFMA peak vs 0.43 with the 32-frame tiles, whose W tile
+    // the frame-tile-fastest decode serves from L2 to the second tile (profiles/r06_fc_tall_ab.txt)
+    static const bool tall_ok = [] {
+        const char* v = getenv("OWRX_FC_TALL");
+        return v && strcmp(v, "1") == 0;
+    }();
+    bool tall = tall_ok && F > 32 && lds_ring;
+    const bool wide = F > 16;
+    int ctt = 0, ftt = 0, ncg = 0, nfg = 0;
+    dim3 gm;
+    auto shape = [&]() {
+        ctt = tall ? 4 : wide ? 4 : 8;
+        ftt = tall ? 4 : wide ? 2 : 1;
+        ncg = (nchains + 8 * ctt - 1) / (8 * ctt);
+        nfg = (F + 16 * ftt - 1) / (16 * ftt);
+        gm = dim3(M * ncg * nfg);
+    };
+    shape();
+    // the tall tiles only in the ring form (below): a grid of one round keeps the register form
+    if (tall && (int)gm.x <= (ncu > 0 ? ncu : 256)) {
+        tall = false;
+        shape();
+    }
+    if (Dp % kFcDpAlign) return hipErrorInvalidValue;
+    static const int chain_fastest = [] {  // OWRX_FC_ORDER=kappa: the previous order (A/B)
+        const char* v = getenv("OWRX_FC_ORDER");
+        return (v && strcmp(v, "kappa") == 0) ? 0 : 1;
     }();
     // the ring where the grid needs two or more workgroups per CU (C3: 512); a grid one round of
     // single workgroups holds (C4's per-GPU share: 128, long K) keeps register operands, which
@@ -790,11 +809,13 @@ hipError_t launch_fc_ddc(int M, const float2* blk, int64_t blk_start, const FcSu
     const bool ring = lds_ring && (int)gk.x > ncu;
     if (form) *form = ring ? ks : 0;  // 0: register form; k >= 1: the ring with k K slices
     if (mac0) HIPCHK_RET(hipEventRecord(mac0, st));
-    if (ring && wide)
+    if (ring && tall)
+        hipLaunchKernelGGL((fc_mac_lds<4, 4, 2>), gk, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y, ks, y_slice);
+    else if (ring && wide)
         hipLaunchKernelGGL((fc_mac_lds<2, 4, 2>), gk, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y, ks, y_slice);
     else if (ring)
         hipLaunchKernelGGL((fc_mac_lds<1, 8, 2>), gk, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y, ks, y_slice);
-    else if (wide)
+    else if (wide)  // (the register form keeps 32-frame tiles: at 64 it spills)
         hipLaunchKernelGGL((fc_mac<2, 4, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);
     else
         hipLaunchKernelGGL((fc_mac<1, 8, false>), gm, dim3(64 * kFcKSplit), 0, st, U, W, w_cs, w_ks, nchains, Fs, F, Dp, M, ncg, chain_fastest, Y);

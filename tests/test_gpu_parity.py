@@ -578,6 +578,52 @@ def test_block_pairing_same_outputs(amd, fs, modes, B, group):
     assert a[2] == b[2]
 
 
+def test_block_quads_tall_gemm_tiles_same_outputs(amd):
+    """BASELINE config 3 (10 Msps, 256 NFM/USB/CW chains, 2^20-sample blocks) grouped in fours
+    (owrx_set_block_group(4)): one DDC GEMM over 52 frames, which takes the 64-frame GEMM tiles
+    (fc_mac_lds<4, 4, 2>) and the frame-tile-fastest decode.  Audio and s-meter byte-identical to
+    pairs and to one block at a time.  (The per-bin GEMM's K order is the same for every tile
+    shape; the tile grids of all three stay unsliced at 256 chains -- fc_kslices -- which a grid
+    with few chains would not, and K slices change the summation order.)"""
+    import numpy as np
+    import torch
+    from openwebrx_amd import _lib, synth
+    fs, B, nb = 10000000, 1 << 20, 4
+    modes = (["nfm", "usb", "cw"] * 86)[:256]
+    offs = synth.carrier_offsets(fs, len(modes))
+    plist = [amd.params.chain_params(fs, o, m) for o, m in zip(offs, modes)]
+    code = {"nfm": 0, "usb": 2, "cw": 3}
+
+    def run(group):
+        eng = amd.Engine(fs, max_block=B)
+        eng.set_input_retention(8)
+        if group > 1:
+            eng.set_block_group(group)
+        chains = [eng.chain(p) for p in plist]
+        h = eng.history
+        buf = torch.zeros(h + nb * B, dtype=torch.complex64, device="cuda")
+        o64 = np.asarray(offs, np.float64)
+        mds = np.asarray([code[m] for m in modes], np.int32)
+        _lib.check(_lib.lib.owrx_synth_iq(0, buf.data_ptr() + 8 * h, nb * B, 0, float(fs), len(mds),
+                                          o64.ctypes.data, mds.ctypes.data, 20251114, 0.01, 0.05),
+                   "owrx_synth_iq")
+        torch.cuda.synchronize()
+        for k in range(nb):
+            eng.process_device(buf.data_ptr() + 8 * (h + k * B), B)
+        eng.sync()
+        st = eng.stats()
+        out = ([c.read_audio() for c in chains], [c.read_smeter().tobytes() for c in chains])
+        eng.close()
+        return out, st
+
+    (a, sa), (b, sb), (c, sc) = run(1), run(4), run(2)
+    assert sa["blocks"] == nb and sb["blocks"] == 1 and sc["blocks"] == 2
+    assert all(len(x) > 0 for x in a[0])
+    for i in range(len(plist)):
+        assert a[0][i] == b[0][i] and a[1][i] == b[1][i], i
+        assert a[0][i] == c[0][i] and a[1][i] == c[1][i], i
+
+
 def test_retention_floor_while_paired(amd):
     """Block pairing needs input retention >= 4 (owrx_set_block_pairing); lowering the retention
     below that afterwards is refused, and the paired engine keeps its retention."""
