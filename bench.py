@@ -161,8 +161,33 @@ def cpu_baseline(fs, n_fft, hop, avg, plist):
             c_ok = c_try
             break
         c_try = int(c_try * 0.85)
+    # the csdr-shaped leg: one thread per module per chain, bounded queues between
+    # modules (oracle/cpu_baseline.c cpb_run_pipeline), the OS scheduling them on this process's
+    # cores; a bounded sample of the same workload
+    _log("cpu baseline: csdr-shaped (thread per module per chain)")
+    fp = lib.cpb_run_pipeline
+    fp.restype = ctypes.c_int64
+    fp.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_float, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    npipe = 1 << 22
+    if npipe not in iq_cache:
+        iq_cache.clear()
+        iq_cache[npipe] = synth.make_iq(fs, npipe, ["nfm"])[0]
+    arr = (orc.ChainParams * len(cps))(*cps)
+    nth = ctypes.c_int(0)
+    t0 = time.perf_counter()
+    rb = fp(iq_cache[npipe].ctypes.data, npipe, n_fft, hop, avg, -70.0, arr, len(cps), ctypes.byref(nth))
+    dtp = time.perf_counter() - t0
+    csdr_shaped = {"value": round(npipe / dtp / 1e6, 3), "unit": "Msps", "cores": allc,
+                   "threads": int(nth.value), "output_bytes": int(rb),
+                   "sample": "%d samples (%.2f s of stream) through the waterfall + %d chains, one "
+                             "thread per module (%d threads) with bounded chunk queues between "
+                             "modules, %.2f s wall on %d cores; chunk-local module state (a timing "
+                             "model, not the exact stream)" % (npipe, npipe / fs, len(cps),
+                                                               nth.value, dtp, allc)}
     return {"value": round(nall / dta / 1e6, 3), "unit": "Msps", "cores": allc,
             "kind": "port",
+            "csdr_shaped": csdr_shaped,
             "one_core_msps": round(n1 / dt1 / 1e6, 4),
             "waterfall_only_msps": round(nw / dtw / 1e6, 3),
             "waterfall_only_cores": 1,

@@ -28,7 +28,7 @@ namespace owrx {
 constexpr int kPostThreads = 256;
 constexpr int kMaxSqBlocks = 1024;
 constexpr int kMaxSqLen = 3072;  // longest squelch block kept in registers while compacting
-constexpr int kBpLds = 6144;     // bandpass input window staged in LDS (48 KiB)
+constexpr int kBpLds = 6400;     // bandpass input window staged in LDS (50 KiB)
 // the staged bandpass on the f32 MFMA (bp_mfma_tiles, round 6); false keeps round 5's packed-FMA
 // direct form (A/B builds: -DOWRX_BP_FMA)
 #ifdef OWRX_BP_FMA
@@ -36,6 +36,10 @@ constexpr bool kBpMfma = false;
 #else
 constexpr bool kBpMfma = true;
 #endif
+// LDS position of bandpass-window sample i: one float2 of padding per 16 with the MFMA tiles,
+// whose 16 lanes of one A-operand read are 16 samples apart (a 16-way bank conflict unpadded,
+// 17 apart = conflict-free)
+OWRX_DEV int bpw(int i) { return kBpMfma ? i + (i >> 4) : i; }
 
 // 1 / prod_{j != i} (i - j) for the 12 Lagrange nodes
 OWRX_DEV float lagrange_den(int i) {
@@ -146,7 +150,7 @@ OWRX_DEV int wfm_audio(const ChainPost& P, ChainStateP& S, int nsq) {
 // 3125-tap complex FIR at 250 kHz) stops after section 1; bp_long then filters it across many
 // workgroups and PHASE 2 (post_tail) runs sections 3-4.
 // The workgroup's LDS, declared by each kernel (post_body has two instantiations in post_parallel)
-constexpr int kBpPad = kBpHist + 48;  // the bandpass taps zero-padded for the MFMA tiles (>= Kp + 16)
+constexpr int kBpPad = 272 + 32;  // the bandpass taps zero-padded for the MFMA tiles (>= Kp + 18)
 struct PostLds {
     ChainStateP S;
     int n_fd;
@@ -157,43 +161,36 @@ struct PostLds {
     uint8_t pass[kMaxSqBlocks];
 };
 
-// Bandpass (complex FIR, nbt taps) on the f32 MFMA: y[j] = sum_t h[t] x[j - t] for the n_fd
-// outputs of the window x[j] = win[kBpHist + j] (history below), written to out[j].  Tiles of 256
-// outputs j = j0 + 16 c + a are one 16 x 16 product D[c][a] = sum_s X[c][s] H[s][a] over
-// s < Kp = nbt + 15 (rounded up to 4): X[c][s] = x[j0 + 16 c + p - s], H[s][a] = h[a - p + s]
-// (p = Kp - nbt), so s runs over the taps t = a - p + s in ascending order and the zero taps
-// outside [0, nbt) are exact no-ops; complex as four real products per k-step (re: h.x x.x then
-// -h.y x.y; im: h.x x.y then h.y x.x).  v_mfma_f32_16x16x4_f32 is a k-ordered f32 fmaf chain
-// (cdna_hip_programming.md, FP32-input MFMA), and each output's row a is its absolute index mod
-// 16 (abs0 = that of j = 0), so every output's arithmetic is the same whatever the block cut:
-// paired / unpaired and sharded runs stay byte-identical.  One tile is 4 x Kp / 4 MFMAs of 32
-// cycles on one wave; the FMA form it replaces issued ~600 dependent VALU ops per output at one
-// wave per SIMD (30-40 of post_parallel's ~50 us per C3 pair, profiles/r05_post_parallel_phases.txt).
-// The window reads are clamped into [0, kBpHist + n_fd): only zero-tap products and outputs past
-// n_fd (not stored) see a clamped value, and it is a finite sample of the window.
-template <typename OUT, typename DBG>
-OWRX_DEV void bp_mfma_tiles(const float2* __restrict__ win, const float2* __restrict__ hp, int nbt,
-                            int n_fd, int64_t abs0, OUT out, DBG dbg) {
+// One tile shape KP (bp_mfma_tiles below picks it).
+template <int KP, typename OUT, typename DBG>
+OWRX_DEV void bp_mfma_tiles_k(const float2* __restrict__ win, const float2* __restrict__ hp, int nbt,
+                              int n_fd, int64_t abs0, OUT out, DBG dbg) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int Kp = (nbt + 18) & ~3;
-    const int p = Kp - nbt;
+    const int p = KP - nbt;
     const int a0 = (int)(abs0 & 15);
     const int ntile = (n_fd + a0 + 255) >> 8;
     const int xmax = kBpHist + n_fd - 1;
     const float2* hq = hp + (lane & 15) + (lane >> 4);
     for (int tl = wv; tl < ntile; tl += kPostThreads / 64) {
         const int j0 = 256 * tl - a0;
-        const int xb = kBpHist + j0 + 16 * (lane & 15) + p - (lane >> 4);
+        const int xi = kBpHist + j0 + 16 * (lane & 15) + p - (lane >> 4);
         f4 ar = {0.0f, 0.0f, 0.0f, 0.0f}, ai = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 6
-        for (int kc = 0; kc < Kp; kc += 4) {
-            const float2 xv = win[min(max(xb - kc, 0), xmax)];
-            const float2 hv = hq[kc];
-            ar = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, hv.x, ar, 0, 0, 0);
-            ai = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, hv.x, ai, 0, 0, 0);
-            ar = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, -hv.y, ar, 0, 0, 0);
-            ai = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, hv.y, ai, 0, 0, 0);
+        // fully unrolled (KP a compile-time constant): the compiler issues the k-steps' LDS reads
+        // ahead of the MFMAs that use them (as a runtime loop every k-step waited for its own
+        // reads, lgkmcnt(0): post_parallel 39 us per C3 pair)
+        float2 xv[KP / 4], hv[KP / 4];
+#pragma unroll
+        for (int k = 0; k < KP / 4; ++k) {
+            xv[k] = win[bpw(min(max(xi - 4 * k, 0), xmax))];
+            hv[k] = hq[4 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < KP / 4; ++k) {
+            ar = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[k].x, hv[k].x, ar, 0, 0, 0);
+            ai = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[k].y, hv[k].x, ai, 0, 0, 0);
+            ar = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[k].y, -hv[k].y, ar, 0, 0, 0);
+            ai = __builtin_amdgcn_mfma_f32_16x16x4f32(xv[k].x, hv[k].y, ai, 0, 0, 0);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -201,11 +198,38 @@ OWRX_DEV void bp_mfma_tiles(const float2* __restrict__ win, const float2* __rest
             if (j >= 0 && j < n_fd) {
                 const float2 y = make_float2(ar[r], ai[r]);
                 out(j, y);
-                dbg(j, win[kBpHist + j], y);
+                dbg(j, win[bpw(kBpHist + j)], y);
             }
         }
     }
 }
+
+// Bandpass (complex FIR, nbt taps) on the f32 MFMA: y[j] = sum_t h[t] x[j - t] for the n_fd
+// outputs of the window x[j] = win[bpw(kBpHist + j)] (history below), written to out[j].  Tiles of
+// 256 outputs j = j0 + 16 c + a are one 16 x 16 product D[c][a] = sum_s X[c][s] H[s][a] over
+// s < Kp (nbt + 15 rounded up to an instantiated 64 / 168 / 272): X[c][s] = x[j0 + 16 c + p - s],
+// H[s][a] = h[a - p + s] (p = Kp - nbt), so s runs over the taps t = a - p + s in ascending order
+// and the zero taps outside [0, nbt) are exact no-ops; complex as four real products per k-step
+// (re: h.x x.x then -h.y x.y; im: h.x x.y then h.y x.x).  v_mfma_f32_16x16x4_f32 is a k-ordered
+// f32 fmaf chain (cdna_hip_programming.md, FP32-input MFMA), and each output's row a is its
+// absolute index mod 16 (abs0 = that of j = 0), so every output's arithmetic is the same whatever
+// the block cut: paired / unpaired and sharded runs stay byte-identical.  One tile is Kp MFMAs of
+// 32 cycles on one wave; the FMA form it replaces issued ~600 dependent VALU ops per output at one
+// wave per SIMD (30-40 of post_parallel's ~50 us per C3 pair, profiles/r05_post_parallel_phases.txt).
+// The window reads are clamped into [0, kBpHist + n_fd): only zero-tap products and outputs past
+// n_fd (not stored) see a clamped value, and it is a finite sample of the window.  nbt <= 257.
+template <typename OUT, typename DBG>
+OWRX_DEV void bp_mfma_tiles(const float2* __restrict__ win, const float2* __restrict__ hp, int nbt,
+                            int n_fd, int64_t abs0, OUT out, DBG dbg) {
+    if (nbt + 15 <= 64)
+        bp_mfma_tiles_k<64>(win, hp, nbt, n_fd, abs0, out, dbg);
+    else if (nbt + 15 <= 168)
+        bp_mfma_tiles_k<168>(win, hp, nbt, n_fd, abs0, out, dbg);
+    else
+        bp_mfma_tiles_k<272>(win, hp, nbt, n_fd, abs0, out, dbg);
+}
+// the tile depth bp_mfma_tiles uses for nbt taps (hp is filled for it)
+OWRX_DEV int bp_mfma_kp(int nbt) { return nbt + 15 <= 64 ? 64 : nbt + 15 <= 168 ? 168 : 272; }
 
 // FUSED (PHASE 0): the block's DDC outputs, FractionalDecimator output (the bandpass window) and
 // bandpass output stay in LDS -- stages 0-4 read and write the chain's global buffers only for
@@ -220,7 +244,8 @@ OWRX_DEV bool post_fits(const ChainPost& P, const StepTable* steps) {
     const double r = P.frac_enabled ? P.frac_rate : 1.0;
     if (!(r >= 0.5)) return false;
     const int64_t nfd = (int64_t)((double)nk / r) + 2;
-    return kBpHist + nfd + kFdHist + nk <= kBpLds && kBpHist + nfd + P.sq_len + nfd <= kBpLds;
+    const int64_t win = kBpHist + nfd + (kBpMfma ? (kBpHist + nfd) / 16 + 1 : 0);  // bpw padding
+    return win + kFdHist + nk <= kBpLds && win + P.sq_len + nfd <= kBpLds;
 }
 
 template <int PHASE, bool FUSED = false>
@@ -272,7 +297,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     }();
     if constexpr (FUSED) {
         if (tid < kFdHist) ddc_l[tid] = ddc_g[tid];
-        sh_x[tid] = fd_buf[tid];  // kBpHist == NT
+        sh_x[bpw(tid)] = fd_buf[tid];  // kBpHist == NT
     }
     if (P.nseg == 1 && P.output != OWRX_OUT_IQ) {
         // one segment (the fast-convolution DDC): eight outputs' loads in flight per thread (the
@@ -380,13 +405,13 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
                 acc.x = fmaf(L, xi.x, acc.x);
                 acc.y = fmaf(L, xi.y, acc.y);
             }
-            if constexpr (FUSED) sh_x[kBpHist + j] = acc;
+            if constexpr (FUSED) sh_x[bpw(kBpHist + j)] = acc;
             else fd_buf[H + j] = acc;
         }
     } else {
         if (tid == 0) sh_n_fd = n_new;
         for (int j = tid; j < n_new; j += NT) {
-            if constexpr (FUSED) sh_x[kBpHist + j] = ddc_buf[kFdHist + j];
+            if constexpr (FUSED) sh_x[bpw(kBpHist + j)] = ddc_buf[kFdHist + j];
             else fd_buf[H + j] = ddc_buf[kFdHist + j];
         }
     }
@@ -453,8 +478,8 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
                 if (j0 + u * NT + tid < pend) sq_l[j0 + u * NT + tid] = v[u];
         }
         if (lds_bp && kBpMfma) {
-            const int Kp = (nbt + 18) & ~3;
-            for (int k = tid; k < Kp + 16; k += NT) {
+            const int Kp = bp_mfma_kp(nbt);
+            for (int k = tid; k < kBpPad; k += NT) {
                 const int t = k - (Kp - nbt);
                 Ls.hp[k] = (t >= 0 && t < nbt) ? bp_taps[t] : make_float2(0.0f, 0.0f);
             }
@@ -463,10 +488,10 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
         }
         __syncthreads();
     } else if (lds_bp) {
-        for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[j] = fd_buf[j];
+        for (int j = tid; j < kBpHist + n_fd; j += NT) sh_x[bpw(j)] = fd_buf[j];
         if (kBpMfma) {
-            const int Kp = (nbt + 18) & ~3;
-            for (int k = tid; k < Kp + 16; k += NT) {
+            const int Kp = bp_mfma_kp(nbt);
+            for (int k = tid; k < kBpPad; k += NT) {
                 const int t = k - (Kp - nbt);
                 Ls.hp[k] = (t >= 0 && t < nbt) ? bp_taps[t] : make_float2(0.0f, 0.0f);
             }
@@ -575,18 +600,20 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
                 ai = fmaf(g.y, v.x, ai);
             }
             y = make_float2(ar, ai);
+        } else if constexpr (FUSED) {
+            y = sh_x[bpw(kBpHist + j)];  // (the LDS window is padded: bpw)
         } else {
             y = x[0];
         }
         sq_buf[pend + j] = y;
         if (P.debug && j < P.dbg_cap) {
-            P.dbg_fd[j] = x[0];
+            P.dbg_fd[j] = FUSED ? y : x[0];
             P.dbg_bp[j] = y;
         }
     }
     __syncthreads();
     if constexpr (FUSED) {
-        fd_buf[tid] = sh_x[n_fd + tid];  // keep the last kBpHist bandpass inputs
+        fd_buf[tid] = sh_x[bpw(n_fd + tid)];  // keep the last kBpHist bandpass inputs
     } else if (P.bp_long) {  // keep the last H bandpass inputs
         move_front<float2>(fd_buf, n_fd, H);
     } else {  // keep the last kBpHist bandpass inputs

@@ -218,3 +218,239 @@ int64_t cpb_run_workload(const float* iq, int64_t n, int N, int hop, int avg, fl
     }
     return total;
 }
+
+/* ---- the csdr-shaped baseline (round 6) -------------------------------------
+ * csdr runs every module of a chain in a thread of its own, modules connected by ring buffers
+ * (csdr/module/__init__.py:36-53 pump threads; pycsdr Buffer / Reader between modules).  This
+ * leg reproduces that structure: per chain one thread per module -- Shift + FirDecimate (one
+ * module pair reading the shared wideband buffer), FractionalDecimator, Bandpass, Squelch, the
+ * demodulator (FmDemod + Limit + NfmDeemphasis | AmDemod + DcBlock | RealPart), Agc, Convert,
+ * AdpcmEncoder -- and for the waterfall Fft + LogAveragePower, FftSwap, FftAdpcm, every pair of
+ * threads joined by a bounded queue of chunks (mutex + condition variables, as pycsdr's Buffer
+ * wakes its readers).  The work per chunk is the same code as the OpenMP leg (fp32 DDC and FFT,
+ * the oracle's 12 kHz tail), each module applied to each chunk on its own (a timing model: a
+ * module's state is not carried from one chunk to the next, so its output is not the exact
+ * stream).  The OS schedules the threads on the cores the process may use. */
+#include <pthread.h>
+
+#define CPB_QCAP 4
+#define CPB_PIPE_CHUNK (1 << 20)
+
+typedef struct {
+    float* data;   /* NULL: end of stream */
+    int64_t n;     /* samples (complex or real) or bytes */
+} cpb_chunk;
+
+typedef struct {
+    cpb_chunk slot[CPB_QCAP];
+    int head, count;
+    pthread_mutex_t mu;
+    pthread_cond_t not_empty, not_full;
+} cpb_queue;
+
+static void q_init(cpb_queue* q) {
+    q->head = q->count = 0;
+    pthread_mutex_init(&q->mu, NULL);
+    pthread_cond_init(&q->not_empty, NULL);
+    pthread_cond_init(&q->not_full, NULL);
+}
+static void q_free(cpb_queue* q) {
+    pthread_mutex_destroy(&q->mu);
+    pthread_cond_destroy(&q->not_empty);
+    pthread_cond_destroy(&q->not_full);
+}
+static void q_push(cpb_queue* q, cpb_chunk c) {
+    pthread_mutex_lock(&q->mu);
+    while (q->count == CPB_QCAP) pthread_cond_wait(&q->not_full, &q->mu);
+    q->slot[(q->head + q->count) % CPB_QCAP] = c;
+    q->count++;
+    pthread_cond_signal(&q->not_empty);
+    pthread_mutex_unlock(&q->mu);
+}
+static cpb_chunk q_pop(cpb_queue* q) {
+    pthread_mutex_lock(&q->mu);
+    while (q->count == 0) pthread_cond_wait(&q->not_empty, &q->mu);
+    cpb_chunk c = q->slot[q->head];
+    q->head = (q->head + 1) % CPB_QCAP;
+    q->count--;
+    pthread_cond_signal(&q->not_full);
+    pthread_mutex_unlock(&q->mu);
+    return c;
+}
+
+enum { ST_DDC, ST_FD, ST_BP, ST_SQ, ST_DEMOD, ST_AGC, ST_CONV, ST_ADPCM, ST_N,
+       ST_WF_FFT = 100, ST_WF_SWAP, ST_WF_ADPCM };
+
+typedef struct {
+    int kind;
+    cpb_queue* in;   /* NULL for the first stage (reads the wideband buffer) */
+    cpb_queue* out;  /* NULL for the last stage */
+    const float* iq;
+    int64_t n;
+    const orc_chain_params* p;
+    int N, hop, avg;
+    float add_db;
+    int64_t produced;
+} cpb_stage;
+
+static void* cpb_stage_run(void* arg) {
+    cpb_stage* s = (cpb_stage*)arg;
+    const orc_chain_params* p = s->p;
+    if (s->kind == ST_DDC || s->kind == ST_WF_FFT) {
+        /* the wideband source in chunks (with the filter / FFT history): 2^20 samples for a chain
+         * (~1 260 outputs at 12 kHz: a whole squelch block, as the chunk-local modules need), one
+         * waterfall row's frames (avg x hop) for the waterfall */
+        const int64_t hist = s->kind == ST_DDC ? p->ntaps : s->N;
+        const int64_t step = s->kind == ST_DDC ? CPB_PIPE_CHUNK : (int64_t)s->avg * s->hop;
+        for (int64_t s0 = 0; s0 + hist < s->n; s0 += step) {
+            const int64_t len = (s0 + step + hist <= s->n) ? step + hist : s->n - s0;
+            cpb_chunk c;
+            if (s->kind == ST_DDC) {
+                float* o = (float*)malloc(sizeof(float) * 2 * (size_t)(len / p->decimation + 2));
+                c.n = cpb_ddc(s->iq + 2 * s0, len, p->shift_rate, p->taps, p->ntaps, p->decimation, o);
+                c.data = o;
+            } else {
+                const int64_t nfr = (len - s->N) / s->hop + 1;
+                const int64_t nr = nfr / s->avg + 1;
+                float* o = (float*)malloc(sizeof(float) * (size_t)s->N * (size_t)nr);
+                c.n = cpb_waterfall(s->iq + 2 * s0, len, s->N, s->hop, s->avg, s->add_db, o);
+                c.data = o;
+            }
+            q_push(s->out, c);
+        }
+        q_push(s->out, (cpb_chunk){NULL, 0});
+        return NULL;
+    }
+    for (;;) {
+        cpb_chunk c = q_pop(s->in);
+        if (!c.data) {
+            if (s->out) q_push(s->out, c);
+            return NULL;
+        }
+        const int64_t m = c.n;
+        cpb_chunk o = {NULL, 0};
+        switch (s->kind) {
+            case ST_FD:
+                if (p->frac_rate != 1.0) {
+                    o.data = (float*)malloc(sizeof(float) * 2 * (size_t)(m + 2));
+                    o.n = orc_fractional_decimator(c.data, m, p->frac_rate, o.data);
+                } else {
+                    o.data = (float*)malloc(sizeof(float) * 2 * (size_t)(m + 1));
+                    memcpy(o.data, c.data, sizeof(float) * 2 * (size_t)m);
+                    o.n = m;
+                }
+                break;
+            case ST_BP:
+                o.data = (float*)malloc(sizeof(float) * 2 * (size_t)(m + 1));
+                if (p->bp_ntaps > 0) orc_fir_complex(c.data, m, p->bp_taps, p->bp_ntaps, o.data);
+                else memcpy(o.data, c.data, sizeof(float) * 2 * (size_t)m);
+                o.n = m;
+                break;
+            case ST_SQ: {
+                float* sm = (float*)malloc(sizeof(float) * (size_t)(m / 4 + 16));
+                int64_t nsm = 0;
+                o.data = (float*)malloc(sizeof(float) * 2 * (size_t)(m + 1));
+                o.n = orc_squelch(c.data, m, p->sq_length, p->sq_decimation, p->sq_hang, p->sq_flush,
+                                  p->sq_report, p->sq_level, o.data, sm, &nsm);
+                free(sm);
+                break;
+            }
+            case ST_DEMOD: {
+                o.data = (float*)malloc(sizeof(float) * (size_t)(m + 1));
+                if (p->mode == 0) {
+                    float* t = (float*)malloc(sizeof(float) * (size_t)(m + 1));
+                    orc_fmdemod(c.data, m, o.data);
+                    orc_limit(o.data, m, 1.0f, t);
+                    orc_deemphasis(t, m, p->deemph_alpha, o.data);
+                    free(t);
+                } else if (p->mode == 1) {
+                    float* t = (float*)malloc(sizeof(float) * (size_t)(m + 1));
+                    orc_amdemod(c.data, m, t);
+                    orc_dcblock(t, m, o.data);
+                    free(t);
+                } else {
+                    orc_realpart(c.data, m, o.data);
+                }
+                o.n = m;
+                break;
+            }
+            case ST_AGC:
+                o.data = (float*)malloc(sizeof(float) * (size_t)(m + 1));
+                orc_agc(c.data, m, &p->agc, o.data);
+                o.n = m;
+                break;
+            case ST_CONV:
+                o.data = (float*)malloc(sizeof(int16_t) * (size_t)(m + 1));
+                orc_convert_f_s16(c.data, m, (int16_t*)o.data);
+                o.n = m;
+                break;
+            case ST_ADPCM: {
+                uint8_t* b = (uint8_t*)malloc((size_t)(m / 2 + 8 * (m / 2 / 1001 + 1) + 16));
+                s->produced += orc_adpcm_encode((const int16_t*)c.data, m, 1, b);
+                free(b);
+                break;
+            }
+            case ST_WF_SWAP: {
+                o.data = (float*)malloc(sizeof(float) * (size_t)s->N * (size_t)(m + 1));
+                for (int64_t r = 0; r < m; r++) orc_fftswap(c.data + r * s->N, s->N, o.data + r * s->N);
+                o.n = m;
+                break;
+            }
+            case ST_WF_ADPCM: {
+                uint8_t* b = (uint8_t*)malloc((size_t)s->N + 16);
+                for (int64_t r = 0; r < m; r++) s->produced += orc_fft_adpcm_row(c.data + r * s->N, s->N, b);
+                free(b);
+                break;
+            }
+        }
+        free(c.data);
+        if (s->out) q_push(s->out, o);
+    }
+}
+
+/* One thread per module per chain (and per waterfall module), bounded queues between them; the
+ * threads run on whatever cores the process may use.  Returns the output bytes (audio + rows);
+ * *nthreads_out = the module threads started. */
+int64_t cpb_run_pipeline(const float* iq, int64_t n, int N, int hop, int avg, float add_db,
+                         const orc_chain_params* p, int nchains, int* nthreads_out) {
+    const int nst = nchains * ST_N + 3;
+    cpb_stage* st = (cpb_stage*)calloc((size_t)nst, sizeof(cpb_stage));
+    cpb_queue* qs = (cpb_queue*)calloc((size_t)nst, sizeof(cpb_queue));
+    pthread_t* th = (pthread_t*)calloc((size_t)nst, sizeof(pthread_t));
+    for (int i = 0; i < nst; i++) q_init(&qs[i]);
+    int k = 0;
+    for (int c = 0; c < nchains; c++) {
+        for (int j = 0; j < ST_N; j++, k++) {
+            st[k].kind = j;
+            st[k].in = j ? &qs[k - 1] : NULL;
+            st[k].out = j + 1 < ST_N ? &qs[k] : NULL;
+            st[k].iq = iq;
+            st[k].n = n;
+            st[k].p = &p[c];
+        }
+    }
+    const int wf_kinds[3] = {ST_WF_FFT, ST_WF_SWAP, ST_WF_ADPCM};
+    for (int j = 0; j < 3; j++, k++) {
+        st[k].kind = wf_kinds[j];
+        st[k].in = j ? &qs[k - 1] : NULL;
+        st[k].out = j + 1 < 3 ? &qs[k] : NULL;
+        st[k].iq = iq;
+        st[k].n = n;
+        st[k].N = N;
+        st[k].hop = hop;
+        st[k].avg = avg;
+        st[k].add_db = add_db;
+    }
+    int started = 0;
+    for (int i = 0; i < nst; i++)
+        if (pthread_create(&th[i], NULL, cpb_stage_run, &st[i]) == 0) started++;
+    int64_t total = 0;
+    for (int i = 0; i < started; i++) pthread_join(th[i], NULL);
+    for (int i = 0; i < nst; i++) total += st[i].produced;
+    for (int i = 0; i < nst; i++) q_free(&qs[i]);
+    free(st);
+    free(qs);
+    free(th);
+    if (nthreads_out) *nthreads_out = started;
+    return started == nst ? total : -1;
+}
