@@ -36,6 +36,12 @@ constexpr bool kBpMfma = false;
 #else
 constexpr bool kBpMfma = true;
 #endif
+// Timing ablations of post_parallel's sections (diagnostic builds only, wrong outputs):
+// -DOWRX_PP_ABL=1 no bandpass arithmetic, 2 no FractionalDecimator interpolation, 4 no demodulator
+// front, 8 no squelch block powers
+#ifndef OWRX_PP_ABL
+#define OWRX_PP_ABL 0
+#endif
 // LDS position of bandpass-window sample i: one float2 of padding per 16 with the MFMA tiles,
 // whose 16 lanes of one A-operand read are 16 samples apart (a 16-way bank conflict unpadded,
 // 17 apart = conflict-free)
@@ -364,7 +370,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     ddc_total = S.ddc_count + n_new;
 
     // ---- 1. FractionalDecimator ------------------------------------------------------------
-    if (P.frac_enabled) {
+    if (P.frac_enabled && !(OWRX_PP_ABL & 2)) {
         if (tid == 0) {
             const double r = P.frac_rate;
             auto valid = [&](int64_t k) {
@@ -457,7 +463,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
 
     // ---- 2. Bandpass (inputs + taps staged in LDS when they fit) ------------------------
     const int pend = S.sq_pending;
-    const int nbt = P.bp_ntaps;
+    const int nbt = (OWRX_PP_ABL & 1) ? 0 : P.bp_ntaps;
     const bool lds_bp = !P.bp_long && nbt > 0 && (kBpHist + n_fd) <= kBpLds;
     // FUSED: the squelch input (the pending samples, then this block's bandpass output) at the
     // top of x[], where the DDC outputs were
@@ -629,7 +635,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     {   // block power: one wave per block, lanes stride the decimated samples
         const int wave = tid >> 6, lane = tid & 63;
         const int nper = (L + P.sq_dec - 1) / P.sq_dec;
-        for (int b = wave; b < nb; b += NT / 64) {
+        for (int b = wave; b < ((OWRX_PP_ABL & 8) ? 0 : nb); b += NT / 64) {
             float p = 0.0f;
             for (int m = lane; m < nper; m += 64) {
                 const float2 v = sq_buf[b * L + m * P.sq_dec];
@@ -672,7 +678,7 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     const int nsq = nb * L;
     const float2 fm_prev0 = S.fm_last;
     const bool sel_out = P.output == OWRX_OUT_SEL;  // the Selector output is the product
-    for (int i = tid; i < nsq; i += NT) {
+    for (int i = tid; i < ((OWRX_PP_ABL & 4) ? 0 : nsq); i += NT) {
         const float2 x = sh_pass[i / L] ? sq_buf[i] : make_float2(0.0f, 0.0f);
         if (sel_out) {
             if (P.debug && i < P.dbg_cap) P.dbg_sq[i] = x;

@@ -436,4 +436,56 @@ OWRX_DEV uint32_t adpcm_encode_rem_o(AdpcmRemO& s, uint32_t xo, const uint2* __r
     return acc;
 }
 
+// The remainder form with 16-B successor records (round 6): {step | (2 index) << 16, h | q << 16,
+// step >> 3, 0}, read with one ds_read_b128, so dq's s3 term comes with the record instead of a
+// v_bfe_u32 per sample (the encoder is issue-bound: one instruction fewer of ~25 per sample).
+// Same record order, index and return value as adpcm_encode_rem; bit-identical.
+template <int EXT>
+OWRX_DEV void adpcm_rem4_fill(uint4 (&NSR)[EXT], int tid, int nthreads) {
+    static_assert(EXT >= kAdpcmRemEntries, "16-B successor table too small");
+    for (int e = tid; e < kAdpcmRemEntries; e += nthreads) {
+        const int i = e >> 4, m = 7 - (e & 7);
+        int ni = i + kAdpcmIndex[m];
+        ni = ni < 0 ? 0 : (ni > 88 ? 88 : ni);
+        const uint32_t st = (uint32_t)kAdpcmStep[ni];
+        NSR[e] = make_uint4(st | ((uint32_t)(ni * 2) << 16), (st >> 1) | ((st >> 2) << 16), st >> 3, 0u);
+    }
+}
+
+struct AdpcmRem4 {
+    uint32_t w0, w1, s3;
+    int pred;
+    OWRX_DEV int index() const { return (int)(w0 >> 17); }
+};
+
+OWRX_DEV AdpcmRem4 adpcm_rem4_state(AdpcmState s) {
+    const uint32_t st = (uint32_t)kAdpcmStep[s.index];
+    return AdpcmRem4{st | ((uint32_t)(s.index * 2) << 16), (st >> 1) | ((st >> 2) << 16), st >> 3, s.pred};
+}
+
+OWRX_DEV uint32_t adpcm_encode_rem4(AdpcmRem4& s, int sample, const uint4* __restrict__ NSR) {
+    const int d = sample - s.pred;
+    const int sgn = d >> 31;
+    const uint32_t a0 = (uint32_t)max(d, -d);
+    const uint32_t w0 = s.w0, w1 = s.w1;
+    uint32_t acc = ((uint32_t)d >> 31) + (w0 >> 16);
+    const uint32_t u4 = a0 - (w0 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u4, 31);
+    const uint32_t a1 = min(a0, u4);
+    const uint32_t u2 = a1 - (w1 & 0xffffu);
+    acc = __builtin_amdgcn_alignbit(acc, u2, 31);
+    const uint32_t a2 = min(a1, u2);
+    const uint32_t u1 = a2 - (w1 >> 16);
+    acc = __builtin_amdgcn_alignbit(acc, u1, 31);
+    const uint32_t a3 = min(a2, u1);
+    const uint4 r = NSR[acc];
+    const int dq = (int)((a0 > a3 ? a0 - a3 : a3 - a0) + s.s3);
+    s.w0 = r.x;
+    s.w1 = r.y;
+    s.s3 = r.z;
+    const int p = s.pred + ((dq ^ sgn) - sgn);
+    s.pred = min(max(p, -32768), 32767);
+    return acc;
+}
+
 }  // namespace owrx

@@ -20,12 +20,15 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
                                            long long* cyc) {
     __shared__ __align__(16) uint2 NSR[kAdpcmRemEntries];
     adpcm_rem_fill(NSR, threadIdx.x, 64);
+    __shared__ __align__(16) uint4 NSR4[V == 2 ? kAdpcmRemEntries : 1];
+    if constexpr (V == 2) adpcm_rem4_fill(NSR4, threadIdx.x, 64);
     __syncthreads();
     const int lane = threadIdx.x;
     const int16_t* src = x + (size_t)lane * (n + 16);
     uint8_t* o = out + (size_t)lane * n;
     AdpcmRem rem = adpcm_rem_state(AdpcmState{0, 0});
     AdpcmRemO remo = adpcm_rem_o_state(AdpcmState{0, 0});
+    AdpcmRem4 rem4 = adpcm_rem4_state(AdpcmState{0, 0});
     int cur[8], nxt[8];
     for (int q = 0; q < 8; ++q) cur[q] = src[q];
     const long long t0 = clock64();
@@ -36,6 +39,9 @@ __global__ void __launch_bounds__(64) kern(const int16_t* __restrict__ x, int n,
         if constexpr (V == 0) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) w |= (adpcm_encode_rem(rem, cur[u], NSR) & 15u) << (4 * u);
+        } else if constexpr (V == 2) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w |= (adpcm_encode_rem4(rem4, cur[u], NSR4) & 15u) << (4 * u);
         } else {
 #pragma unroll
             for (int u = 0; u < 8; ++u)
@@ -92,6 +98,11 @@ int main() {
         run("adpcm_encode_rem (round-5 production)", kern<0>, d0);
         run("adpcm_encode_rem_o (offset predictor, short update)", kern<1>, d1);
     }
+    uint8_t* d2;
+    hipMalloc(&d2, (size_t)S * n);
+    run("adpcm_encode_rem4 (16-B records, s3 in the record)", kern<2>, d2);
+    run("adpcm_encode_rem (round-5 production)", kern<0>, d0);
+    run("adpcm_encode_rem4 (16-B records, s3 in the record)", kern<2>, d2);
     std::vector<uint8_t> a((size_t)S * n), b(a.size());
     hipMemcpy(a.data(), d0, a.size(), hipMemcpyDeviceToHost);
     hipMemcpy(b.data(), d1, b.size(), hipMemcpyDeviceToHost);
@@ -99,5 +110,10 @@ int main() {
     for (int c = 0; c < S; ++c)
         for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
     printf("adpcm_encode_rem_o codes differing: %zu of %d bytes\n", diff, S * n / 2);
+    hipMemcpy(b.data(), d2, b.size(), hipMemcpyDeviceToHost);
+    diff = 0;
+    for (int c = 0; c < S; ++c)
+        for (int i = 0; i < n / 2; ++i) diff += a[(size_t)c * n + i] != b[(size_t)c * n + i];
+    printf("adpcm_encode_rem4 codes differing: %zu of %d bytes\n", diff, S * n / 2);
     return 0;
 }
