@@ -782,9 +782,11 @@ def main():
     ap.add_argument("--no-waterfall", action="store_true")
     ap.add_argument("--no-pairing", action="store_true",
                     help="one engine block per 2^20-sample block (owrx_set_block_pairing off)")
-    ap.add_argument("--block-group", type=int, default=int(os.environ.get("OWRX_BENCH_GROUP", "2")),
+    ap.add_argument("--block-group", type=int, default=int(os.environ.get("OWRX_BENCH_GROUP", "4")),
                     help="contiguous 2^20-sample blocks per engine block (owrx_set_block_group: "
-                         "2 = pairs, 4 = quads; input retention raised to 4 x this when lower)")
+                         "2 = pairs, 4 = quads, the default: driver form 10 124-10 144 vs 9 761-9 838 "
+                         "Msps in pairs, profiles/r06_group_ab.txt; input retention raised to "
+                         "4 x this when lower)")
     ap.add_argument("--realtime-seconds", type=float, default=3.0,
                     help="paced real-time check at 10 Msps through the host push path (0: skip)")
     ap.add_argument("--no-timing", action="store_true",
@@ -1028,6 +1030,13 @@ def main():
     tsteps = max(1, d["timed_blocks"])  # the gpu_ms_* sums cover the timed blocks only
     # caller blocks per engine block (2 when every pair formed: owrx_set_block_pairing)
     per_engine = max(1.0, d["samples_in"] / block / max(1, d["blocks"]))
+    # every rank's grouping (owrx_set_block_group over IqBroadcast(group=g) windows on ranks > 0):
+    # the fewest caller blocks per engine block any rank formed
+    per_engine_min = per_engine
+    if dist:
+        te = torch.tensor([per_engine], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MIN)
+        per_engine_min = float(te.item())
     tblocks = tsteps * per_engine
     launches = d["ddc_launches"]
     ddc_ms = d["gpu_ms_ddc"]
@@ -1267,6 +1276,7 @@ def main():
                 "post_to_encoder_end": round(d["gpu_ms_serial"] / tsteps, 3),
                 "timed_blocks": d["timed_blocks"],
                 "blocks_per_engine_block": round(per_engine, 3),
+                "blocks_per_engine_block_min_over_ranks": round(per_engine_min, 3),
             },
             "pool_allocs_timed": int(d["pool_allocs"]),
             "host_ms_per_block": {k[8:]: round(d[k] / (args.steps * bps), 3) for k in
