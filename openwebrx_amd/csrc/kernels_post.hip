@@ -1211,9 +1211,13 @@ hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const i
 // such a byte, or which runs past a lane's last sample, takes the checked per-sample path.
 // Runs on stream C behind post_serial_front, so block k's encoding overlaps block k+1's front
 // and block k+2's DDC.
-constexpr int kAdChunk = 128;           // samples per staged chunk
+#ifndef OWRX_AD_G
+#define OWRX_AD_G 64
+#endif
+constexpr int kAdG = OWRX_AD_G;         // samples per encoder group (kAdG / 2 byte starts)
+constexpr int kAdChunk = 4 * kAdG;      // samples per staged chunk
 constexpr int kAdQ = kAdChunk / 8;      // 16-B quads (8 samples) per lane and chunk
-constexpr int kAdG = 32;                // samples per encoder group (16 byte starts)
+constexpr int kAdGQ = kAdG / 8;         // quads per encoder group
 constexpr int kAdGroups = kAdChunk / kAdG;
 
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
@@ -1286,27 +1290,27 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     };
     for (int ch = 0; ch < nchunks; ++ch) {
         const uint4(*rg)[64] = ring[ch & 1];
-        uint4 vn[4];
+        uint4 vn[kAdGQ];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) vn[k] = rg[k][lane];
+        for (int k = 0; k < kAdGQ; ++k) vn[k] = rg[k][lane];
         for (int g = 0; g < kAdGroups; ++g) {
             const int i0 = ch * kAdChunk + kAdG * g;
             if (i0 >= nmax) break;
-            uint4 v[4];  // the next group's reads are in flight while this one encodes
+            uint4 v[kAdGQ];  // the next group's reads are in flight while this one encodes
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = vn[k];
+            for (int k = 0; k < kAdGQ; ++k) v[k] = vn[k];
             if (g + 1 < kAdGroups) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) vn[k] = rg[4 * (g + 1) + k][lane];
+                for (int k = 0; k < kAdGQ; ++k) vn[k] = rg[kAdGQ * (g + 1) + k][lane];
             }
-            // sixteen byte starts in the group: bytes K .. K + 15; a frame precedes byte k when
+            // kAdG / 2 byte starts in the group: bytes K .. K + kAdG / 2 - 1; a frame precedes byte k when
             // k % 1001 == 0
             const bool frame_here = kmod == 0 || kmod > kAdpcmSyncPeriod - kAdG / 2;
             const bool slow = sl.active && (frame_here || i0 + kAdG > n);
             if (!__any(slow) && i0 + kAdG <= nmin) {
-                uint32_t w[4];  // the codes ^ 7 (adpcm_encode_rem), fixed below
+                uint32_t w[kAdGQ];  // the codes ^ 7 (adpcm_encode_rem), fixed below
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < kAdGQ; ++k) {
                     const uint32_t wv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
                     // each code enters at the top nibble and the word shifts down by one
                     // (alignbit: one instruction; the record index's high bits fall off)
@@ -1318,18 +1322,25 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
                     }
                     w[k] = acc ^ 0x77777777u;
                 }
-                uint4 b = make_uint4(w[0], w[1], w[2], w[3]);
                 if (pend) {  // bytes start at odd samples: shift the nibble stream by one
-                    b = make_uint4((w[0] << 4) | (uint32_t)left, (w[1] << 4) | (w[0] >> 28),
-                                   (w[2] << 4) | (w[1] >> 28), (w[3] << 4) | (w[2] >> 28));
-                    left = (int)(w[3] >> 28);
+                    uint32_t prev = (uint32_t)left;
+#pragma unroll
+                    for (int k = 0; k < kAdGQ; ++k) {
+                        const uint32_t wk = w[k];
+                        w[k] = (wk << 4) | prev;
+                        prev = wk >> 28;
+                    }
+                    left = (int)prev;
                 }
                 if (sl.active) {
-                    auto* d = reinterpret_cast<__attribute__((address_space(1))) U128Unaligned*>(&out.p[ob]);
-                    d->x = b.x;
-                    d->y = b.y;
-                    d->z = b.z;
-                    d->w = b.w;
+#pragma unroll
+                    for (int q = 0; q < kAdGQ / 4; ++q) {
+                        auto* d = reinterpret_cast<__attribute__((address_space(1))) U128Unaligned*>(&out.p[ob + 16 * q]);
+                        d->x = w[4 * q];
+                        d->y = w[4 * q + 1];
+                        d->z = w[4 * q + 2];
+                        d->w = w[4 * q + 3];
+                    }
                 }
                 ob += kAdG / 2;
                 kmod += kAdG / 2;
@@ -1338,7 +1349,7 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
             }
             // checked path: per sample (read back from the ring), lanes past their end keep
             // their state
-            const uint32_t* gw = reinterpret_cast<const uint32_t*>(&rg[4 * g][0]);
+            const uint32_t* gw = reinterpret_cast<const uint32_t*>(&rg[kAdGQ * g][0]);
             int nib = left;
 #pragma unroll 1
             for (int t = 0; t < kAdG; ++t) {
