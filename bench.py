@@ -259,12 +259,17 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
     gc.collect()
     gc.disable()
     parts = []  # per block: (push, reads) seconds
+    hk = ("host_ms_wait_slots", "host_ms_collect", "host_ms_drain_wait", "host_ms_drain_copy",
+          "host_ms_wait_input", "host_ms_build", "host_ms_launch", "pipeline_drains", "pool_allocs")
+    hparts = []  # per block: the engine's own host-time deltas (hk) over push + reads
+    handles = eng.handles(chains)  # kept in step with `chains` (read_chains takes the array)
     t0 = time.perf_counter()
     for i in range(nblocks):
         deadline = t0 + i * period
         wait = deadline - time.perf_counter()
         if wait > 0:
             time.sleep(wait)
+        sa = eng.stats()
         a = time.perf_counter()
         eng.push(stream_host[(i * block) % (stream_host.size - block):][:block])
         b = time.perf_counter()
@@ -279,10 +284,13 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             wf_set_ms.append(time.perf_counter() - w0)
         if churn and chains:
             c0 = time.perf_counter()
-            chains.pop(int(rng.integers(len(chains)))).close()
+            j = int(rng.integers(len(chains)))
+            chains.pop(j).close()
             c1 = time.perf_counter()
             chains.append(eng.chain(plist[int(rng.integers(len(plist)))]))
             c2 = time.perf_counter()
+            handles[j:-1] = handles[j + 1:].copy()
+            handles[-1] = chains[-1].id
             k = int(rng.integers(len(chains)))
             lo = float(rng.uniform(-0.2, 0.0))
             chains[k].set_bandpass(params.f32(lo), params.f32(lo + 0.15))
@@ -294,9 +302,11 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
         if not pipelined:
             eng.sync()
         d = time.perf_counter()
-        eng.read_chains(chains)
+        eng.read_chains(handles)
         wf.read()
         e = time.perf_counter()
+        sb = eng.stats()
+        hparts.append([round(sb[k] - sa[k], 1) for k in hk])
         ts += d - c
         tr += e - d
         # pipelined: how late the block's push (and this iteration) ran against its deadline
@@ -337,10 +347,15 @@ def realtime_check(Engine, params, fs, n_fft, hop, avg, plist, stream_host, seco
             "blocks": nblocks, "block_period_ms": round(1e3 * period, 2),
             "max_block_latency_ms": round(1e3 * max(lat), 3),
             "mean_block_latency_ms": round(1e3 * sum(lat) / len(lat), 3),
-            # the five latest blocks: [block index, latency, push, reads] in ms
+            # the five latest blocks: [block index, latency, push, reads] in ms, and the
+            # engine's host time in them (worst_blocks_host: hk's deltas over push + reads)
             "worst_blocks": [[i, round(1e3 * lat[i], 1), round(1e3 * parts[i][0], 1),
                               round(1e3 * parts[i][1], 1)]
                              for i in sorted(range(len(lat)), key=lambda i: -lat[i])[:5]],
+            "worst_blocks_host": {"fields": list(hk),
+                                  "blocks": {str(i): hparts[i] for i in
+                                             sorted(range(len(lat)), key=lambda i: -lat[i])[:5]}},
+            "latency_ms_p99": round(1e3 * float(np.percentile(lat, 99)), 3),
             "latency_definition": ("push start to outputs in the host rings (sync per block)"
                                    if not pipelined else
                                    "deadline to the end of the block's push + churn + reads "
@@ -386,7 +401,7 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
         ok = bool(agree(1.0 if ok else 0.0, "min") > 0)
         lvl = {k: r[k] for k in ("chains", "max_block_latency_ms", "mean_block_latency_ms",
                                  "finish_lag_ms", "overruns", "setup_s", "host_per_block",
-                                 "waterfall_rows", "error")
+                                 "waterfall_rows", "worst_blocks", "error")
                if k in r}
         lvl["keeps_up"] = ok
         if world > 1:
@@ -420,8 +435,9 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
                                    wf_cap_ms=wf_cap_ms)
                 ok = bool(agree(1.0 if r["keeps_up"] else 0.0, "min") > 0)
                 h = {k: r[k] for k in ("chains", "seconds", "blocks", "max_block_latency_ms",
-                                       "mean_block_latency_ms", "finish_lag_ms", "overruns",
-                                       "waterfall_rows", "host_per_block") if k in r}
+                                       "mean_block_latency_ms", "latency_ms_p99", "finish_lag_ms",
+                                       "overruns", "waterfall_rows", "host_per_block",
+                                       "worst_blocks", "worst_blocks_host") if k in r}
                 h["keeps_up"] = ok
             except Exception as exc:
                 h = {"chains": C, "error": str(exc)[:200], "keeps_up": False}

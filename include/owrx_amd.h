@@ -254,7 +254,9 @@ int64_t owrx_chain_read_smeter(owrx_engine* e, int handle, float* dst, int64_t m
  * one pump thread per output, owrx/dsp.py:846-863): chain handles[i]'s available bytes / values
  * are appended to dst in order until max_bytes / max_values; lens[i] / counts[i] receive each
  * chain's share.  Returns the total.  Every handle may appear once: a repeated or unknown
- * handle returns OWRX_EINVAL and reads nothing. */
+ * handle returns OWRX_EINVAL and reads nothing.  dst == NULL with max_bytes / max_values == 0
+ * is a size query: lens[i] / counts[i] receive what each chain holds, the sum is returned and
+ * nothing is read (a pump sizes its buffer so one call drains every ring). */
 int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
                                int64_t max_bytes, int64_t* lens);
 int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float* dst,
@@ -343,6 +345,11 @@ typedef struct {
     double  gpu_ms_waterfall_fft_max;  /* the longest timed waterfall FFT + finalize launch */
     int64_t waterfall_timed_launches;  /* the launches gpu_ms_waterfall_fft and
                                           waterfall_timed_samples cover */
+    /* finished blocks moved into the output rings (in host_ms_wait_slots and host_ms_collect):
+     * waiting for a block's chain outputs to land in pinned memory, and copying them into the
+     * chains' rings */
+    double  host_ms_drain_wait;
+    double  host_ms_drain_copy;
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

@@ -115,6 +115,8 @@ class Stats(ctypes.Structure):
         ("pool_allocs", ctypes.c_int64),
         ("gpu_ms_waterfall_fft_max", ctypes.c_double),
         ("waterfall_timed_launches", ctypes.c_int64),
+        ("host_ms_drain_wait", ctypes.c_double),
+        ("host_ms_drain_copy", ctypes.c_double),
     ]
 
 

@@ -441,6 +441,9 @@ struct Chain {
     // and audioBuffer (f32 demodulator-chain output); staging bytes per step, 0 = off
     int64_t tap_sq_cap = 0, tap_agc_cap = 0;
     ByteRing tap_sel, tap_audio;
+    int64_t ring_dropped() const {
+        return audio.dropped + smeter.dropped + sfft.dropped + tap_sel.dropped + tap_audio.dropped;
+    }
     // bumped by owrx_chain_set_secondary_fft / owrx_chain_set_taps: blocks built before the
     // change (still in flight, they are not drained) deliver no rows / tap bytes afterwards
     uint32_t sf_gen = 0, tap_gen = 0;
@@ -682,6 +685,7 @@ struct owrx_engine {
     // setup, buffers + state uploads, bandpass taps, W reserve + build, group refresh, staging
     double cc_ms[6] = {};
     int64_t hl_n[2] = {};
+    int64_t ring_dropped = 0;  // bytes the chains' host rings dropped (oldest first), all time
     bool hl_forced = false;
     int64_t history = kDefaultHistory;
     int64_t pos = 0;  // absolute samples processed
@@ -1256,13 +1260,14 @@ static int drain_slot(owrx_engine* e, int si) {
         }
         // each chain's outputs into its rings: chains are independent, so ranges of them on
         // the host workers; the counters are summed per range
-        std::atomic<int64_t> ov{0}, ab{0}, dd{0};
+        std::atomic<int64_t> ov{0}, ab{0}, dd{0}, dr{0};
         for_range(e, (int64_t)s.post_ids.size(), [&](int64_t k0, int64_t k1) {
-        int64_t overruns = 0, audio_bytes = 0, ddc_outputs = 0;
+        int64_t overruns = 0, audio_bytes = 0, ddc_outputs = 0, dropped = 0;
         for (int64_t k = k0; k < k1; ++k) {
             auto it = e->chains.find(s.post_ids[k]);
             if (it == e->chains.end()) continue;
             Chain* c = it->second.get();
+            const int64_t dropped0 = c->ring_dropped();
             const ChainCounts& cc = s.h_counts[k];
             const PostLayout& L = s.layout[k];  // as this block was built
             const int64_t nb = std::min<int64_t>(cc.out_bytes, L.out_cap);
@@ -1291,6 +1296,7 @@ static int drain_slot(owrx_engine* e, int si) {
             ddc_outputs += cc.n_ddc;
             c->smeter.push((const uint8_t*)(s.h_sm + (int64_t)k * e->sm_stride),
                            sizeof(float) * (size_t)std::min<int64_t>(cc.smeter, e->sm_stride));
+            dropped += c->ring_dropped() - dropped0;
             if (s.debug && s.h_dbg) {
                 const uint8_t* base = s.h_dbg + (int64_t)k * kDebugStages * e->dbg_stride;
                 const int64_t cnt[kDebugStages] = {cc.n_ddc,  cc.n_fd,    cc.n_bp,
@@ -1305,11 +1311,15 @@ static int drain_slot(owrx_engine* e, int si) {
         ov += overruns;
         ab += audio_bytes;
         dd += ddc_outputs;
+        dr += dropped;
         });
         e->stats.overruns += ov.load();
+        e->ring_dropped += dr.load();
         e->stats.audio_bytes += ab.load();
         e->stats.ddc_outputs += dd.load();
         e->hl_push[hk] += now_ms() - th1;
+        e->stats.host_ms_drain_wait += th1 - th0;
+        e->stats.host_ms_drain_copy += now_ms() - th1;
     } else if (s.timed) {
         float ms = 0;
         RCCHK(wait_ev(e, s.a3));
@@ -3518,7 +3528,8 @@ static bool batched_duplicates(owrx_engine* e, const std::vector<Chain*>& cs) {
 int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_t* dst,
                                int64_t max_bytes, int64_t* lens) {
     ENGINE_GUARD_HELD(e);
-    if (n < 0 || (n > 0 && (!handles || !dst || !lens)) || max_bytes < 0) return OWRX_EINVAL;
+    const bool query = !dst && max_bytes == 0;  // size query: nothing is read
+    if (n < 0 || (n > 0 && (!handles || (!dst && !query) || !lens)) || max_bytes < 0) return OWRX_EINVAL;
     // sizes first (each chain's ring, on the host workers), offsets (in order, up to max_bytes),
     // then the copies (workers again)
     std::vector<Chain*> cs((size_t)n);
@@ -3532,6 +3543,11 @@ int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_
         }
     });
     if (bad || batched_duplicates(e, cs)) return OWRX_EINVAL;
+    if (query) {
+        int64_t total = 0;
+        for (int i = 0; i < n; ++i) total += lens[i];
+        return total;
+    }
     std::vector<int64_t> offs((size_t)n);
     int64_t off = 0;
     for (int i = 0; i < n; ++i) {
@@ -3548,7 +3564,8 @@ int64_t owrx_chains_read_audio(owrx_engine* e, int n, const int* handles, uint8_
 int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float* dst,
                                 int64_t max_values, int64_t* counts) {
     ENGINE_GUARD_HELD(e);
-    if (n < 0 || (n > 0 && (!handles || !dst || !counts)) || max_values < 0) return OWRX_EINVAL;
+    const bool query = !dst && max_values == 0;  // size query: nothing is read
+    if (n < 0 || (n > 0 && (!handles || (!dst && !query) || !counts)) || max_values < 0) return OWRX_EINVAL;
     std::vector<Chain*> cs((size_t)n);
     std::atomic<bool> bad{false};
     for_range(e, n, [&](int64_t a, int64_t b) {
@@ -3560,6 +3577,11 @@ int64_t owrx_chains_read_smeter(owrx_engine* e, int n, const int* handles, float
         }
     });
     if (bad || batched_duplicates(e, cs)) return OWRX_EINVAL;
+    if (query) {
+        int64_t total = 0;
+        for (int i = 0; i < n; ++i) total += counts[i];
+        return total;
+    }
     std::vector<int64_t> offs((size_t)n);
     int64_t off = 0;
     for (int i = 0; i < n; ++i) {
@@ -3716,12 +3738,9 @@ int owrx_get_stats(owrx_engine* e, owrx_stats* s) {
     ENGINE_GUARD_HELD(e);
     if (!s) return OWRX_EINVAL;
     *s = e->stats;
-    int64_t dropped = 0;
-    for (auto& kv : e->chains) {
-        const Chain& c = *kv.second;
-        dropped += c.audio.dropped + c.smeter.dropped + c.sfft.dropped + c.tap_sel.dropped +
-                   c.tap_audio.dropped;
-    }
+    // the chains' ring drops are summed as they happen (drain_slot): no pass over 10^5 chains
+    // per call
+    int64_t dropped = e->ring_dropped;
     for (auto& kv : e->wfs) dropped += kv.second->ring.dropped;
     s->overruns += dropped;
     return OWRX_OK;

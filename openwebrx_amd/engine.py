@@ -2,6 +2,7 @@
 (FftChain) and Chain (ClientDemodulatorChain) objects attached to it.  Thin: every call goes
 straight to libowrx_amd.so."""
 import ctypes
+import threading
 
 import numpy as np
 
@@ -13,14 +14,32 @@ _STAGE_DTYPE = {0: np.complex64, 1: np.complex64, 2: np.complex64, 3: np.complex
                 4: np.float32, 5: np.float32}
 
 
-_SCRATCH = {}
+_TLS = threading.local()  # read buffers per thread: pump threads of several engines read at once
+
+
+def _scratch_map():
+    m = getattr(_TLS, "bufs", None)
+    if m is None:
+        m = _TLS.bufs = {}
+    return m
 
 
 def _scratch(nbytes):
     """Reusable host buffer for ring reads (avoids a fresh multi-MB allocation per call)."""
-    b = _SCRATCH.get(nbytes)
+    m = _scratch_map()
+    b = m.get(nbytes)
     if b is None:
-        b = _SCRATCH[nbytes] = np.empty(nbytes, dtype=np.uint8)
+        b = m[nbytes] = np.empty(nbytes, dtype=np.uint8)
+    return b
+
+
+def _grown(key, n, dtype):
+    """A reusable buffer of at least n items for `key`, grown geometrically (read_chains)."""
+    m = _scratch_map()
+    b = m.get(key)
+    if b is None or b.size < n:
+        b = m[key] = np.empty(max(n, int(1.5 * (b.size if b is not None else 0)), 1 << 16),
+                              dtype=dtype)
     return b
 
 
@@ -155,42 +174,49 @@ class Engine:
         check(lib.owrx_get_stats(self._h, ctypes.byref(s)), "owrx_get_stats")
         return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
 
-    def read_chains(self, chains, max_bytes=64 << 20, max_values=1 << 20):
-        """Drains the audio and s-meter rings of many chains with two native calls
-        (owrx_chains_read_audio / owrx_chains_read_smeter) -- the one-thread pump for a server with
-        hundreds of clients.  Returns (audio, alens, smeter, scounts): the concatenated bytes and
-        float values as numpy arrays plus each chain's share, in the order of `chains`."""
+    @staticmethod
+    def handles(chains):
+        """The chains' native handles as an int32 array (for read_chains)."""
+        return np.fromiter((c.id for c in chains), dtype=np.int32, count=len(chains))
+
+    def read_chains(self, chains, max_bytes=None, max_values=None):
+        """Drains the audio and s-meter rings of many chains (owrx_chains_read_audio /
+        owrx_chains_read_smeter) -- the one-thread pump for a server with many clients.  Returns
+        (audio, alens, smeter, scounts): the concatenated bytes and float values as numpy arrays
+        plus each chain's share, in the order of `chains`.  The arrays are views of reused read
+        buffers: valid until the next read_chains call.
+
+        max_bytes / max_values None (default): everything the rings hold -- a size query, then
+        one read into a buffer of that size (at 131 072 C3 chains a block leaves ~80 MB of
+        audio: a fixed 64 MiB buffer left the rest to pile up in the rings, whose growth then
+        stalled the drains).  A number caps the call (the rest stays in the rings).
+
+        `chains` may also be an int32 array of chain handles (`Engine.handles`): a server that
+        keeps one pays no Python pass over its chain objects per read (~8 ms at 131 072 chains)."""
         n = len(chains)
-        handles = np.fromiter((c.id for c in chains), dtype=np.int32, count=n)
+        if isinstance(chains, np.ndarray):
+            handles = np.ascontiguousarray(chains, dtype=np.int32)
+        else:
+            handles = self.handles(chains)
+        ph = handles.ctypes.data_as(_lib._pi32)
         alens = np.zeros(n, np.int64)
-        abuf = _scratch(max_bytes)
-        na = check(lib.owrx_chains_read_audio(self._h, n, handles.ctypes.data_as(_lib._pi32),
-                                              abuf.ctypes.data, max_bytes,
-                                              alens.ctypes.data_as(_lib._pi64)), "read_chains")
-        # s-meter values: a call that fills the buffer leaves the later chains' values in their
-        # rings; read again until a call comes back short, then put each chain's pieces together
-        rounds = []
-        while True:
-            sbuf = np.empty(max_values, np.float32)
-            cnt = np.zeros(n, np.int64)
-            ns = check(lib.owrx_chains_read_smeter(self._h, n, handles.ctypes.data_as(_lib._pi32),
-                                                   sbuf.ctypes.data, max_values,
-                                                   cnt.ctypes.data_as(_lib._pi64)), "read_chains")
-            rounds.append((sbuf[:ns], cnt))
-            if ns < max_values:
-                break
-        if len(rounds) == 1:
-            return abuf[:na], alens, rounds[0][0], rounds[0][1]
-        # chain i's values: its piece of round 0, then of round 1, ... (vectorised scatter)
-        scounts = sum(c for _, c in rounds)
-        start = np.concatenate(([0], np.cumsum(scounts)[:-1]))  # chain i's output offset
-        out = np.empty(int(scounts.sum()), np.float32)
-        before = np.zeros(n, np.int64)  # chain i's values placed by the earlier rounds
-        for buf, c in rounds:
-            src0 = np.concatenate(([0], np.cumsum(c)[:-1]))
-            out[np.repeat(start + before - src0, c) + np.arange(buf.size)] = buf
-            before += c
-        return abuf[:na], alens, out, scounts
+        scounts = np.zeros(n, np.int64)
+        pl, pc = alens.ctypes.data_as(_lib._pi64), scounts.ctypes.data_as(_lib._pi64)
+        if max_bytes is None:
+            max_bytes = check(lib.owrx_chains_read_audio(self._h, n, ph, None, 0, pl), "read_chains")
+        if max_values is None:
+            max_values = check(lib.owrx_chains_read_smeter(self._h, n, ph, None, 0, pc), "read_chains")
+        abuf = _grown("read_audio", max_bytes, np.uint8)
+        sbuf = _grown("read_smeter", max_values, np.float32)
+        na = check(lib.owrx_chains_read_audio(self._h, n, ph, abuf.ctypes.data, max_bytes, pl),
+                   "read_chains") if max_bytes > 0 else 0
+        ns = check(lib.owrx_chains_read_smeter(self._h, n, ph, sbuf.ctypes.data, max_values, pc),
+                   "read_chains") if max_values > 0 else 0
+        if max_bytes == 0:
+            alens[:] = 0
+        if max_values == 0:
+            scounts[:] = 0
+        return abuf[:na], alens, sbuf[:ns], scounts
 
     def waterfall(self, fft_size, every_n_samples, avg_number, add_db=-70.0, adpcm=True):
         return Waterfall(self, fft_size, every_n_samples, avg_number, add_db, adpcm)

@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -42,7 +44,9 @@ def test_engine_create_without_device_raises():
         Engine(10e6)
 
 
-def test_chain_params_struct_layout_matches_header():
+@pytest.mark.parametrize("ctype,cname", [("ChainParams", "owrx_chain_params"),
+                                         ("Stats", "owrx_stats")])
+def test_struct_layout_matches_header(ctype, cname):
     from openwebrx_amd import _lib
     # int/float fields are 4 bytes, frac_rate is an 8-byte double at offset 16
     assert _lib.ChainParams.frac_rate.offset == 16
@@ -52,10 +56,11 @@ def test_chain_params_struct_layout_matches_header():
     import tempfile
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
-    names = [n for n, _ in _lib.ChainParams._fields_]
+    st = getattr(_lib, ctype)
+    names = [n for n, _ in st._fields_]
     prog = ('#include <stdio.h>\n#include <stddef.h>\n#include "owrx_amd.h"\nint main(void){'
-            + "".join('printf("%%zu\\n", offsetof(owrx_chain_params, %s));' % n for n in names)
-            + 'printf("%zu\\n", sizeof(owrx_chain_params)); return 0;}')
+            + "".join('printf("%%zu\\n", offsetof(%s, %s));' % (cname, n) for n in names)
+            + 'printf("%%zu\\n", sizeof(%s)); return 0;}' % cname)
     inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
     with tempfile.TemporaryDirectory() as d:
         src, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
@@ -64,7 +69,7 @@ def test_chain_params_struct_layout_matches_header():
         subprocess.run(["gcc", "-I", inc, src, "-o", exe], check=True)
         got = [int(v) for v in subprocess.run([exe], capture_output=True, text=True,
                                               check=True).stdout.split()]
-    want = [getattr(_lib.ChainParams, n).offset for n in names] + [ctypes.sizeof(_lib.ChainParams)]
+    want = [getattr(st, n).offset for n in names] + [ctypes.sizeof(st)]
     assert got == want
 
 

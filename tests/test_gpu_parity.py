@@ -477,9 +477,32 @@ def test_read_chains_rejects_duplicate_handles(amd):
     eng.sync()
     with pytest.raises(Exception):
         eng.read_chains([a, b, a])
-    audio, lens, _, _ = eng.read_chains([a, b])
+    with pytest.raises(Exception):
+        eng.read_chains(eng.handles([a, b, a]))
+    # half the stream read by chain objects, the rest by a handle array: same bytes as one read
+    # of a twin engine
+    audio, lens, sm, sc = eng.read_chains([a, b])
+    audio = audio.copy()  # a view of the engine's read scratch, reused by the next read
     assert lens[0] > 0 and lens[1] > 0
+    for i in range(0, iq.size, 1 << 16):
+        eng.push(iq[i:i + (1 << 16)])
+    eng.sync()
+    audio2, lens2, sm2, sc2 = eng.read_chains(eng.handles([a, b]))
+    audio2 = audio2.copy()
     eng.close()
+    twin = amd.Engine(fs, max_block=1 << 16)
+    a2, b2 = (twin.chain(amd.params.chain_params(fs, o, m)) for o, m in zip(offs, ["nfm", "am"]))
+    for _ in range(2):
+        for i in range(0, iq.size, 1 << 16):
+            twin.push(iq[i:i + (1 << 16)])
+    twin.sync()
+    ta, tl, tsm, tsc = twin.read_chains([a2, b2])
+    twin.close()
+    for k in range(2):
+        got = audio[lens[:k].sum():lens[:k + 1].sum()].tobytes() + \
+            audio2[lens2[:k].sum():lens2[:k + 1].sum()].tobytes()
+        assert got == ta[tl[:k].sum():tl[:k + 1].sum()].tobytes()
+    assert np.array_equal(np.concatenate([sm[:sc[0]], sm2[:sc2[0]], sm[sc[0]:], sm2[sc2[0]:]]), tsm)
 
 
 def test_input_retention_same_outputs(amd):
@@ -1285,13 +1308,25 @@ def test_batched_chain_reads_equal_per_chain_reads(amd):
     for i, ch in enumerate(c1):
         assert ch.read_audio() == audio[ao[i]:ao[i + 1]].tobytes(), i
         assert np.array_equal(ch.read_smeter(), sm[so[i]:so[i + 1]]), i
+    audio, sm, alens, scounts = audio.copy(), sm.copy(), alens.copy(), scounts.copy()
     again, alens2, _, _ = e2.read_chains(c2)
     assert again.size == 0 and not alens2.any()
-    # a value buffer smaller than the pending s-meter values: several native reads, each chain's
-    # pieces put back together in order
+    # capped reads: the chains in order until the cap, the rest stays in the rings for the next
+    # (uncapped: size query + one read) call; each chain's pieces put together equal one read
     e3, c3 = _run_chains(amd, iq, fs, plist, 1 << 17, debug=False)
-    _, _, sm3, sc3 = e3.read_chains(c3, max_values=5)
-    assert np.array_equal(sc3, scounts) and np.array_equal(sm3, sm)
+    a3, al3, sm3, sc3 = (x.copy() for x in e3.read_chains(c3, max_bytes=1000, max_values=5))
+    assert al3.sum() == a3.size == 1000 and sc3.sum() == sm3.size == 5
+    assert a3.tobytes() == audio[:1000].tobytes() and np.array_equal(sm3, sm[:5])
+    a4, al4, sm4, sc4 = e3.read_chains(c3)
+    assert np.array_equal(al3 + al4, alens) and np.array_equal(sc3 + sc4, scounts)
+    o3, o4 = np.concatenate([[0], np.cumsum(al3)]), np.concatenate([[0], np.cumsum(al4)])
+    for i in range(len(c3)):
+        assert (a3[o3[i]:o3[i + 1]].tobytes() + a4[o4[i]:o4[i + 1]].tobytes()
+                == audio[ao[i]:ao[i + 1]].tobytes()), i
+    q3, q4 = np.concatenate([[0], np.cumsum(sc3)]), np.concatenate([[0], np.cumsum(sc4)])
+    for i in range(len(c3)):
+        assert np.array_equal(np.concatenate([sm3[q3[i]:q3[i + 1]], sm4[q4[i]:q4[i + 1]]]),
+                              sm[so[i]:so[i + 1]]), i
     e1.close()
     e2.close()
     e3.close()
