@@ -401,7 +401,7 @@ def max_realtime_chains(Engine, params, fs, n_fft, hop, avg, modes, offsets_of, 
         ok = bool(agree(1.0 if ok else 0.0, "min") > 0)
         lvl = {k: r[k] for k in ("chains", "max_block_latency_ms", "mean_block_latency_ms",
                                  "finish_lag_ms", "overruns", "setup_s", "host_per_block",
-                                 "waterfall_rows", "worst_blocks", "error")
+                                 "waterfall_rows", "worst_blocks", "worst_blocks_host", "error")
                if k in r}
         lvl["keeps_up"] = ok
         if world > 1:

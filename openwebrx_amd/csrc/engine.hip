@@ -285,6 +285,15 @@ struct ByteRing {  // host-side output queue
         }
     }
     size_t avail() const { return buf.size() - rd; }
+    // capacity for n bytes, its pages touched now: at 10^5 chains the rings otherwise grow
+    // together (every chain's output is the same size) and one block's drain takes the page
+    // faults of hundreds of MB of fresh heap (100-200 ms drains at 196 608 chains)
+    void prime(size_t n) {
+        if (buf.capacity() >= n) return;
+        const size_t keep = buf.size();
+        buf.resize(std::max(n, keep));
+        buf.resize(keep);
+    }
     void clear() {
         buf.clear();
         rd = 0;
@@ -3340,6 +3349,10 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
                  : p->output == OWRX_OUT_S16 ? 2 * an + 64
                                              : 4 * an + 64;
     c->sm_cap = p->output == OWRX_OUT_IQ ? 4 : (int)(scap / p->sq_length + 4);
+    // the host rings: room for three blocks' outputs (the reader drains once per block; a drain
+    // may land two or three blocks first)
+    c->audio.prime((size_t)(3 * c->out_cap));
+    c->smeter.prime(3 * sizeof(float) * (size_t)c->sm_cap);
     if (p->output != OWRX_OUT_IQ && scap / p->sq_length + 2 > 1024) {  // kMaxSqBlocks
         set_last_error("owrx_chain_create: squelch length %d too short for the block size",
                        p->sq_length);
