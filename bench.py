@@ -813,7 +813,7 @@ def main():
                     help="chains of the paced churn check (join + leave + setBandpass every "
                          "block, no per-block sync; 0: skip)")
     ap.add_argument("--capacity-ladder",
-                    default="256,1024,4096,16384,32768,65536,98304,131072,196608,262144",
+                    default="256,1024,4096,16384,32768,65536,98304,131072,196608,221184,262144",
                     help="chain counts tried by the max_realtime_chains sweep ('' = skip)")
     ap.add_argument("--capacity-seconds", type=float, default=2.0,
                     help="seconds of paced stream per sweep level")
