@@ -3351,8 +3351,9 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
     c->sm_cap = p->output == OWRX_OUT_IQ ? 4 : (int)(scap / p->sq_length + 4);
     // the host rings: room for three blocks' outputs (the reader drains once per block; a drain
     // may land two or three blocks first)
-    c->audio.prime((size_t)(3 * c->out_cap));
-    c->smeter.prime(3 * sizeof(float) * (size_t)c->sm_cap);
+    // (at most 1 MiB each: an IQ chain's block can be hundreds of KB)
+    c->audio.prime(std::min<size_t>((size_t)(3 * c->out_cap), 1u << 20));
+    c->smeter.prime(std::min<size_t>(3 * sizeof(float) * (size_t)c->sm_cap, 1u << 20));
     if (p->output != OWRX_OUT_IQ && scap / p->sq_length + 2 > 1024) {  // kMaxSqBlocks
         set_last_error("owrx_chain_create: squelch length %d too short for the block size",
                        p->sq_length);
