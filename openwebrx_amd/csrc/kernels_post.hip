@@ -464,7 +464,8 @@ OWRX_DEV void post_body(const ChainPost& Pin, ChainCounts& cnt, PostLds& Ls,
     // ---- 2. Bandpass (inputs + taps staged in LDS when they fit) ------------------------
     const int pend = S.sq_pending;
     const int nbt = (OWRX_PP_ABL & 1) ? 0 : P.bp_ntaps;
-    const bool lds_bp = !P.bp_long && nbt > 0 && (kBpHist + n_fd) <= kBpLds;
+    // (the MFMA form's window is padded, bpw: its last entry must lie inside x[] too)
+    const bool lds_bp = !P.bp_long && nbt > 0 && bpw(kBpHist + n_fd - 1) < kBpLds;
     // FUSED: the squelch input (the pending samples, then this block's bandpass output) at the
     // top of x[], where the DDC outputs were
     float2* const sq_l = sh_x + (kBpLds - pend - n_fd);
