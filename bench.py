@@ -976,6 +976,8 @@ def main():
                 eng.process_device(base + 8 * (j % loop if loop else j) * block, block)
                 dt_ = time.perf_counter() - t0
                 host_s["process"] += dt_
+                if call_log is not None and i >= prime + args.warmup and len(call_log) < 64:
+                    call_log.append(("process", j, round(1e3 * dt_, 3)))
                 if i >= prime + args.warmup:
                     host_s["process_t"] += dt_
             else:  # the one exchange step: rank 0's block to every rank over RCCL
@@ -990,8 +992,15 @@ def main():
                 if rank != 0:
                     eng.wait_stream(torch.cuda.current_stream(dev).cuda_stream)
                 eng.process_device(t.data_ptr() + 8 * off, block)
+        if call_log is not None and i >= prime + args.warmup and len(call_log) < 64:
+            t1 = time.perf_counter()
+            n = drain()
+            call_log.append(("drain", i, round(1e3 * (time.perf_counter() - t1), 3)))
+            return n
         return drain()
 
+    # OWRX_BENCH_CALLS=1: the host time of each call of the first timed steps (diagnostic)
+    call_log = [] if os.environ.get("OWRX_BENCH_CALLS") else None
     for i in range(prime + args.warmup):
         step(i)
     # the Python driver's garbage collector stalls the host for milliseconds at times; keep it
@@ -1000,6 +1009,12 @@ def main():
     gc.collect()
     gc.disable()
     eng.sync()
+    # the warm-up's last outputs (what the sync above completed: its held blocks, the pending
+    # waterfall batch's rows) are read here, with the warm-up: left in the rings, the first timed
+    # step's read took them (0.8 ms of host time, and the host launched the second timed engine
+    # block that much later: stream C then idled ~0.6 ms).  OWRX_BENCH_PREDRAIN=0: the old order (A/B)
+    if os.environ.get("OWRX_BENCH_PREDRAIN", "1") != "0":
+        drain()
     # HIP events in every 8th block (each block's events cost host time: ~8 more API calls; the
     # waterfall's batched launches are all timed)
     eng.set_timing(not args.no_timing, every=8)
@@ -1033,6 +1048,8 @@ def main():
     print("host seconds over all steps: process_device %.4f, step total %.4f, wall %.4f"
           % (host_s["process"], host_s["drain"], dt), file=sys.stderr)
     print("step marks (ms): " + " ".join("%.2f" % (1e3 * m) for m in marks), file=sys.stderr)
+    if call_log:
+        print("first timed calls (ms): " + " ".join("%s%d:%.3f" % c for c in call_log), file=sys.stderr)
     samples = args.steps * bps * block
     value = samples / dt / 1e6  # the one ingested stream, at any N (chains scale with N)
     ms_step = dt * 1e3 / args.steps
