@@ -1208,8 +1208,8 @@ hipError_t launch_chain_afc(const ChainPost* posts, ChainCounts* counts, const i
 // Byte stream: low nibble first; a byte started by the last sample of a block completes with
 // the next block's first sample (has_left).  Frames: "SYNC" + (index, predictor) before every
 // byte whose index in the chain's byte stream is a multiple of 1001 (AudioEngine.js:449-491),
-// written with the state before that byte's first sample.  A group in which any lane starts
-// such a byte, or which runs past a lane's last sample, takes the checked per-sample path.
+// written with the state before that byte's first sample.  A group in which a lane starts such a
+// byte, or in which a lane's samples end, runs a variant of the same unrolled encoder (below).
 // Runs on stream C behind post_serial_front, so block k's encoding overlaps block k+1's front
 // and block k+2's DDC.
 #ifndef OWRX_AD_G
@@ -1238,11 +1238,8 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     const int c = sl.c;
     const ChainPost* Pp = posts + c;
     const int n = sl.active ? (int)counts[c].n_sq : 0;
-    int nmax = n, nmin = sl.active ? n : INT_MAX;
-    for (int o = 32; o > 0; o >>= 1) {
-        nmax = max(nmax, __shfl_xor(nmax, o));
-        nmin = min(nmin, __shfl_xor(nmin, o));
-    }
+    int nmax = n;
+    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
     const int nchunks = (nmax + kAdChunk - 1) / kAdChunk;
     const auto src = gp(reinterpret_cast<const uint4*>(Pp->s16));  // 16-B aligned slot
 
@@ -1278,17 +1275,6 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
     const auto out = gp(Pp->out);
     const int64_t cap = Pp->out_cap;
     int ob = 0;  // bytes staged this block (< 2^31)
-    auto frame = [&]() {
-        if (sl.active && ob + 8 <= cap) {
-            out[ob] = (uint8_t)'S';
-            out[ob + 1] = (uint8_t)'Y';
-            out[ob + 2] = (uint8_t)'N';
-            out[ob + 3] = (uint8_t)'C';
-            const uint32_t w1 = (uint32_t)(uint16_t)ad.index() | ((uint32_t)(uint16_t)ad.pred << 16);
-            for (int b = 0; b < 4; ++b) out[ob + 4 + b] = (uint8_t)(w1 >> (8 * b));
-        }
-        ob += 8;
-    };
     for (int ch = 0; ch < nchunks; ++ch) {
         const uint4(*rg)[64] = ring[ch & 1];
         uint4 vn[kAdGQ];
@@ -1305,11 +1291,31 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
                 for (int k = 0; k < kAdGQ; ++k) vn[k] = rg[kAdGQ * (g + 1) + k][lane];
             }
             // kAdG / 2 byte starts in the group: bytes K .. K + kAdG / 2 - 1; a frame precedes byte k when
-            // k % 1001 == 0
-            const bool frame_here = kmod == 0 || kmod > kAdpcmSyncPeriod - kAdG / 2;
-            const bool slow = sl.active && (frame_here || i0 + kAdG > n);
-            if (!__any(slow) && i0 + kAdG <= nmin) {
-                uint32_t w[kAdGQ];  // the codes ^ 7 (adpcm_encode_rem), fixed below
+            // k % 1001 == 0, here the group's start fb (< 0: none), whose first sample is sf.  Every
+            // group runs the unrolled encoder; two conditions take variants of it instead of the
+            // per-sample path rounds 2-5 used:
+            //  - a lane with a frame (chains that joined at different blocks have their frames at
+            //    different starts: nearly every group has such a lane in a server, 1 - (1 -
+            //    32 / 1001)^64 = 87 %): the state before sample sf is captured in passing and the
+            //    frame goes into the lane's stores;
+            //  - a lane whose samples end in the group (the chains of a wave release different
+            //    squelch-block counts, so their ends differ by up to a squelch block): its state
+            //    is held past its m samples and only its complete bytes are stored.
+            // With both on the per-sample path, chains created a few blocks apart encoded 2.2x
+            // slower than chains created together (tools/dbg/adpcm_phase.py).
+            const int m = sl.active ? min(max(n - i0, 0), kAdG) : 0;  // the lane's samples here
+            const int fb = kmod == 0 ? 0 : kmod > kAdpcmSyncPeriod - kAdG / 2 ? kAdpcmSyncPeriod - kmod : -1;
+            const int sf = fb >= 0 ? 2 * fb + pend : kAdG;
+            const bool framed = sf < m;
+            const bool any_part = __any(sl.active && m < kAdG);
+            const bool any_frame = __any(framed);
+            uint32_t w[kAdGQ];  // the codes ^ 7 (adpcm_encode_rem), fixed below
+            uint32_t cw0 = 0;   // the state before sample sf
+            int cpred = 0;
+            auto encode_group = [&](auto capture, auto hold) {
+                constexpr bool kCap = decltype(capture)::value, kHold = decltype(hold)::value;
+                int rem = m;  // kHold: samples left to the lane's end (opaque per step: the 64
+                              // compares against m hoisted were 128 SGPRs)
 #pragma unroll
                 for (int k = 0; k < kAdGQ; ++k) {
                     const uint32_t wv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -1319,21 +1325,52 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
 #pragma unroll
                     for (int t = 0; t < 8; ++t) {
                         const int x = (int)(int16_t)(wv[t >> 1] >> (16 * (t & 1)));
-                        acc = __builtin_amdgcn_alignbit(adpcm_encode_rem(ad, x, NS), acc, 4);
+                        if constexpr (kCap) {
+                            const bool hit = 8 * k + t == sf;
+                            cw0 = hit ? ad.w0 : cw0;
+                            cpred = hit ? ad.pred : cpred;
+                        }
+                        if constexpr (kHold) {
+                            asm volatile("" : "+v"(rem));
+                            const AdpcmRem keep = ad;
+                            acc = __builtin_amdgcn_alignbit(adpcm_encode_rem(ad, x, NS), acc, 4);
+                            if (rem <= 0) ad = keep;  // past the lane's end: the state holds
+                            --rem;
+                        } else {
+                            acc = __builtin_amdgcn_alignbit(adpcm_encode_rem(ad, x, NS), acc, 4);
+                        }
                     }
                     w[k] = acc ^ 0x77777777u;
                 }
-                if (pend) {  // bytes start at odd samples: shift the nibble stream by one
-                    uint32_t prev = (uint32_t)left;
+            };
+            if (any_part) {
+                if (any_frame) encode_group(std::true_type{}, std::true_type{});
+                else encode_group(std::false_type{}, std::true_type{});
+            } else {
+                if (any_frame) encode_group(std::true_type{}, std::false_type{});
+                else encode_group(std::false_type{}, std::false_type{});
+            }
+            uint32_t prev = (uint32_t)left;
+            if (pend) {  // bytes start at odd samples: shift the nibble stream by one
 #pragma unroll
-                    for (int k = 0; k < kAdGQ; ++k) {
-                        const uint32_t wk = w[k];
-                        w[k] = (wk << 4) | prev;
-                        prev = wk >> 28;
-                    }
-                    left = (int)prev;
+                for (int k = 0; k < kAdGQ; ++k) {
+                    const uint32_t wk = w[k];
+                    w[k] = (wk << 4) | prev;
+                    prev = wk >> 28;
                 }
-                if (sl.active) {
+            }
+            // the lane's complete bytes: nibble 0 the pending start's code (pend), then its m codes
+            const int nb = (pend + m) >> 1;
+            if (m == kAdG) {
+                if (pend) left = (int)prev;
+            } else if (any_part && m > 0 && ((pend + m) & 1)) {
+                uint32_t wn = w[0];  // w[nb >> 2] (a select chain: no indexed registers)
+#pragma unroll
+                for (int k = 1; k < kAdGQ; ++k) wn = (nb >> 2) == k ? w[k] : wn;
+                left = (int)((wn >> (8 * (nb & 3))) & 15u);  // the start left open
+            }
+            if (m > 0) {
+                if (m == kAdG && !framed) {
 #pragma unroll
                     for (int q = 0; q < kAdGQ / 4; ++q) {
                         auto* d = reinterpret_cast<__attribute__((address_space(1))) U128Unaligned*>(&out.p[ob + 16 * q]);
@@ -1342,36 +1379,33 @@ chain_adpcm(const ChainPost* __restrict__ posts, ChainCounts* __restrict__ count
                         d->z = w[4 * q + 2];
                         d->w = w[4 * q + 3];
                     }
+                } else if ((any_part || any_frame) && ob + nb + (framed ? 8 : 0) <= cap) {
+                    // bytes [0, nb), the 8-B frame before byte pf when framed (the pending byte's
+                    // completion comes first when pend): whole words in place or 8 bytes on, a
+                    // word that pf or nb splits byte by byte
+                    const int pf = framed ? fb + pend : kAdG;
+                    auto st32 = [&](int off, uint32_t val) {
+                        *reinterpret_cast<__attribute__((address_space(1))) u32_unaligned*>(&out.p[off]) = val;
+                    };
+#pragma unroll
+                    for (int k = 0; k < kAdGQ; ++k) {
+                        const int lo = 4 * k;
+                        if (lo + 4 <= nb && (lo + 4 <= pf || lo >= pf)) {
+                            st32(ob + lo + (lo >= pf ? 8 : 0), w[k]);
+                        } else if (lo < nb) {
+                            for (int b = 0; b < 4; ++b)
+                                if (lo + b < nb) out[ob + lo + b + (lo + b >= pf ? 8 : 0)] = (uint8_t)(w[k] >> (8 * b));
+                        }
+                    }
+                    if (framed) {
+                        st32(ob + pf, 0x434E5953u);  // "SYNC"
+                        st32(ob + pf + 4, (uint32_t)(uint16_t)(cw0 >> 17) | ((uint32_t)(uint16_t)cpred << 16));
+                    }
                 }
-                ob += kAdG / 2;
-                kmod += kAdG / 2;
+                ob += nb + (framed ? 8 : 0);
+                kmod += pend ? m >> 1 : (m + 1) >> 1;  // the starts among its m samples
                 if (kmod >= kAdpcmSyncPeriod) kmod -= kAdpcmSyncPeriod;
-                continue;
             }
-            // checked path: per sample (read back from the ring), lanes past their end keep
-            // their state
-            const uint32_t* gw = reinterpret_cast<const uint32_t*>(&rg[kAdGQ * g][0]);
-            int nib = left;
-#pragma unroll 1
-            for (int t = 0; t < kAdG; ++t) {
-                if (!sl.active || i0 + t >= n) break;
-                // quad t >> 3 of the group, word (t & 7) >> 1 of this lane's 16 B
-                const uint32_t word = gw[(t >> 3) * 256 + lane * 4 + ((t & 7) >> 1)];
-                const int x = (int)(int16_t)(word >> (16 * (t & 1)));
-                const bool start = (t & 1) == pend;
-                if (start) {
-                    if (kmod == 0) frame();
-                    if (++kmod == kAdpcmSyncPeriod) kmod = 0;
-                }
-                const int code = (int)((adpcm_encode_rem(ad, x, NS) & 15u) ^ 7u);
-                if (start) {
-                    nib = code;
-                } else {
-                    if (ob < cap) out[ob] = (uint8_t)(nib | (code << 4));
-                    ob++;
-                }
-            }
-            left = nib;
         }
         __syncthreads();  // chunk ch + 1 staged; slot ch & 1 free for chunk ch + 2
     }

@@ -974,6 +974,46 @@ def test_adpcm_chains_many_lanes_ragged_blocks(amd):
     eng.close()
 
 
+def test_adpcm_chains_staggered_sync_frames(amd):
+    """Clients join a live server at different blocks, so the AdpcmEncoder byte counters -- and
+    the places of the SYNC frames -- differ between the lanes of one chain_adpcm wave (frames on
+    the encoder's group path, round 6): 70 chains created in seven batches, ragged blocks pushed
+    between the batches; every chain's bytes equal the oracle's encoding of its own AGC output,
+    and the batches' frame phases do differ."""
+    from openwebrx_amd import synth
+    fs, block = 2400000, 1 << 17
+    modes = [("nfm", "am", "usb", "cw", "lsb")[c % 5] for c in range(70)]
+    iq, offs = synth.make_iq(fs, 6 << 20, modes)
+    plist = [amd.params.chain_params(fs, o, m, output=amd._lib.OUT_ADPCM)
+             for o, m in zip(offs, modes)]
+    eng = amd.Engine(fs, max_block=block)
+    eng.set_debug(True)
+    sizes = [block, block // 3 + 17, block // 2 + 1]
+    chains, i, k = [], 0, 0
+
+    def push():
+        nonlocal i, k
+        s = sizes[k % 3]
+        eng.push(iq[i:i + s])
+        i += s
+        k += 1
+    for b in range(7):
+        chains += [eng.chain(p) for p in plist[10 * b:10 * (b + 1)]]
+        for _ in range(1 + b % 3):
+            push()
+    while i < iq.size:
+        push()
+    eng.sync()
+    starts = set()
+    for c, ch in enumerate(chains):
+        data = ch.read_audio()
+        ref = oracle.adpcm_encode(oracle.convert_s16(ch.read_debug(5)), 1)
+        assert len(data) > 10000 and data == ref[:len(data)] and len(ref) - len(data) <= 9, c
+        starts.add(len(data) % 1009)  # byte counters of the batches at the end of the stream
+    eng.close()
+    assert len(starts) >= 5  # the batches' frame phases differ
+
+
 @pytest.mark.parametrize("rates", [(48000, 12000), (12000, 48000), (24000, 12000)])
 def test_audio_resampler_module(amd, rates):
     """AudioResampler(inputRate, clientRate) (csdr/chain/clientaudio.py:15-16), the standalone
