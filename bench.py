@@ -1223,6 +1223,7 @@ def main():
                               else achieved_tf / FP32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
                 "mac_form": mac_name,
+                "frame_length_M": int(s1.get("ddc_frame_length", 0)) if fast else None,
                 "k_slices": mac_kslices,
                 "algorithmic_bytes_per_launch": round(mac_bytes_launch) if mac_bytes_launch else None,
                 "algorithmic_flop_per_launch": round(mac_flop_launch) if mac_flop_launch else None,

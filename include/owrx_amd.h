@@ -350,6 +350,7 @@ typedef struct {
      * chains' rings */
     double  host_ms_drain_wait;
     double  host_ms_drain_copy;
+    int64_t ddc_frame_length;  /* the fast DDC's frame length M of the newest chain group */
 } owrx_stats;
 int owrx_get_stats(owrx_engine* e, owrx_stats* s);
 /* n > 0 => record HIP events around each kernel group on the engine's streams in every n-th

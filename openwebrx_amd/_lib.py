@@ -117,6 +117,7 @@ class Stats(ctypes.Structure):
         ("waterfall_timed_launches", ctypes.c_int64),
         ("host_ms_drain_wait", ctypes.c_double),
         ("host_ms_drain_copy", ctypes.c_double),
+        ("ddc_frame_length", ctypes.c_int64),
     ]
 
 

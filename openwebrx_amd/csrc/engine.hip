@@ -1600,19 +1600,29 @@ static int group_refresh_device(owrx_engine* e, ChainGroup* g) {
 // the least modelled time per block and chain, max(f32 MFMA time of the padded frame tiles, HBM
 // time of the W reads), ties to the longer frame (fewer frames: less U / Y traffic).  0 when
 // the branch filters are too long for these frames (the group then runs the direct form).
+//
+// The frame length is chosen for the caller's block, so a grouped engine (owrx_set_block_group)
+// keeps the ungrouped design and its outputs byte for byte.  C3 in fours would model faster at
+// M = 192 (32 frames, no tile padding, against 52 frames of M = 128 padded to 64): fc_mac rose
+// to 0.45-0.50 of the MFMA peak, but the job ran 2.5 % slower over eleven interleaved pairs of
+// runs (stream C, the bound, slower with the GEMM's power drawn in a shorter time is the likely
+// reading; profiles/r06_fc_m_ab.txt), so it is not the default (OWRX_FC_M=192 for the A/B).
+static double fc_model_t(int M, int Dp, int P, int64_t nk_max) {
+    const int V = M - P + 1;
+    const int64_t F = (nk_max + V - 1) / V;
+    const int64_t ft = F > 16 ? 32 : 16;
+    const int64_t Fp = (F + ft - 1) / ft * ft;
+    const double flop = 8.0 * M * Dp * Fp;
+    const double wbytes = 8.0 * M * Dp * (Fp / ft);
+    return std::max(flop / 150e12, wbytes / 5e12);
+}
 static int fc_choose_m(int D, int P, int64_t nk_max) {
     const int Dp = (D + 95) / 96 * 96;
     int best = 0;
     double best_t = 0;
     for (int M : {384, 256, 192, 128, 64}) {
-        const int V = M - P + 1;
-        if (V < M / 2) continue;
-        const int64_t F = (nk_max + V - 1) / V;
-        const int64_t ft = F > 16 ? 32 : 16;
-        const int64_t Fp = (F + ft - 1) / ft * ft;
-        const double flop = 8.0 * M * Dp * Fp;
-        const double wbytes = 8.0 * M * Dp * (Fp / ft);
-        const double t = std::max(flop / 150e12, wbytes / 5e12);
+        if (M - P + 1 < M / 2) continue;
+        const double t = fc_model_t(M, Dp, P, nk_max);
         if (!best || t < best_t * 0.999) {
             best = M;
             best_t = t;
@@ -3303,6 +3313,7 @@ int owrx_chain_create(owrx_engine* e, const owrx_chain_params* p, int* handle) {
             const int m = atoi(v);
             if (ng->fc_M && fc_frame_supported(m) && m - ng->fc_P + 1 >= m / 2) ng->fc_M = m;
         }
+        e->stats.ddc_frame_length = ng->fc_M;
         if (ng->fc_M) {
             const int M = ng->fc_M;
             ng->fc_V = M - ng->fc_P + 1;

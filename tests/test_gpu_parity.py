@@ -545,10 +545,11 @@ def test_input_retention_same_outputs(amd):
     (2400000, ["nfm", "usb", "am", "cw"] * 3, 1 << 17),
     (10000000, ["nfm", "usb", "cw"] * 4, 1 << 18),  # C3's design: D = 833, fast convolution
 ])
-def test_block_pairing_same_outputs(amd, fs, modes, B, group):
+def test_block_pairing_same_outputs(amd, fs, modes, B, group, monkeypatch):
     """owrx_set_block_pairing / owrx_set_block_group: contiguous blocks run two (three, four) at a
     time (one DDC GEMM over all their frames); audio, s-meter and waterfall rows byte-identical to
-    unpaired processing.  A block count that leaves blocks held (owrx_sync runs them), a block
+    unpaired processing at the same DDC frame length (a grouped engine may pick a longer one:
+    test_block_quads_frame_length).  A block count that leaves blocks held (owrx_sync runs them), a block
     from another buffer (the held ones run alone) and a chain created mid-stream (the guard runs
     the held blocks first)."""
     import torch
@@ -588,7 +589,10 @@ def test_block_pairing_same_outputs(amd, fs, modes, B, group):
         eng.close()
         return out, st
 
-    (a, sa), (b, sb) = run(False), run(True)
+    (a, sa) = run(False)
+    monkeypatch.setenv("OWRX_FC_M", str(sa["ddc_frame_length"]))
+    (b, sb) = run(True)
+    assert sb["ddc_frame_length"] == sa["ddc_frame_length"]
     # engine blocks: the held blocks run when the group is complete, before the chain created at
     # block 5, and before the other buffer's block 6 and the block after it
     expect = {2: [(0, 1), (2, 3), (4,), (5,), (6,), (7, 8), (9, 10), (11,)],
@@ -601,7 +605,7 @@ def test_block_pairing_same_outputs(amd, fs, modes, B, group):
     assert a[2] == b[2]
 
 
-def test_block_quads_tall_gemm_tiles_same_outputs(amd):
+def test_block_quads_tall_gemm_tiles_same_outputs(amd, monkeypatch):
     """BASELINE config 3 (10 Msps, 256 NFM/USB/CW chains, 2^20-sample blocks) grouped in fours
     (owrx_set_block_group(4)): one DDC GEMM over 52 frames, which takes the 64-frame GEMM tiles
     (fc_mac_lds<4, 4, 2>) and the frame-tile-fastest decode.  Audio and s-meter byte-identical to
@@ -639,12 +643,66 @@ def test_block_quads_tall_gemm_tiles_same_outputs(amd):
         eng.close()
         return out, st
 
+    monkeypatch.setenv("OWRX_FC_M", "128")  # the default (pinned: the next test varies it)
     (a, sa), (b, sb), (c, sc) = run(1), run(4), run(2)
     assert sa["blocks"] == nb and sb["blocks"] == 1 and sc["blocks"] == 2
+    assert sa["ddc_frame_length"] == sb["ddc_frame_length"] == sc["ddc_frame_length"] == 128
     assert all(len(x) > 0 for x in a[0])
     for i in range(len(plist)):
         assert a[0][i] == b[0][i] and a[1][i] == b[1][i], i
         assert a[0][i] == c[0][i] and a[1][i] == c[1][i], i
+
+
+def test_block_quads_frame_length(amd, monkeypatch):
+    """BASELINE config 3 in fours at the other DDC frame length the A/B tried (OWRX_FC_M=192: 32
+    frames per grouped GEMM, no tile padding) against one block at a time at the default 128.
+    The two frame lengths round the DDC differently (~1e-7), so the chains' int16 audio agrees to
+    1 LSB on 99.9 % and their s-meter values to 1e-4 (relative), not byte for byte (at one frame
+    length they are: the test above)."""
+    import numpy as np
+    import torch
+    from openwebrx_amd import _lib, synth
+    fs, B, nb = 10000000, 1 << 20, 4
+    modes = (["nfm", "usb", "cw"] * 86)[:256]
+    offs = synth.carrier_offsets(fs, len(modes))
+    plist = [amd.params.chain_params(fs, o, m, output=_lib.OUT_S16) for o, m in zip(offs, modes)]
+    code = {"nfm": 0, "usb": 2, "cw": 3}
+
+    def run(group):
+        eng = amd.Engine(fs, max_block=B)
+        eng.set_input_retention(8)
+        if group > 1:
+            eng.set_block_group(group)
+        chains = [eng.chain(p) for p in plist]
+        h = eng.history
+        buf = torch.zeros(h + nb * B, dtype=torch.complex64, device="cuda")
+        o64 = np.asarray(offs, np.float64)
+        mds = np.asarray([code[m] for m in modes], np.int32)
+        _lib.check(_lib.lib.owrx_synth_iq(0, buf.data_ptr() + 8 * h, nb * B, 0, float(fs), len(mds),
+                                          o64.ctypes.data, mds.ctypes.data, 20251114, 0.01, 0.05),
+                   "owrx_synth_iq")
+        torch.cuda.synchronize()
+        for k in range(nb):
+            eng.process_device(buf.data_ptr() + 8 * (h + k * B), B)
+        eng.sync()
+        st = eng.stats()
+        out = ([np.frombuffer(c.read_audio(), np.int16) for c in chains], [c.read_smeter() for c in chains])
+        eng.close()
+        return out, st
+
+    (a, sa) = run(1)
+    monkeypatch.setenv("OWRX_FC_M", "192")
+    (b, sb) = run(4)
+    assert sa["ddc_frame_length"] == 128 and sb["ddc_frame_length"] == 192
+    close = total = 0
+    for i in range(len(plist)):
+        x, y = a[0][i].astype(np.int32), b[0][i].astype(np.int32)
+        assert x.size == y.size > 0, i
+        close += int(np.sum(np.abs(x - y) <= 1))
+        total += x.size
+        assert a[1][i].size == b[1][i].size > 0, i
+        assert np.allclose(a[1][i], b[1][i], rtol=1e-4, atol=1e-12), i
+    assert close / total >= 0.999, close / total
 
 
 def test_retention_floor_while_paired(amd):
