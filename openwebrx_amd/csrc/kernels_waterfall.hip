@@ -649,6 +649,14 @@ OWRX_DEV int wf_swz32(int e) { return e ^ ((e >> 5) & 15); }
 // fma(y, y, x x)), so a group summed in a workgroup's registers and the same group's frames
 // folded in order by wf_finalize from their own partial rows give the same bits: the split
 // changes no result, only how finely the last round of work is dealt.
+//
+// FUS (N = 16384 << qlog without the split's scratch): item w = (group << qlog) + j reads its
+// group's frames from the stream itself and forms sub-frame j on load, y_j[n] = W_N^(nj) sum_q
+// w[n + 16384 q] x[n + 16384 q] W_Q^(qj) with the split kernel's operations in its order (rows
+// bit-identical to the split path); the Q workgroups of a frame group read it through L2 / the
+// Infinity Cache instead of the split writing and re-reading 2 x 8 N bytes per frame.  No
+// next-frame prefetch (the Q quarters do not fit the registers): the frame's loads go in chunks.
+template <bool FUS>
 __global__ void __launch_bounds__(WfL32::NT)
 wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
            const float* __restrict__ window, const float2* __restrict__ tw,
@@ -679,14 +687,14 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         const int gi = w >> qlog;
         const WfGroup g = groups[gi];
         const int64_t g0 = __builtin_amdgcn_readfirstlane(
-            qlog ? (int)((((int64_t)gi * fstride << qlog) + (w & ((1 << qlog) - 1))) * N)
-                 : (int)(g.start - blk_start));
+            qlog && !FUS ? (int)((((int64_t)gi * fstride << qlog) + (w & ((1 << qlog) - 1))) * N)
+                         : (int)(g.start - blk_start));
         Item it;
-        it.hop = __builtin_amdgcn_readfirstlane(qlog ? N << qlog : g.hop);
+        it.hop = __builtin_amdgcn_readfirstlane(qlog && !FUS ? N << qlog : g.hop);
         it.nfr = __builtin_amdgcn_readfirstlane(g.nframes);
         it.xr = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float2*>(blk + g0), 0,
-            (int)(sizeof(float2) * ((int64_t)(it.nfr - 1) * it.hop + N)), 0x00020000);
+            (int)(sizeof(float2) * ((int64_t)(it.nfr - 1) * it.hop + (FUS ? N << qlog : N))), 0x00020000);
         return it;
     };
     const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
@@ -708,6 +716,63 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
 #pragma unroll
         for (int r = 0; r < 32; ++r)
             v[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, t0 * 4, r * NT * 4, 0));
+    };
+    // FUS: the frame at byte offset fo of xr as sub-frame j (the split's y_j), in chunks of
+    // kFusPts points: every quarter's samples, window taps and the point's twiddle in flight
+    // together
+    constexpr int kFusPts = 2;
+    // (tt: the thread index made opaque per frame, so the frame-invariant window and twiddle
+    // loads are not hoisted out of the frame loop: 64 + 128 values held across it spilled)
+    auto fused_frame = [&](__amdgpu_buffer_rsrc_t xr, int fo, int j, int tt, float2* a) {
+#pragma clang fp contract(off)  // the split kernel's roundings exactly (it is uncontracted too)
+        const int NQ = N << qlog;
+        const auto wq = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(window), 0,
+                                                          (int)(sizeof(float) * NQ), 0x00020000);
+        // (the twiddles through a buffer resource too: 32-bit offsets; per-lane 64-bit addresses
+        // for every point were the kernel's spills)
+        const auto tq = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(tw), 0,
+                                                          (int)(sizeof(float2) * NQ), 0x00020000);
+        // unrolled (a[] keeps constant indices: registers), a scheduling barrier per chunk (with
+        // 8-point chunks and no barrier the kernel spilled 186 registers)
+#pragma unroll
+        for (int c = 0; c < 32 / kFusPts; ++c) {
+            __builtin_amdgcn_sched_barrier(0);
+            float2 v[4][kFusPts];
+            float wv8[4][kFusPts];
+            float2 tj[kFusPts];
+#pragma unroll
+            for (int u = 0; u < kFusPts; ++u) {
+                const int n = tt + NT * (kFusPts * c + u);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= (1 << qlog)) break;
+                    const int vo = (n + N * q) * 8 + fo;
+                    v[q][u] = make_float2(
+                        __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo, 0, 0)),
+                        __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, vo + 4, 0, 0)));
+                    wv8[q][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wq, (n + N * q) * 4, 0, 0));
+                }
+                const int to = ((n * j) & (NQ - 1)) * 8;
+                tj[u] = make_float2(__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(tq, to, 0, 0)),
+                                    __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(tq, to + 4, 0, 0)));
+            }
+#pragma unroll
+            for (int u = 0; u < kFusPts; ++u) {
+                float2 vq[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q < (1 << qlog)) vq[q] = make_float2(v[q][u].x * wv8[q][u], v[q][u].y * wv8[q][u]);
+                float2 y;
+                if (qlog == 1) {
+                    y = j ? f2sub(vq[0], vq[1]) : f2add(vq[0], vq[1]);
+                } else {  // the split's DFT4 over q, output j
+                    const float2 e0 = f2add(vq[0], vq[2]), e1 = f2sub(vq[0], vq[2]);
+                    const float2 e2 = f2add(vq[1], vq[3]), d = f2mi(f2sub(vq[1], vq[3]));
+                    y = j == 0 ? f2add(e0, e2) : j == 2 ? f2sub(e0, e2) : j == 1 ? f2add(e1, d) : f2sub(e1, d);
+                }
+                a[kFusPts * c + u] = j ? f2mul(y, tj[u]) : y;
+            }
+        }
     };
     // L2-resident tables first (vmcnt retires in order: the frame's HBM loads queue behind them)
     float2 tp[4];  // W_N^(2^i t), i < 4: P3's bases W_N^(r t) are products of at most four
@@ -737,8 +802,8 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     }
     w = desc(w);
     Item cur = item(w);
-    float2 nx[32];
-    load_x(cur.xr, 0, nx);
+    float2 nx[FUS ? 1 : 32];
+    if constexpr (!FUS) load_x(cur.xr, 0, nx);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
         if (t0 + NT * i < 31 * 32) sm[K::TW2 + t0 + NT * i] = t2v[i];
@@ -763,16 +828,20 @@ wf_fft_l32(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
             const int sb = 1 + 6 * f;
             if (f < 2) WF_STAMP(sb);
             float2 a[32];
-            {
-                float wv[32];
-                load_w(wv);
+            if constexpr (FUS) {
+                fused_frame(cur.xr, f * cur.hop * 8, __builtin_amdgcn_readfirstlane(w & ((1 << qlog) - 1)), t, a);
+            } else {
+                {
+                    float wv[32];
+                    load_w(wv);
 #pragma unroll
-                for (int r = 0; r < 32; ++r) a[r] = make_float2(nx[r].x * wv[r], nx[r].y * wv[r]);
+                    for (int r = 0; r < 32; ++r) a[r] = make_float2(nx[r].x * wv[r], nx[r].y * wv[r]);
+                }
+                // next frame: this item's, else the next item's first, else nothing (zeros)
+                const bool last = f + 1 == cur.nfr;
+                load_x(last ? nxt.xr : cur.xr,
+                       !last ? (f + 1) * cur.hop * 8 : has_next ? 0 : kWfOob, nx);
             }
-            // next frame: this item's, else the next item's first, else nothing (zeros)
-            const bool last = f + 1 == cur.nfr;
-            load_x(last ? nxt.xr : cur.xr,
-                   !last ? (f + 1) * cur.hop * 8 : has_next ? 0 : kWfOob, nx);
             f2dft32(a);
             if (f < 2) WF_STAMP(sb + 1);
             __syncthreads();  // the previous frame's P3 reads (and, at f = 0, the table stores)
@@ -1248,6 +1317,7 @@ __global__ void __launch_bounds__(256)
 wf_dif_split(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
              const float* __restrict__ window, const float2* __restrict__ tw, int fstride,
              float2* __restrict__ y) {
+#pragma clang fp contract(off)  // (wf_fft_l32<true> forms the same values on load: same roundings)
     constexpr int M = 16384, Q = 1 << QLOG, N = M << QLOG;
     const int n = blockIdx.x * 256 + threadIdx.x;
     const int f = blockIdx.y;
@@ -1576,23 +1646,31 @@ bool wf_uses_split(int logn) {
 static hipError_t launch_fft_l32(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw,
                                  float* partial, int* work, int cus, hipStream_t st, int qlog = 0,
-                                 int fstride = 0, int skip = 0, int tail = 0) {
+                                 int fstride = 0, int skip = 0, int tail = 0, bool fus = false) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)wf_fft_l32,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)WfL32::kLds);
-        if (e != hipSuccess) return e;
+        for (const void* k : {(const void*)wf_fft_l32<false>, (const void*)wf_fft_l32<true>}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)WfL32::kLds);
+            if (e != hipSuccess) return e;
+        }
         attr = true;
     }
+    if (fus && !qlog) return hipErrorInvalidValue;
     if (!work || skip < 0 || skip > ngroups || (qlog && (skip || tail))) return hipErrorInvalidValue;
     // items: the whole groups, then the split groups' frames (descriptors ngroups ..)
     const int whole = (ngroups - skip) << qlog;
     const int items = whole + tail;
     // one workgroup per CU (the 136 KiB image), at most one per item
     const int grid = std::max(1, std::min(items, cus));
-    hipLaunchKernelGGL(wf_fft_l32, dim3(grid), dim3(WfL32::NT), WfL32::kLds, st, blk, blk_start,
-                       groups, window, tw, partial, qlog, fstride, items, work, whole, skip);
+    if (fus)
+        hipLaunchKernelGGL(wf_fft_l32<true>, dim3(grid), dim3(WfL32::NT), WfL32::kLds, st, blk,
+                           blk_start, groups, window, tw, partial, qlog, fstride, items, work, whole,
+                           skip);
+    else
+        hipLaunchKernelGGL(wf_fft_l32<false>, dim3(grid), dim3(WfL32::NT), WfL32::kLds, st, blk,
+                           blk_start, groups, window, tw, partial, qlog, fstride, items, work, whole,
+                           skip);
     return hipGetLastError();
 }
 
@@ -1634,13 +1712,25 @@ int wf_tail_split(int logn, int ngroups, int cus, int64_t frames, int fpg) {
 }
 
 // N = 16384 << QLOG: the split into sub-frames, then wf_fft_l32 on them (window of ones: the
-// split applied the frame's window)
+// split applied the frame's window); or, OWRX_WF_FUSED=1 (A/B, read at every launch),
+// wf_fft_l32<true> forming the sub-frames on load without the scratch.  Rows bit-identical; the
+// fused form measured slower at C4 (0.068 vs 0.091-0.094 of HBM, profiles/r06_wf_fused_split_ab.txt):
+// a frame's four quarters, window taps and twiddles do not fit the registers beside the FFT's, so
+// its loads go two points at a time with their latency exposed, where the split streams them.
+bool wf_split_fused() {
+    const char* s = getenv("OWRX_WF_FUSED");
+    return s && strcmp(s, "1") == 0;
+}
 template <int QLOG>
 static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                    int ngroups, int fpg, const float* window, const float* ones,
                                    const float2* tw, float* partial, float2* scratch, int* work,
                                    int cus, hipStream_t st) {
-    if (!scratch || !ones || fpg < 1) return hipErrorInvalidValue;
+    if (fpg < 1) return hipErrorInvalidValue;
+    if (wf_split_fused())
+        return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
+                              QLOG, fpg, 0, 0, true);
+    if (!scratch || !ones) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wf_dif_split<QLOG>, dim3(16384 / 256, fpg, ngroups), dim3(256), 0, st, blk,
                        blk_start, groups, window, tw, fpg, scratch);
     return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, work, cus, st, QLOG, fpg);

@@ -837,6 +837,26 @@ def test_waterfall_kernel_variants(variant, sizes):
     assert len(errs) == sizes and all(e is not None and e < 2e-3 for e in errs.values()), errs
 
 
+@pytest.mark.parametrize("N,fs", [(32768, 20000000), (65536, 61440000)])
+def test_waterfall_fused_split_rows_bit_identical(amd, N, fs, monkeypatch):
+    """N = 32768 / 65536: wf_fft_l32<true> forms the DIF split's sub-frames on load (no scratch)
+    with the split kernel's operations in its order (OWRX_WF_FUSED=1, an A/B read at every launch),
+    so its float and ADPCM rows are bit-identical to wf_dif_split + wf_fft_l32 (the default)."""
+    from openwebrx_amd import synth
+    avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
+    avg = min(avg, 8)
+    n = hop * avg * 4 + N + 1000
+    iq, _ = synth.make_iq(fs, n, ["nfm", "am", "usb"])
+    rows = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("OWRX_WF_FUSED", fused)
+        rows[fused] = (_wf(amd, iq, fs, N, hop, avg, False, 1 << 17),
+                       _wf(amd, iq, fs, N, hop, avg, True, 1 << 18))
+    assert rows["1"][0].shape[0] >= 3 and rows["1"][0].shape == rows["0"][0].shape
+    assert np.array_equal(rows["1"][0], rows["0"][0])
+    assert rows["1"][1] == rows["0"][1] if isinstance(rows["1"][1], bytes) else np.array_equal(rows["1"][1], rows["0"][1])
+
+
 def test_wide_serial_streams_same_audio():
     """Past OWRX_WIDE_SERIAL_CHAINS chains the serial kernels move from the CU-masked streams to
     unmasked ones (engine.hip process_block); a stream whose chain count crosses the threshold
