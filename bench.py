@@ -879,7 +879,7 @@ def main():
         # sixteen frames per stream-A CU for the 16384-point kernel (two groups of 8 per
         # workgroup: its start-up and first frame amortise over the frames, 0.294 vs 0.259 of
         # HBM at 8 per CU in the micro, profiles/r05_wf_micro.txt); two per CU above it (each
-        # frame is 4 or 2 sub-frames of wf_fft_l32 after the DIF split).  The row-latency cap
+        # frame is 4 or 2 sub-frames of wf_fft_q16 after the DIF split).  The row-latency cap
         # bounds the wait at real-time rates.
         per_cu = 16 if n_fft <= 16384 else 2
         wf_batch = per_cu * max(1, cus - 16) if args.wf_batch < 0 else args.wf_batch
@@ -1099,7 +1099,8 @@ def main():
     wf_fft_ms = d["gpu_ms_waterfall_fft"]
     wf_bytes = 8.0 * d["waterfall_timed_samples"]
     wf_gbs = wf_bytes / (wf_fft_ms / 1e3) / 1e9 if wf_fft_ms > 0 else None
-    wf_kernels = (["wf_dif_split", "wf_fft_l32", "wf_finalize"] if n_fft > 16384 else
+    wf_sub = "wf_fft_l32" if os.environ.get("OWRX_WF_SUB") == "l32" else "wf_fft_q16"
+    wf_kernels = (["wf_dif_split", wf_sub, "wf_finalize"] if n_fft > 16384 else
                   ["wf_fft_q16", "wf_finalize"])
     wf_traffic, wf_traffic_src = 0, []
     for kname in wf_kernels:

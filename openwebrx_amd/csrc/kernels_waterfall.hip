@@ -992,7 +992,8 @@ template <int ABL = 0>
 __global__ void __launch_bounds__(WfQ16::NT)
 wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __restrict__ groups,
            const float* __restrict__ window, const float2* __restrict__ tw,
-           float* __restrict__ partial, int items, int* __restrict__ work, int whole, int skip) {
+           float* __restrict__ partial, int items, int* __restrict__ work, int whole, int skip,
+           int qlog, int fstride) {
     using K = WfQ16;
     WF_RSTAMP(14);
     WF_STAMP(12);
@@ -1014,12 +1015,17 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
         int hop, nfr;
     };
     auto desc = [&](int i) { return i < whole ? i : i + skip; };
+    // qlog > 0 (N = 16384 << qlog, wf_dif_split first): item w = (group << qlog) + j transforms
+    // sub-frame j of its group's frames from the split scratch (as wf_fft_l32 does), tw is the
+    // (N << qlog)-point table read at stride 1 << qlog, the window is ones
     auto item = [&](int w) {
-        const WfGroup g = groups[w];
+        const WfGroup g = groups[w >> qlog];
         Item it;
-        it.hop = __builtin_amdgcn_readfirstlane(g.hop);
+        it.hop = __builtin_amdgcn_readfirstlane(qlog ? N << qlog : g.hop);
         it.nfr = __builtin_amdgcn_readfirstlane(g.nframes);
-        const int g0 = __builtin_amdgcn_readfirstlane((int)(g.start - blk_start));
+        const int g0 = __builtin_amdgcn_readfirstlane(
+            qlog ? (int)(((((int64_t)(w >> qlog) * fstride) << qlog) + (w & ((1 << qlog) - 1))) * N)
+                 : (int)(g.start - blk_start));
         it.xr = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float2*>(blk + g0), 0,
             (int)(sizeof(float2) * ((int64_t)(it.nfr - 1) * it.hop + N)), 0x00020000);
@@ -1047,16 +1053,16 @@ wf_fft_q16(const float2* __restrict__ blk, int64_t blk_start, const WfGroup* __r
     float wv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) wv[r] = window[n1 + NT * r];
-    const float2 t2v = tw[((t0 & 63) * (t0 >> 6) * 16) & (N - 1)];          // [k1b][n1a]
-    const float2 t3v = tw[((t0 & 3) * ((t0 >> 2) & 15) * 256) & (N - 1)];   // [c][q], t0 < 64
-    const float2 tav = tw[((t0 & 63) * (t0 >> 6)) & (N - 1)];               // [k2][n1a]
-    const float2 tbv = tw[((t0 & 15) * ((t0 >> 4) & 15) * 64) & (N - 1)];   // [k2][n1b], t0 < 256
+    const float2 t2v = tw[(((t0 & 63) * (t0 >> 6) * 16) & (N - 1)) << qlog];          // [k1b][n1a]
+    const float2 t3v = tw[(((t0 & 3) * ((t0 >> 2) & 15) * 256) & (N - 1)) << qlog];   // [c][q], t0 < 64
+    const float2 tav = tw[(((t0 & 63) * (t0 >> 6)) & (N - 1)) << qlog];               // [k2][n1a]
+    const float2 tbv = tw[(((t0 & 15) * ((t0 >> 4) & 15) * 64) & (N - 1)) << qlog];   // [k2][n1b], t0 < 256
     // kTbS: n1b = t >> 6 is the wave's index, so W_256^(n1b k2) is uniform over the wave
     float2 tbs[16];
     if constexpr (kTbS && !kW16) {
         const int wv6 = __builtin_amdgcn_readfirstlane(t0 >> 6);
 #pragma unroll
-        for (int r = 1; r < 16; ++r) tbs[r] = tw[(64 * r * wv6) & (N - 1)];
+        for (int r = 1; r < 16; ++r) tbs[r] = tw[((64 * r * wv6) & (N - 1)) << qlog];
     }
     auto finish = [&]() {
         __syncthreads();
@@ -1711,6 +1717,10 @@ int wf_tail_split(int logn, int ngroups, int cus, int64_t frames, int fpg) {
     return std::min(s, ngroups);
 }
 
+static hipError_t launch_fft_q16(const float2* blk, int64_t blk_start, const WfGroup* groups,
+                                 int ngroups, const float* window, const float2* tw,
+                                 float* partial, int* work, int cus, hipStream_t st, int skip,
+                                 int tail, int qlog, int fstride);
 // N = 16384 << QLOG: the split into sub-frames, then wf_fft_l32 on them (window of ones: the
 // split applied the frame's window); or, OWRX_WF_FUSED=1 (A/B, read at every launch),
 // wf_fft_l32<true> forming the sub-frames on load without the scratch.  Rows bit-identical; the
@@ -1731,8 +1741,16 @@ static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const W
         return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
                               QLOG, fpg, 0, 0, true);
     if (!scratch || !ones) return hipErrorInvalidValue;
+    // the sub-frames on wf_fft_q16 (its qlog form), or wf_fft_l32 with OWRX_WF_SUB=l32 (A/B):
+    // C4 0.0965-0.0968 vs 0.0928-0.0935 of HBM (profiles/r06_wf_sub_q16_ab.txt)
+    // (read at every launch, as OWRX_WF_FUSED: the fused form's rows test compares against l32)
+    const char* sv = getenv("OWRX_WF_SUB");
+    const bool sub_q16 = !(sv && strcmp(sv, "l32") == 0);
     hipLaunchKernelGGL(wf_dif_split<QLOG>, dim3(16384 / 256, fpg, ngroups), dim3(256), 0, st, blk,
                        blk_start, groups, window, tw, fpg, scratch);
+    if (sub_q16)
+        return launch_fft_q16(scratch, 0, groups, ngroups, ones, tw, partial, work, cus, st, 0, 0,
+                              QLOG, fpg);
     return launch_fft_l32(scratch, 0, groups, ngroups, ones, tw, partial, work, cus, st, QLOG, fpg);
 }
 
@@ -1740,7 +1758,7 @@ static hipError_t launch_fft_split(const float2* blk, int64_t blk_start, const W
 static hipError_t launch_fft_q16(const float2* blk, int64_t blk_start, const WfGroup* groups,
                                  int ngroups, const float* window, const float2* tw,
                                  float* partial, int* work, int cus, hipStream_t st, int skip,
-                                 int tail) {
+                                 int tail, int qlog, int fstride) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)wf_fft_q16<kWfQ16>,
@@ -1749,13 +1767,15 @@ static hipError_t launch_fft_q16(const float2* blk, int64_t blk_start, const WfG
         if (e != hipSuccess) return e;
         attr = true;
     }
-    if (!work || skip < 0 || skip > ngroups || tail < 0) return hipErrorInvalidValue;
-    const int whole = ngroups - skip;
+    if (!work || skip < 0 || skip > ngroups || tail < 0 || (qlog && (skip || tail)))
+        return hipErrorInvalidValue;
+    const int whole = (ngroups - skip) << qlog;
     const int items = whole + tail;
     // one 1024-thread workgroup per CU (the 147 KiB LDS image), at most one per item
     const int grid = std::max(1, std::min(items, cus));
     hipLaunchKernelGGL(wf_fft_q16<kWfQ16>, dim3(grid), dim3(WfQ16::NT), WfQ16::kLds, st, blk,
-                       blk_start, groups, window, tw, partial, items, work, whole, skip);
+                       blk_start, groups, window, tw, partial, items, work, whole, skip, qlog,
+                       fstride);
     return hipGetLastError();
 }
 
@@ -1766,7 +1786,7 @@ static hipError_t launch_fft_sel(const float2* blk, int64_t blk_start, const WfG
     if constexpr (LOGN == 14) {
         if (wf_n16k_kernel() == 0)
             return launch_fft_q16(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
-                                  skip, tail);
+                                  skip, tail, 0, 0);
         if (!wf_force_r16())
             return launch_fft_l32(blk, blk_start, groups, ngroups, window, tw, partial, work, cus, st,
                                   0, 0, skip, tail);

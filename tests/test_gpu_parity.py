@@ -841,13 +841,15 @@ def test_waterfall_kernel_variants(variant, sizes):
 def test_waterfall_fused_split_rows_bit_identical(amd, N, fs, monkeypatch):
     """N = 32768 / 65536: wf_fft_l32<true> forms the DIF split's sub-frames on load (no scratch)
     with the split kernel's operations in its order (OWRX_WF_FUSED=1, an A/B read at every launch),
-    so its float and ADPCM rows are bit-identical to wf_dif_split + wf_fft_l32 (the default)."""
+    so its float and ADPCM rows are bit-identical to wf_dif_split + wf_fft_l32 (OWRX_WF_SUB=l32;
+    the default transforms the sub-frames with wf_fft_q16)."""
     from openwebrx_amd import synth
     avg, hop = amd.params.fft_parameters(fs, N, 9, 0.3)
     avg = min(avg, 8)
     n = hop * avg * 4 + N + 1000
     iq, _ = synth.make_iq(fs, n, ["nfm", "am", "usb"])
     rows = {}
+    monkeypatch.setenv("OWRX_WF_SUB", "l32")
     for fused in ("1", "0"):
         monkeypatch.setenv("OWRX_WF_FUSED", fused)
         rows[fused] = (_wf(amd, iq, fs, N, hop, avg, False, 1 << 17),

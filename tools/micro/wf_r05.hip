@@ -266,7 +266,7 @@ int main(int argc, char** argv) {
                     case 104: k = wf_fft_q16<104>; break;
                 }
                 hipLaunchKernelGGL(k, dim3(std::min(items, cus)), dim3(WfQ16::NT), WfQ16::kLds, s_a, dx,
-                                   (int64_t)0, dg, dwin, dtw, dpart, items, dwork, G - skip, skip);
+                                   (int64_t)0, dg, dwin, dtw, dpart, items, dwork, G - skip, skip, 0, 0);
             };
             std::vector<V> vs = {
                 {"l32", [&] { l32(0, 0); }, 1},

@@ -133,7 +133,7 @@ int main(int argc, char** argv) {
     if (abl == v) k = wf_fft_q16<v>;
             Q16_VARIANTS(CASEQ)
             hipLaunchKernelGGL(k, dim3(std::min(G, cus)), dim3(WfQ16::NT), WfQ16::kLds, s_a, dx, (int64_t)0, dg,
-                               dwin, dtw, dpart, G, dwork, G, 0);
+                               dwin, dtw, dpart, G, dwork, G, 0, 0, 0);
         };
         for (int abl : {72, 328, 584, 840, 79, 335, 591, 847}) {
             const double us = time_us([&] { q16(abl); }, s_a);
